@@ -1,0 +1,276 @@
+#!/usr/bin/env python3
+"""Benchmark: beam-cell updates/s + frontier-extract ms (BASELINE.json metric).
+
+Workload (per GPU): BASELINE config C3 — a 16384 x 16384 grid at 5 cm,
+64 robots random-walking in a seeded synthetic world, 64-scan x 4096-beam
+LD06-format batches.  One step = integrate one 64-scan batch (inputs already
+resident in HBM, dm_integrate_device) + full frontier extraction
+(mask + CCL + clusters, clusters copied to the host, dm_frontiers).
+
+N GPUs (weak scaling): rank r owns a 16384-row band of a 16384 x 16384*N map
+with its own 64 robots; frontiers are merged across bands with RCCL
+(halo rows, edge labels, cluster all-gather; dm/sharded.py).
+
+Prints ONE JSON line on rank 0.  See DESIGN.md §5 for every field.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "distributed-autonomous-exploration-and-mapping_amd")
+sys.path[:0] = [PKG]
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md §Chip-level parameters
+TILE_APPLY_BYTES_PER_UPDATE = 8.0   # one 4 B counter RMW per update
+TILE_APPLY_BYTES_PER_TOUCHED = 25.0  # read h,m,L; write L, state; zero h,m
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--grid", type=int, default=16384, help="cells per side of each GPU's band")
+    ap.add_argument("--robots", type=int, default=64)
+    ap.add_argument("--beams", type=int, default=4096)
+    ap.add_argument("--pool", type=int, default=6, help="distinct pre-generated batches")
+    ap.add_argument("--profile-steps", type=int, default=10)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0,
+                    help="budget for the CPU-oracle baseline sample (0 disables)")
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != args.gpus:
+        if world_size == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    torch.cuda.set_device(local_rank)
+    if world_size > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import dm
+    from dm import synth
+    from dm.sharded import ShardedMapper
+
+    G, res = args.grid, 0.05
+    H_total = G * world_size
+    half_w = G * res / 2.0
+    oy_global = -H_total * res / 2.0
+    # this rank's band of the world, in metres
+    y0 = oy_global + rank * G * res
+    y1 = y0 + G * res
+    world = synth.make_world(args.seed * 1000 + rank, -half_w, y0, half_w, y1)
+    margin = float(12.5) if world_size > 1 else 1.0  # scans stay inside the band
+    stream = synth.ScanStream(world, args.robots, args.beams, args.seed * 1000 + 500 + rank,
+                              region=(-half_w + 1.0, y0 + margin, half_w - 1.0, y1 - margin))
+    t_gen = time.perf_counter()
+    pool = [stream.next_batch() for _ in range(args.pool)]
+    t_gen = time.perf_counter() - t_gen
+    amin = float(synth.LD06_ANGLE_MIN)
+    inc = float(synth.ld06_angle_increment(args.beams))
+    dev = torch.device("cuda", local_rank)
+    dpool = [(torch.from_numpy(synth.pose4(p)).to(dev), torch.from_numpy(r).to(dev)) for p, r in pool]
+
+    params = dm.default_params(G, H_total, resolution=res)
+    params.origin_x = -half_w
+    params.origin_y = oy_global
+    mapper = ShardedMapper(params, rank=rank, world_size=world_size, device=local_rank,
+                           group=dist.group.WORLD if world_size > 1 else None)
+    band = mapper.band
+    S, N = args.robots, args.beams
+
+    def integrate(k):
+        pose4, rng = dpool[k % len(dpool)]
+        band.integrate_device(pose4.data_ptr(), S, rng.data_ptr(), N, amin, inc)
+
+    # per-batch U and T are properties of the batch (not of the map state):
+    # measure them once, untimed
+    counts = []
+    for k in range(len(dpool)):
+        integrate(k)
+        counts.append(band.last_counts())
+    band.reset()
+
+    def step(k):
+        integrate(k)
+        return mapper.frontiers()
+
+    for k in range(args.warmup):
+        step(k)
+
+    def barrier():
+        if world_size > 1:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n_clusters = 0
+    for k in range(args.steps):
+        fr = step(args.warmup + k)
+        n_clusters = len(fr)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world_size > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    U_rank = sum(counts[(args.warmup + k) % len(counts)][0] for k in range(args.steps))
+    U_all = U_rank
+    if world_size > 1:
+        t = torch.tensor([U_rank], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        U_all = int(t.item())
+
+    # integrate-only and frontier-only timings (untimed w.r.t. `value`)
+    reps = max(3, min(args.steps, 20))
+    ti = []
+    for k in range(reps):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        integrate(k)
+        band.synchronize()
+        ti.append(time.perf_counter() - a)
+    tf = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        fr = mapper.frontiers()
+        tf.append(time.perf_counter() - a)
+    t_int = float(np.median(ti))
+    t_fr = float(np.median(tf))
+    U_mean = float(np.mean([c[0] for c in counts]))
+    T_mean = float(np.mean([c[1] for c in counts]))
+
+    # live per-kernel timing with HIP events on the library's stream
+    band.profile(True)
+    band.profile_reset()
+    for k in range(args.profile_steps):
+        step(k)
+    kstats = band.profile_read()
+    band.profile(False)
+    avg = {name: tot / max(1, n) for name, (n, tot) in kstats.items()}
+    dominant = max(kstats, key=lambda n: kstats[n][1]) if kstats else None
+    t_apply_ms = avg.get("tile_apply", float("nan"))
+    bytes_apply = TILE_APPLY_BYTES_PER_UPDATE * U_mean + TILE_APPLY_BYTES_PER_TOUCHED * T_mean
+    achieved = bytes_apply / (t_apply_ms * 1e-3) / 1e9 if t_apply_ms > 0 else None
+
+    result = None
+    if rank == 0:
+        cpu = None
+        if world_size == 1 and args.cpu_seconds > 0:
+            cpu = cpu_baseline(params, pool, amin, inc, args.cpu_seconds)
+        fr_clusters = int(len(fr))
+        result = {
+            "metric": "beam-cell updates/sec + frontier-extract ms on 16384² grid",
+            "value": U_all / elapsed,
+            "unit": "beam-cell updates/s",
+            "n_gpus": world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32/u32 ray math + fp32 log-odds (fp64 endpoints)",
+            "data": "synthetic: seeded rectangle world, random-walk robots, LD06-format scans",
+            "config": {
+                "workload": "C3: 16384² grid @5cm per GPU, 64-scan x 4096-beam batch "
+                            "integrate + full frontier extraction per step",
+                "grid": [G, H_total],
+                "resolution_m": res,
+                "scans_per_batch": S,
+                "beams_per_scan": N,
+                "batch_pool": len(pool),
+                "parallelism": f"row-bands x{world_size}" if world_size > 1 else "single GPU",
+            },
+            "frontier_ms": t_fr * 1e3,
+            "integrate_ms": t_int * 1e3,
+            "integrate_updates_per_s": U_mean / t_int,
+            "updates_per_batch": U_mean,
+            "touched_cells_per_batch": T_mean,
+            "clusters": fr_clusters,
+            "kernel_avg_ms": avg,
+            "roofline": {
+                "kernel": "tile_apply",
+                "dominant_kernel": dominant,
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
+                "traffic": None,
+                "algorithmic_bytes_per_launch": bytes_apply,
+                "bytes_model": "8*U + 25*T per integrate call (SURVEY.md §8(d))",
+            },
+            "cpu_baseline": cpu,
+            "gen_seconds": t_gen,
+        }
+        print(json.dumps(result), flush=True)
+    mapper.close()
+    if world_size > 1:
+        dist.destroy_process_group()
+    return result
+
+
+def cpu_baseline(params, pool, amin, inc, budget_s):
+    """The CPU restatement (oracle/, a port of the SPEC; single thread) on a
+    bounded sample of the same workload: integrate as many pool batches as
+    fit in ~budget_s into a fresh map, then one frontier extraction."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    oracle.build()
+    om = oracle.OracleMap(params)
+    U = 0
+    t_int = 0.0
+    done = 0
+    for poses, ranges in pool:
+        a = time.perf_counter()
+        u, _ = om.integrate(poses, ranges, amin, inc)
+        t_int += time.perf_counter() - a
+        U += u
+        done += 1
+        if t_int > budget_s * 0.6:
+            break
+    a = time.perf_counter()
+    om.frontiers(want_mask=False, want_labels=False)
+    t_fr = time.perf_counter() - a
+    return {
+        "value": U / t_int,
+        "unit": "beam-cell updates/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{done} batch(es) of 64x4096 beams into a fresh 16384² map + 1 frontier pass",
+        "frontier_ms": t_fr * 1e3,
+        "cpu": _cpu_model(),
+    }
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+if __name__ == "__main__":
+    main()

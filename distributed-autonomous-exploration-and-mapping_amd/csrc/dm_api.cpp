@@ -1,0 +1,678 @@
+// dm_api.cpp — the C-ABI of libdm.so (include/dm.h): handle lifetime,
+// validation, error codes, host<->device staging, checkpoints, profiling.
+//
+// Contract from SURVEY.md §8(b): device memory is owned by the handle; host
+// pointers are borrowed for the call; synchronous functions return after
+// outputs are in host memory; errors are negative codes + a thread-local
+// message, never an abort or an exception across the ABI.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "dm_internal.h"
+
+namespace {
+thread_local std::string t_err;
+
+struct HostCluster {
+  long long label, size, sum_x, sum_y;
+};
+
+template <class T>
+int dev_alloc(T** p, int64_t count, const char* what) {
+  if (*p) { (void)hipFree(*p); *p = nullptr; }
+  if (count <= 0) count = 1;
+  hipError_t e = hipMalloc((void**)p, sizeof(T) * (size_t)count);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return dm_set_error(e == hipErrorOutOfMemory ? DM_ERR_OOM : DM_ERR_HIP,
+                        "hipMalloc(%s, %lld bytes): %s", what,
+                        (long long)(sizeof(T) * (size_t)count), hipGetErrorString(e));
+  }
+  return DM_OK;
+}
+
+template <class T>
+void dev_free(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+int validate_params(const dm_params* p) {
+  if (!p) return dm_set_error(DM_ERR_INVALID_ARG, "params is NULL");
+  if (p->width <= 0 || p->height <= 0 || p->width > (1ll << 30) || p->height > (1ll << 30))
+    return dm_set_error(DM_ERR_INVALID_ARG, "width/height must be in [1, 2^30] (got %lld x %lld)",
+                        (long long)p->width, (long long)p->height);
+  if (!(p->resolution > 0.0) || !isfinite(p->resolution))
+    return dm_set_error(DM_ERR_INVALID_ARG, "resolution must be finite and > 0");
+  if (!isfinite(p->origin_x) || !isfinite(p->origin_y))
+    return dm_set_error(DM_ERR_INVALID_ARG, "origin must be finite");
+  if (!(p->range_min >= 0.0f) || !(p->range_max > 0.0f) || !isfinite(p->range_max))
+    return dm_set_error(DM_ERR_INVALID_ARG, "need 0 <= range_min and finite range_max > 0");
+  if ((double)p->range_max / p->resolution > 16384.0)
+    return dm_set_error(DM_ERR_INVALID_ARG,
+                        "range_max / resolution must be <= 16384 cells (rays longer than that "
+                        "are outside the kernels' integer bounds)");
+  if (!isfinite(p->l_occ) || !isfinite(p->l_free) || !isfinite(p->l_min) || !isfinite(p->l_max) ||
+      !(p->l_min <= p->l_max))
+    return dm_set_error(DM_ERR_INVALID_ARG, "log-odds constants must be finite with l_min <= l_max");
+  if (p->band_row0 < 0 || p->band_row0 >= p->height || p->band_row0 % DM_TILE != 0)
+    return dm_set_error(DM_ERR_INVALID_ARG, "band_row0 must be in [0, height) and a multiple of %d",
+                        DM_TILE);
+  int64_t R = p->band_rows > 0 ? p->band_rows : p->height - p->band_row0;
+  if (R <= 0 || p->band_row0 + R > p->height)
+    return dm_set_error(DM_ERR_INVALID_ARG, "band_rows out of range");
+  if (ceil_div(p->width, DM_TILE) * ceil_div(R, DM_TILE) > (1ll << 30))
+    return dm_set_error(DM_ERR_INVALID_ARG, "too many tiles");
+  if (p->min_frontier_size < 0) return dm_set_error(DM_ERR_INVALID_ARG, "min_frontier_size < 0");
+  return DM_OK;
+}
+
+int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
+  const int64_t nb = (int64_t)S * N;
+  const int64_t per_beam = 2 * (g->nmax / DM_TILE) + 8;
+  if (nb > g->beams_cap) {
+    int rc = dev_alloc(&g->beams, nb, "beams");
+    if (rc) return rc;
+    g->beams_cap = nb;
+  }
+  const int64_t segs = nb * per_beam;
+  if (segs > g->segs_cap) {
+    int rc = dev_alloc(&g->segs, segs, "segments");
+    if (rc) return rc;
+    g->segs_cap = segs;
+  }
+  const int64_t side = ceil_div(2 * (int64_t)g->nmax + 1, DM_TILE) + 1;
+  int64_t act = std::min<int64_t>(g->NT, std::min<int64_t>(segs, (int64_t)S * side * side));
+  if (act < 1) act = 1;
+  if (act > g->act_cap) {
+    int rc = dev_alloc(&g->act_tiles, act, "active tiles");
+    if (!rc) rc = dev_alloc(&g->act_off, act, "active offsets");
+    if (!rc) rc = dev_alloc(&g->act_cur, act, "active cursors");
+    if (rc) return rc;
+    g->act_cap = act;
+  }
+  if (2 * (int64_t)N > g->trig_cap) {
+    int rc = dev_alloc(&g->trig, 2 * (int64_t)N, "trig table");
+    if (rc) return rc;
+    g->trig_cap = 2 * (int64_t)N;
+    g->trig_n = -1;
+  }
+  return DM_OK;
+}
+
+int ensure_trig(dm_grid* g, int32_t N, float amin, float inc) {
+  if (N == g->trig_n && amin == g->trig_amin && inc == g->trig_inc) return DM_OK;
+  // the table may still be read by an in-flight call
+  DM_HIP(hipStreamSynchronize(g->stream));
+  std::vector<double> t(2 * (size_t)std::max(N, 1));
+  for (int32_t i = 0; i < N; ++i) {
+    const double phi = (double)amin + (double)i * (double)inc;
+    t[2 * i] = cos(phi);
+    t[2 * i + 1] = sin(phi);
+  }
+  if (N > 0) DM_HIP(hipMemcpy(g->trig, t.data(), sizeof(double) * 2 * N, hipMemcpyHostToDevice));
+  g->trig_n = N;
+  g->trig_amin = amin;
+  g->trig_inc = inc;
+  return DM_OK;
+}
+
+int grow_slots(dm_grid* g, int64_t need) {
+  int64_t cap = std::max<int64_t>(need, 2 * g->slot_cap);
+  if (cap < (1 << 16)) cap = 1 << 16;
+  int rc = dev_alloc(&g->slot_label, cap, "slot labels");
+  if (!rc) rc = dev_alloc(&g->slot_parent, cap, "slot parents");
+  if (!rc) rc = dev_alloc(&g->slot_root, cap, "slot roots");
+  if (!rc) rc = dev_alloc(&g->slot_own, 3 * cap, "slot sums");
+  if (!rc) rc = dev_alloc(&g->slot_acc, 3 * cap, "slot totals");
+  if (!rc) rc = dev_alloc(&g->clusters, 4 * cap, "clusters");
+  if (rc) return rc;
+  g->slot_cap = cap;
+  return DM_OK;
+}
+
+int check_grid(const dm_grid* g) {
+  if (!g) return dm_set_error(DM_ERR_INVALID_ARG, "grid handle is NULL");
+  return DM_OK;
+}
+
+int use_device(const dm_grid* g) {
+  DM_HIP(hipSetDevice(g->device));
+  return DM_OK;
+}
+
+int check_integrate_args(int32_t S, int32_t N, const void* poses, const void* ranges) {
+  if (S < 0 || N < 0) return dm_set_error(DM_ERR_SHAPE, "S and N must be >= 0");
+  if ((int64_t)S * N > (1ll << 31) - 1) return dm_set_error(DM_ERR_SHAPE, "S*N must be < 2^31");
+  if (N > 65535) return dm_set_error(DM_ERR_SHAPE, "N must be <= 65535");
+  if ((int64_t)S * N > 0 && (!poses || !ranges))
+    return dm_set_error(DM_ERR_INVALID_ARG, "poses/ranges is NULL");
+  return DM_OK;
+}
+
+int finish_counts(dm_grid* g, uint64_t* U, uint64_t* T) {
+  DM_HIP(hipMemcpyAsync(g->h_cnt, g->cnt, sizeof(unsigned long long) * CNT_N,
+                        hipMemcpyDeviceToHost, g->stream));
+  DM_HIP(hipStreamSynchronize(g->stream));
+  if (g->h_cnt[CNT_OVERFLOW] & 3ull) {
+    // cannot happen with the bounds in grow_integrate; keep the map consistent anyway
+    (void)hipMemset(g->tile_count, 0, sizeof(int32_t) * (size_t)g->NT);
+    return dm_set_error(DM_ERR_CAPACITY, "integrate workspace overflow (flags %llu)",
+                        (unsigned long long)g->h_cnt[CNT_OVERFLOW]);
+  }
+  if (U) *U = g->h_cnt[CNT_U];
+  if (T) *T = g->h_cnt[CNT_T];
+  return DM_OK;
+}
+
+}  // namespace
+
+int dm_set_error(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  t_err = buf;
+  return code;
+}
+
+int dm_hip_check(hipError_t e, const char* what) {
+  return dm_set_error(e == hipErrorOutOfMemory ? DM_ERR_OOM : DM_ERR_HIP, "%s: %s (%d)", what,
+                      hipGetErrorString(e), (int)e);
+}
+
+void dm_timer_begin(dm_grid* g, const char* name, KernelTimer* t) {
+  if (!g->profile) return;
+  t->name = name;
+  (void)hipEventCreate(&t->start);
+  (void)hipEventCreate(&t->stop);
+  (void)hipEventRecord(t->start, g->stream);
+}
+
+void dm_timer_end(dm_grid* g, KernelTimer* t) {
+  if (!g->profile) return;
+  (void)hipEventRecord(t->stop, g->stream);
+  g->pending.push_back(*t);
+  if (g->pending.size() > 4096) {
+    int32_t n = 0;
+    (void)dm_profile_read(g, nullptr, 0, &n);
+  }
+}
+
+extern "C" {
+
+const char* dm_last_error(void) { return t_err.c_str(); }
+const char* dm_version(void) { return "dm 0.1.0 (gfx950, HIP)"; }
+
+int dm_default_params(dm_params* p, int64_t width, int64_t height) {
+  if (!p) return dm_set_error(DM_ERR_INVALID_ARG, "params is NULL");
+  memset(p, 0, sizeof *p);
+  p->width = width;
+  p->height = height;
+  p->resolution = 0.05;                      // slam_config.yaml:26
+  p->origin_x = -0.5 * (double)width * p->resolution;
+  p->origin_y = -0.5 * (double)height * p->resolution;
+  p->range_min = 0.02f;                      // LD06 driver rodata 0xbc840
+  p->range_max = 12.0f;                      // slam_config.yaml:27
+  p->l_occ = 0.85f;
+  p->l_free = -0.4f;
+  p->l_min = -2.0f;
+  p->l_max = 3.5f;
+  p->occ_thresh = 0.0f;
+  p->free_thresh = 0.0f;
+  p->min_frontier_size = 1;
+  p->band_row0 = 0;
+  p->band_rows = 0;
+  return DM_OK;
+}
+
+int dm_create(dm_grid** out, const dm_params* p, int device) {
+  if (!out) return dm_set_error(DM_ERR_INVALID_ARG, "out is NULL");
+  *out = nullptr;
+  int rc = validate_params(p);
+  if (rc) return rc;
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= 0)
+    return dm_set_error(DM_ERR_HIP, "no HIP device available (%s)", hipGetErrorString(e));
+  if (device < 0 || device >= ndev)
+    return dm_set_error(DM_ERR_INVALID_ARG, "device %d out of range [0, %d)", device, ndev);
+  DM_HIP(hipSetDevice(device));
+  dm_grid* g = new (std::nothrow) dm_grid();
+  if (!g) return dm_set_error(DM_ERR_OOM, "host allocation failed");
+  g->p = *p;
+  if (g->p.band_rows <= 0) g->p.band_rows = p->height - p->band_row0;
+  g->device = device;
+  g->W = p->width;
+  g->H = p->height;
+  g->row0 = p->band_row0;
+  g->R = g->p.band_rows;
+  g->TX = ceil_div(g->W, DM_TILE);
+  g->TY = ceil_div(g->R, DM_TILE);
+  g->NT = g->TX * g->TY;
+  g->nmax = (int32_t)ceil((double)p->range_max / p->resolution) + 2;
+  const int64_t cells = g->W * g->R;
+  auto fail = [&](int code) {
+    dm_destroy(g);
+    return code;
+  };
+  if ((rc = dev_alloc(&g->L, cells, "log-odds"))) return fail(rc);
+  if ((rc = dev_alloc(&g->state, cells, "state"))) return fail(rc);
+  if ((rc = dev_alloc(&g->tile_count, g->NT, "tile counts"))) return fail(rc);
+  if ((rc = dev_alloc(&g->tile_slot, g->NT, "tile slots"))) return fail(rc);
+  if ((rc = dev_alloc(&g->tile_free, g->NT, "tile free counts"))) return fail(rc);
+  if ((rc = dev_alloc(&g->cnt, CNT_N, "counters"))) return fail(rc);
+  if ((rc = dev_alloc(&g->ftiles, g->NT, "frontier tiles"))) return fail(rc);
+  if ((rc = dev_alloc(&g->fmap, g->NT, "frontier tile map"))) return fail(rc);
+  if ((rc = dev_alloc(&g->border, g->NT * 256, "frontier borders"))) return fail(rc);
+  if ((rc = dev_alloc(&g->edge_slot, 2 * g->W, "edge slots"))) return fail(rc);
+  if ((rc = dev_alloc(&g->edge_label, 2 * g->W, "edge labels"))) return fail(rc);
+  if ((rc = dev_alloc(&g->halo, 2 * g->W, "halo rows"))) return fail(rc);
+  if ((rc = grow_slots(g, 1 << 16))) return fail(rc);
+  e = hipHostMalloc((void**)&g->h_cnt, sizeof(unsigned long long) * CNT_N, hipHostMallocDefault);
+  if (e != hipSuccess) return fail(dm_hip_check(e, "hipHostMalloc(counters)"));
+  e = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate"));
+  g->own_stream = true;
+  if ((rc = dm_reset(g))) return fail(rc);
+  *out = g;
+  return DM_OK;
+}
+
+int dm_destroy(dm_grid* g) {
+  if (!g) return DM_OK;
+  (void)hipSetDevice(g->device);
+  if (g->stream) (void)hipStreamSynchronize(g->stream);
+  for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
+  dev_free(g->L); dev_free(g->state); dev_free(g->tile_count); dev_free(g->tile_slot);
+  dev_free(g->tile_free); dev_free(g->cnt); dev_free(g->beams); dev_free(g->segs);
+  dev_free(g->act_tiles); dev_free(g->act_off); dev_free(g->act_cur); dev_free(g->trig);
+  dev_free(g->pose4); dev_free(g->ranges); dev_free(g->ftiles); dev_free(g->fmap);
+  dev_free(g->border); dev_free(g->slot_label); dev_free(g->slot_parent); dev_free(g->slot_root);
+  dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
+  dev_free(g->edge_slot); dev_free(g->edge_label); dev_free(g->mask); dev_free(g->labels);
+  dev_free(g->halo);
+  if (g->h_cnt) (void)hipHostFree(g->h_cnt);
+  if (g->h_pose4) (void)hipHostFree(g->h_pose4);
+  if (g->stream && g->own_stream) (void)hipStreamDestroy(g->stream);
+  delete g;
+  return DM_OK;
+}
+
+int dm_reset(dm_grid* g) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  const int64_t cells = g->W * g->R;
+  DM_HIP(hipMemsetAsync(g->L, 0, sizeof(float) * (size_t)cells, g->stream));
+  DM_HIP(hipMemsetAsync(g->state, 0xFF, (size_t)cells, g->stream));
+  DM_HIP(hipMemsetAsync(g->tile_count, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
+  DM_HIP(hipMemsetAsync(g->tile_free, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
+  DM_HIP(hipMemsetAsync(g->cnt, 0, sizeof(unsigned long long) * CNT_N, g->stream));
+  DM_HIP(hipStreamSynchronize(g->stream));
+  return DM_OK;
+}
+
+int dm_get_params(const dm_grid* g, dm_params* out) {
+  int rc = check_grid(g);
+  if (rc) return rc;
+  if (!out) return dm_set_error(DM_ERR_INVALID_ARG, "out is NULL");
+  *out = g->p;
+  return DM_OK;
+}
+
+int dm_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N, const float* ranges,
+                 float angle_min, float angle_increment, uint64_t* out_updates,
+                 uint64_t* out_touched) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if ((rc = check_integrate_args(S, N, poses, ranges))) return rc;
+  if ((rc = grow_integrate(g, S, N))) return rc;
+  if ((rc = ensure_trig(g, N, angle_min, angle_increment))) return rc;
+  const int64_t nb = (int64_t)S * N;
+  if ((int64_t)S * 4 > g->pose_cap) {
+    if ((rc = dev_alloc(&g->pose4, (int64_t)S * 4, "poses"))) return rc;
+    g->pose_cap = (int64_t)S * 4;
+  }
+  if (nb > g->ranges_cap) {
+    if ((rc = dev_alloc(&g->ranges, nb, "ranges"))) return rc;
+    g->ranges_cap = nb;
+  }
+  if ((int64_t)S * 4 > g->h_pose_cap) {
+    DM_HIP(hipStreamSynchronize(g->stream));
+    if (g->h_pose4) (void)hipHostFree(g->h_pose4);
+    g->h_pose4 = nullptr;
+    DM_HIP(hipHostMalloc((void**)&g->h_pose4, sizeof(double) * 4 * (size_t)S, hipHostMallocDefault));
+    g->h_pose_cap = (int64_t)S * 4;
+  }
+  // the pinned pose staging buffer may still feed an in-flight copy
+  DM_HIP(hipStreamSynchronize(g->stream));
+  for (int32_t s = 0; s < S; ++s) {
+    const double x = poses[3 * s], y = poses[3 * s + 1], yaw = poses[3 * s + 2];
+    g->h_pose4[4 * s + 0] = x;
+    g->h_pose4[4 * s + 1] = y;
+    g->h_pose4[4 * s + 2] = cos(yaw);  // C library, as the oracle
+    g->h_pose4[4 * s + 3] = sin(yaw);
+  }
+  if (S > 0)
+    DM_HIP(hipMemcpyAsync(g->pose4, g->h_pose4, sizeof(double) * 4 * (size_t)S,
+                          hipMemcpyHostToDevice, g->stream));
+  if (nb > 0)
+    DM_HIP(hipMemcpyAsync(g->ranges, ranges, sizeof(float) * (size_t)nb, hipMemcpyHostToDevice,
+                          g->stream));
+  if ((rc = dm_launch_integrate(g, S, g->pose4, N, g->ranges, g->trig))) return rc;
+  g->last_S = S;
+  g->last_N = N;
+  g->frontier_valid = false;
+  return finish_counts(g, out_updates, out_touched);
+}
+
+int dm_integrate_device(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
+                        const float* d_ranges, float angle_min, float angle_increment) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if ((rc = check_integrate_args(S, N, d_pose4, d_ranges))) return rc;
+  if ((rc = grow_integrate(g, S, N))) return rc;
+  if ((rc = ensure_trig(g, N, angle_min, angle_increment))) return rc;
+  if ((rc = dm_launch_integrate(g, S, d_pose4, N, d_ranges, g->trig))) return rc;
+  g->last_S = S;
+  g->last_N = N;
+  g->frontier_valid = false;
+  return DM_OK;
+}
+
+int dm_last_counts(dm_grid* g, uint64_t* updates, uint64_t* touched) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  return finish_counts(g, updates, touched);
+}
+
+int dm_get_state(dm_grid* g, int8_t* out) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (!out) return dm_set_error(DM_ERR_INVALID_ARG, "out is NULL");
+  DM_HIP(hipMemcpyAsync(out, g->state, (size_t)(g->W * g->R), hipMemcpyDeviceToHost, g->stream));
+  DM_HIP(hipStreamSynchronize(g->stream));
+  return DM_OK;
+}
+
+int dm_get_logodds(dm_grid* g, float* out) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (!out) return dm_set_error(DM_ERR_INVALID_ARG, "out is NULL");
+  DM_HIP(hipMemcpyAsync(out, g->L, sizeof(float) * (size_t)(g->W * g->R), hipMemcpyDeviceToHost,
+                        g->stream));
+  DM_HIP(hipStreamSynchronize(g->stream));
+  return DM_OK;
+}
+
+int dm_set_logodds(dm_grid* g, const float* in) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (!in) return dm_set_error(DM_ERR_INVALID_ARG, "in is NULL");
+  DM_HIP(hipStreamSynchronize(g->stream));
+  DM_HIP(hipMemcpy(g->L, in, sizeof(float) * (size_t)(g->W * g->R), hipMemcpyHostToDevice));
+  if ((rc = dm_launch_state_from_logodds(g))) return rc;
+  DM_HIP(hipStreamSynchronize(g->stream));
+  g->frontier_valid = false;
+  return DM_OK;
+}
+
+int dm_set_state(dm_grid* g, const int8_t* in) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (!in) return dm_set_error(DM_ERR_INVALID_ARG, "in is NULL");
+  const int64_t cells = g->W * g->R;
+  int8_t* d = nullptr;
+  if ((rc = dev_alloc(&d, cells, "state staging"))) return rc;
+  DM_HIP(hipStreamSynchronize(g->stream));
+  hipError_t e = hipMemcpy(d, in, (size_t)cells, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    rc = dm_launch_set_state(g, d);
+    if (!rc) e = hipStreamSynchronize(g->stream);
+  }
+  (void)hipFree(d);
+  if (e != hipSuccess) return dm_hip_check(e, "dm_set_state");
+  g->frontier_valid = false;
+  return rc;
+}
+
+int dm_frontiers(dm_grid* g, uint8_t* mask, int64_t* labels, dm_cluster* out, int64_t cap,
+                 int64_t* n_out) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (cap < 0 || (cap > 0 && !out)) return dm_set_error(DM_ERR_INVALID_ARG, "bad cluster buffer");
+  const int64_t cells = g->W * g->R;
+  if (mask && !g->mask && (rc = dev_alloc(&g->mask, cells, "dense mask"))) return rc;
+  if (labels && !g->cell_slot) {
+    if ((rc = dev_alloc(&g->cell_slot, cells, "dense cell slots"))) return rc;
+    if ((rc = dev_alloc(&g->labels, cells, "dense labels"))) return rc;
+  }
+  int64_t n = 0;
+  for (int attempt = 0; attempt < 8; ++attempt) {
+    rc = dm_launch_frontiers(g, mask != nullptr, labels != nullptr, &n);
+    if (rc != DM_ERR_CAPACITY) break;
+    if ((rc = grow_slots(g, n + n / 2 + 1024))) return rc;
+    rc = DM_ERR_CAPACITY;
+  }
+  if (rc) return rc == DM_ERR_CAPACITY ? dm_set_error(rc, "frontier slot arrays kept overflowing") : rc;
+  g->frontier_valid = true;
+  std::vector<HostCluster> hc((size_t)n);
+  if (n > 0)
+    DM_HIP(hipMemcpy(hc.data(), g->clusters, sizeof(HostCluster) * (size_t)n, hipMemcpyDeviceToHost));
+  std::sort(hc.begin(), hc.end(),
+            [](const HostCluster& a, const HostCluster& b) { return a.label < b.label; });
+  const int64_t nw = std::min<int64_t>(n, cap);
+  for (int64_t i = 0; i < nw; ++i) {
+    dm_cluster& c = out[i];
+    c.label = hc[i].label;
+    c.size = hc[i].size;
+    c.sum_x = hc[i].sum_x;
+    c.sum_y = hc[i].sum_y;
+    const double mx = (double)c.sum_x / (double)c.size;
+    const double my = (double)c.sum_y / (double)c.size;
+    c.cx_m = g->p.origin_x + (mx + 0.5) * g->p.resolution;
+    c.cy_m = g->p.origin_y + (my + 0.5) * g->p.resolution;
+  }
+  if (mask) DM_HIP(hipMemcpy(mask, g->mask, (size_t)cells, hipMemcpyDeviceToHost));
+  if (labels) DM_HIP(hipMemcpy(labels, g->labels, sizeof(int64_t) * (size_t)cells, hipMemcpyDeviceToHost));
+  if (n_out) *n_out = n;
+  if (n > cap) return dm_set_error(DM_ERR_CAPACITY, "%lld clusters, capacity %lld", (long long)n,
+                                   (long long)cap);
+  return DM_OK;
+}
+
+int dm_set_halo(dm_grid* g, const int8_t* before, const int8_t* after) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  DM_HIP(hipStreamSynchronize(g->stream));
+  if (before) DM_HIP(hipMemcpy(g->halo, before, (size_t)g->W, hipMemcpyHostToDevice));
+  if (after) DM_HIP(hipMemcpy(g->halo + g->W, after, (size_t)g->W, hipMemcpyHostToDevice));
+  g->has_halo[0] = before != nullptr;
+  g->has_halo[1] = after != nullptr;
+  g->frontier_valid = false;
+  return DM_OK;
+}
+
+int dm_set_halo_device(dm_grid* g, const int8_t* before, const int8_t* after) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (before) DM_HIP(hipMemcpyAsync(g->halo, before, (size_t)g->W, hipMemcpyDeviceToDevice, g->stream));
+  if (after)
+    DM_HIP(hipMemcpyAsync(g->halo + g->W, after, (size_t)g->W, hipMemcpyDeviceToDevice, g->stream));
+  g->has_halo[0] = before != nullptr;
+  g->has_halo[1] = after != nullptr;
+  g->frontier_valid = false;
+  return DM_OK;
+}
+
+int dm_get_edge_rows(dm_grid* g, int8_t* first_row, int8_t* last_row) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (first_row)
+    DM_HIP(hipMemcpyAsync(first_row, g->state, (size_t)g->W, hipMemcpyDeviceToHost, g->stream));
+  if (last_row)
+    DM_HIP(hipMemcpyAsync(last_row, g->state + (g->R - 1) * g->W, (size_t)g->W,
+                          hipMemcpyDeviceToHost, g->stream));
+  DM_HIP(hipStreamSynchronize(g->stream));
+  return DM_OK;
+}
+
+int dm_get_edge_rows_device(dm_grid* g, int8_t* first_row, int8_t* last_row) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (first_row)
+    DM_HIP(hipMemcpyAsync(first_row, g->state, (size_t)g->W, hipMemcpyDeviceToDevice, g->stream));
+  if (last_row)
+    DM_HIP(hipMemcpyAsync(last_row, g->state + (g->R - 1) * g->W, (size_t)g->W,
+                          hipMemcpyDeviceToDevice, g->stream));
+  return DM_OK;
+}
+
+int dm_get_edge_labels(dm_grid* g, int64_t* first_row, int64_t* last_row) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (!g->frontier_valid)
+    return dm_set_error(DM_ERR_STATE, "call dm_frontiers first (map or halo changed since)");
+  if (first_row)
+    DM_HIP(hipMemcpy(first_row, g->edge_label, sizeof(int64_t) * (size_t)g->W, hipMemcpyDeviceToHost));
+  if (last_row)
+    DM_HIP(hipMemcpy(last_row, g->edge_label + g->W, sizeof(int64_t) * (size_t)g->W,
+                     hipMemcpyDeviceToHost));
+  return DM_OK;
+}
+
+static const char kMagic[8] = {'D', 'M', 'A', 'P', '0', '0', '0', '1'};
+
+int dm_save(dm_grid* g, const char* path) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (!path) return dm_set_error(DM_ERR_INVALID_ARG, "path is NULL");
+  const int64_t cells = g->W * g->R;
+  std::vector<float> L((size_t)cells);
+  if ((rc = dm_get_logodds(g, L.data()))) return rc;
+  FILE* f = fopen(path, "wb");
+  if (!f) return dm_set_error(DM_ERR_IO, "cannot open %s for writing", path);
+  bool ok = fwrite(kMagic, 1, 8, f) == 8 && fwrite(&g->p, sizeof(dm_params), 1, f) == 1 &&
+            fwrite(L.data(), sizeof(float), (size_t)cells, f) == (size_t)cells;
+  ok = (fclose(f) == 0) && ok;
+  if (!ok) return dm_set_error(DM_ERR_IO, "short write to %s", path);
+  return DM_OK;
+}
+
+int dm_load(dm_grid* g, const char* path) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (!path) return dm_set_error(DM_ERR_INVALID_ARG, "path is NULL");
+  FILE* f = fopen(path, "rb");
+  if (!f) return dm_set_error(DM_ERR_IO, "cannot open %s", path);
+  char magic[8];
+  dm_params p;
+  const int64_t cells = g->W * g->R;
+  std::vector<float> L((size_t)cells);
+  bool ok = fread(magic, 1, 8, f) == 8 && memcmp(magic, kMagic, 8) == 0 &&
+            fread(&p, sizeof p, 1, f) == 1;
+  if (ok && (p.width != g->p.width || p.height != g->p.height || p.band_row0 != g->p.band_row0 ||
+             p.band_rows != g->p.band_rows || p.resolution != g->p.resolution)) {
+    fclose(f);
+    return dm_set_error(DM_ERR_SHAPE, "checkpoint %s has a different grid geometry", path);
+  }
+  ok = ok && fread(L.data(), sizeof(float), (size_t)cells, f) == (size_t)cells;
+  fclose(f);
+  if (!ok) return dm_set_error(DM_ERR_IO, "%s is not a dm checkpoint or is truncated", path);
+  return dm_set_logodds(g, L.data());
+}
+
+int dm_set_stream(dm_grid* g, void* stream) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  DM_HIP(hipStreamSynchronize(g->stream));
+  if (stream) {
+    if (g->own_stream && g->stream) (void)hipStreamDestroy(g->stream);
+    g->stream = (hipStream_t)stream;
+    g->own_stream = false;
+  } else if (!g->own_stream) {
+    DM_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+    g->own_stream = true;
+  }
+  return DM_OK;
+}
+
+int dm_synchronize(dm_grid* g) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  DM_HIP(hipStreamSynchronize(g->stream));
+  return DM_OK;
+}
+
+int dm_profile_enable(dm_grid* g, int enable) {
+  int rc = check_grid(g);
+  if (rc) return rc;
+  g->profile = enable != 0;
+  return DM_OK;
+}
+
+int dm_profile_read(dm_grid* g, dm_kernel_stat* out, int32_t cap, int32_t* n_out) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  DM_HIP(hipStreamSynchronize(g->stream));
+  for (auto& t : g->pending) {
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, t.start, t.stop);
+    (void)hipEventDestroy(t.start);
+    (void)hipEventDestroy(t.stop);
+    dm_kernel_stat* s = nullptr;
+    for (auto& e : g->stats)
+      if (t.name == e.name) s = &e;
+    if (!s) {
+      dm_kernel_stat ns;
+      memset(&ns, 0, sizeof ns);
+      snprintf(ns.name, sizeof ns.name, "%s", t.name.c_str());
+      g->stats.push_back(ns);
+      s = &g->stats.back();
+    }
+    s->launches += 1;
+    s->total_ms += ms;
+  }
+  g->pending.clear();
+  const int32_t n = (int32_t)g->stats.size();
+  for (int32_t i = 0; i < std::min(n, cap); ++i) out[i] = g->stats[(size_t)i];
+  if (n_out) *n_out = n;
+  return DM_OK;
+}
+
+int dm_profile_reset(dm_grid* g) {
+  int rc = check_grid(g);
+  if (rc) return rc;
+  int32_t n = 0;
+  if ((rc = dm_profile_read(g, nullptr, 0, &n))) return rc;
+  g->stats.clear();
+  return DM_OK;
+}
+
+int dm_map_image(dm_grid* g, uint8_t* out) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (!out) return dm_set_error(DM_ERR_INVALID_ARG, "out is NULL");
+  const int64_t cells = g->W * g->R;
+  uint8_t* d = nullptr;
+  if ((rc = dev_alloc(&d, cells, "image"))) return rc;
+  rc = dm_launch_map_image(g, d);
+  hipError_t e = hipSuccess;
+  if (!rc) e = hipMemcpyAsync(out, d, (size_t)cells, hipMemcpyDeviceToHost, g->stream);
+  if (!rc && e == hipSuccess) e = hipStreamSynchronize(g->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return dm_hip_check(e, "dm_map_image");
+  return rc;
+}
+
+}  // extern "C"

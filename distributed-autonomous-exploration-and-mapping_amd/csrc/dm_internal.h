@@ -1,0 +1,156 @@
+// dm_internal.h — internal types of libdm (not part of the C-ABI).
+//
+// Device data layout in HBM (one handle = one row band of the map):
+//   L      float [R][W]  log-odds, row-major (band-local row = gy - row0)
+//   state  int8  [R][W]  OccupancyGrid.data encoding (-1/0/100)
+//   tile_* int32 [TY][TX] per 64x64 tile summaries (TX = ceil(W/64),
+//          TY = ceil(R/64)): per-call segment counts, active slots, and the
+//          number of free cells (drives which tiles the frontier pass visits)
+// Per-call workspace (grown on demand, reused across calls):
+//   beams  Beam[S*N]     endpoint cells + Bresenham parameters per beam
+//   segs   Seg[...]      (beam, k0, k1) ray pieces binned by tile
+//   active tile lists, frontier slots (one per tile-local component), borders.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/dm.h"
+
+#define DM_TS 64  // tile edge; == DM_TILE
+
+// Bresenham parameters of one beam, in global cell coordinates.  The line is
+// parametrised along its major axis: cell k (0..n) has
+//   major = sa + k*ia,  minor = sb + ib * floor((2*k*adb + n) / (2*n))
+// (n = |d major| > 0), or just (sa, sb) for n == 0.  SPEC a5.
+struct Beam {
+  int32_t sa, sb;   // start cell, major / minor axis
+  int32_t n, adb;   // |d major|, |d minor|
+  int8_t ia, ib;    // unit steps along major / minor
+  uint8_t xmajor;   // 1 if major axis is x
+  uint8_t flags;    // bit0 valid, bit1 hit
+  int32_t pad;
+  double rden;      // 1.0 / (2n), 0 for n == 0
+};
+static_assert(sizeof(Beam) == 32, "Beam layout");
+
+// One ray piece inside one tile: cells k0..k1 of beam `beam`.
+struct Seg {
+  uint32_t beam;
+  uint16_t k0, k1;
+};
+static_assert(sizeof(Seg) == 8, "Seg layout");
+
+// device counters (uint64 each)
+enum {
+  CNT_ACTIVE = 0,   // active tiles this integrate call
+  CNT_U = 1,        // beam-cell updates
+  CNT_T = 2,        // touched cells
+  CNT_SEGS = 3,     // segments emitted
+  CNT_FTILES = 4,   // tiles visited by the frontier pass
+  CNT_SLOTS = 5,    // tile-local frontier components
+  CNT_CLUSTERS = 6, // output clusters
+  CNT_OVERFLOW = 7, // capacity overflow flags
+  CNT_N = 8
+};
+
+struct KernelTimer {
+  std::string name;
+  hipEvent_t start, stop;
+};
+
+struct dm_grid {
+  dm_params p;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int64_t W = 0, H = 0, R = 0, row0 = 0;
+  int64_t TX = 0, TY = 0, NT = 0;
+  int32_t nmax = 0;  // max ray length (cells) bound
+
+  float* L = nullptr;
+  int8_t* state = nullptr;
+  int32_t* tile_count = nullptr;
+  int32_t* tile_slot = nullptr;
+  int32_t* tile_free = nullptr;
+  unsigned long long* cnt = nullptr;  // CNT_N device counters
+  unsigned long long* h_cnt = nullptr;  // pinned mirror
+
+  // integrate workspace
+  Beam* beams = nullptr; int64_t beams_cap = 0;
+  Seg* segs = nullptr; int64_t segs_cap = 0;
+  int32_t* act_tiles = nullptr; int32_t* act_off = nullptr; int32_t* act_cur = nullptr;
+  int64_t act_cap = 0;
+  double* trig = nullptr; int32_t trig_n = -1; float trig_amin = 0, trig_inc = 0;
+  int64_t trig_cap = 0;
+  double* pose4 = nullptr; int64_t pose_cap = 0;
+  float* ranges = nullptr; int64_t ranges_cap = 0;
+  double* h_pose4 = nullptr; int64_t h_pose_cap = 0;  // pinned
+  int32_t last_S = 0, last_N = 0;
+
+  // frontier workspace
+  int32_t* ftiles = nullptr;   // list of tiles visited
+  int32_t* fmap = nullptr;     // tile -> index in ftiles or -1
+  int32_t* border = nullptr;   // [ftile][4][64] slot ids
+  int64_t border_cap = 0;      // in tiles
+  int64_t slot_cap = 0;
+  long long* slot_label = nullptr;
+  int32_t* slot_parent = nullptr;
+  int32_t* slot_root = nullptr;
+  long long* slot_own = nullptr;  // [slot][3] size, sum_x, sum_y
+  long long* slot_acc = nullptr;  // [slot][3]
+  long long* clusters = nullptr;  // [cap][4] label,size,sum_x,sum_y
+  int32_t* cell_slot = nullptr;   // dense [R][W] (only when labels requested)
+  int32_t* edge_slot = nullptr;   // [2][W] slots of the band's first / last row
+  long long* edge_label = nullptr;// [2][W]
+  uint8_t* mask = nullptr;        // dense [R][W] (only when mask requested)
+  long long* labels = nullptr;    // dense [R][W] int64 (only when requested)
+  int8_t* halo = nullptr;         // [2][W]: row before band, row after band
+  int has_halo[2] = {0, 0};
+  bool frontier_valid = false;
+
+  // profiling
+  bool profile = false;
+  std::vector<KernelTimer> pending;
+  std::vector<dm_kernel_stat> stats;
+};
+
+// ---- device helpers ------------------------------------------------------
+__host__ __device__ inline int64_t dm_floordiv(int64_t a, int64_t b) {
+  int64_t q = a / b;
+  if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+  return q;
+}
+
+// floor(num / den) for 0 <= num < 2^31, den > 0, via a double reciprocal and
+// one integer correction (exact).
+__device__ inline int32_t dm_udiv(int32_t num, int32_t den, double rden) {
+  int32_t q = (int32_t)((double)num * rden);
+  if ((int64_t)(q + 1) * den <= num) ++q;
+  else if ((int64_t)q * den > num) --q;
+  return q;
+}
+
+// ---- launchers (dm_integrate.hip / dm_frontier.hip) -----------------------
+int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
+                        const float* d_ranges, const double* d_trig);
+int dm_launch_recount(dm_grid* g);
+int dm_launch_state_from_logodds(dm_grid* g);
+int dm_launch_map_image(dm_grid* g, uint8_t* d_img);
+int dm_launch_set_state(dm_grid* g, const int8_t* d_state_in);
+int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters);
+
+// error plumbing (dm_api.cpp)
+int dm_set_error(int code, const char* fmt, ...);
+int dm_hip_check(hipError_t e, const char* what);
+void dm_timer_begin(dm_grid* g, const char* name, KernelTimer* t);
+void dm_timer_end(dm_grid* g, KernelTimer* t);
+
+#define DM_HIP(call)                                         \
+  do {                                                       \
+    hipError_t _e = (call);                                  \
+    if (_e != hipSuccess) return dm_hip_check(_e, #call);    \
+  } while (0)

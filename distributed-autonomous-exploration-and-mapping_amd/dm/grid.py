@@ -1,0 +1,266 @@
+"""Python host side of the hot path: a locked handle over libdm.so.
+
+``OccupancyMapper`` is what a ROS 2 node calls (dm/ros_node.py): it takes the
+same data a ``sensor_msgs/LaserScan`` carries (ranges, angle_min,
+angle_increment) plus the laser pose, and yields what ``nav_msgs/OccupancyGrid``
+carries (int8 row-major -1/0/100, origin bottom-left), i.e. the data
+``ThymioBrain.map_cb`` caches and ``get_map_image`` renders
+(server/thymio_project/thymio_project/main.py:80-81, 241-279).
+
+Threading: the reference writes ``latest_map`` on the
+rclpy spin thread and reads it on the Flask thread (main.py:80-81 vs
+:244-256); a libdm handle is not thread-safe, so every call here holds a
+per-handle lock and every array returned is a fresh copy.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _ffi
+from ._ffi import CLUSTER_DTYPE, DmCluster, DmError, DmParams, check, load_library
+
+
+def default_params(width: int, height: int, **overrides) -> DmParams:
+    """dm_default_params + keyword overrides (resolution 0.05 and max range
+    12.0 from slam_config.yaml:26-27)."""
+    lib = load_library()
+    p = DmParams()
+    check(lib.dm_default_params(ctypes.byref(p), int(width), int(height)))
+    res_given = "resolution" in overrides
+    for k, v in overrides.items():
+        if not hasattr(p, k):
+            raise DmError(_ffi.DM_ERR_INVALID_ARG, f"unknown parameter {k!r}")
+        setattr(p, k, v)
+    if res_given and "origin_x" not in overrides:
+        p.origin_x = -0.5 * p.width * p.resolution
+    if res_given and "origin_y" not in overrides:
+        p.origin_y = -0.5 * p.height * p.resolution
+    return p
+
+
+def params_from_dict(d: dict) -> DmParams:
+    p = DmParams()
+    for k, v in d.items():
+        setattr(p, k, v)
+    return p
+
+
+@dataclass
+class Frontiers:
+    """Result of one frontier extraction."""
+
+    clusters: np.ndarray            # structured CLUSTER_DTYPE, sorted by label
+    mask: np.ndarray | None = None  # uint8 [rows, W]
+    labels: np.ndarray | None = None  # int64 [rows, W], -1 off-frontier
+
+    def __len__(self) -> int:
+        return int(self.clusters.shape[0])
+
+
+def _vp(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class OccupancyMapper:
+    """One device-resident map (or one row band of a sharded map)."""
+
+    def __init__(self, params: DmParams, device: int = 0):
+        self._lib = load_library()
+        self._lock = threading.RLock()
+        self._h = ctypes.c_void_p()
+        check(self._lib.dm_create(ctypes.byref(self._h), ctypes.byref(params), int(device)))
+        out = DmParams()
+        check(self._lib.dm_get_params(self._h, ctypes.byref(out)))
+        self.params = out
+        self.device = device
+        self.width = int(out.width)
+        self.rows = int(out.band_rows)
+        self.row0 = int(out.band_row0)
+
+    # -- lifetime ---------------------------------------------------------
+    def close(self):
+        with self._lock:
+            if self._h:
+                self._lib.dm_destroy(self._h)
+                self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _handle(self):
+        if not self._h:
+            raise DmError(_ffi.DM_ERR_STATE, "mapper is closed")
+        return self._h
+
+    # -- integration ------------------------------------------------------
+    def integrate(self, poses, ranges, angle_min, angle_increment):
+        """Integrate S scans: poses [S,3] (x, y, yaw), ranges [S,N] float32.
+        Returns (updates U, touched cells T)."""
+        poses = np.ascontiguousarray(poses, dtype=np.float64).reshape(-1, 3)
+        ranges = np.ascontiguousarray(ranges, dtype=np.float32).reshape(poses.shape[0], -1)
+        S, N = ranges.shape
+        U = ctypes.c_uint64(0)
+        T = ctypes.c_uint64(0)
+        with self._lock:
+            check(self._lib.dm_integrate(self._handle(), S, _vp(poses), N, _vp(ranges),
+                                         float(angle_min), float(angle_increment),
+                                         ctypes.byref(U), ctypes.byref(T)))
+        return int(U.value), int(T.value)
+
+    def integrate_scan(self, scan, pose):
+        """One LaserScan-like message (attributes ranges, angle_min,
+        angle_increment) at laser pose (x, y, yaw) in the map frame."""
+        ranges = np.asarray(scan.ranges, dtype=np.float32)[None, :]
+        return self.integrate(np.asarray(pose, np.float64)[None, :], ranges,
+                              np.float32(scan.angle_min), np.float32(scan.angle_increment))
+
+    def integrate_device(self, d_pose4_ptr: int, S: int, d_ranges_ptr: int, N: int,
+                         angle_min, angle_increment):
+        """Asynchronous integrate from device pointers (pose4 = x, y, cos yaw,
+        sin yaw as float64 [S,4]; ranges float32 [S,N])."""
+        with self._lock:
+            check(self._lib.dm_integrate_device(self._handle(), int(S), ctypes.c_void_p(d_pose4_ptr),
+                                                int(N), ctypes.c_void_p(d_ranges_ptr),
+                                                float(angle_min), float(angle_increment)))
+
+    def last_counts(self):
+        U = ctypes.c_uint64(0)
+        T = ctypes.c_uint64(0)
+        with self._lock:
+            check(self._lib.dm_last_counts(self._handle(), ctypes.byref(U), ctypes.byref(T)))
+        return int(U.value), int(T.value)
+
+    # -- map access -------------------------------------------------------
+    def state(self) -> np.ndarray:
+        out = np.empty((self.rows, self.width), np.int8)
+        with self._lock:
+            check(self._lib.dm_get_state(self._handle(), _vp(out)))
+        return out
+
+    def logodds(self) -> np.ndarray:
+        out = np.empty((self.rows, self.width), np.float32)
+        with self._lock:
+            check(self._lib.dm_get_logodds(self._handle(), _vp(out)))
+        return out
+
+    def set_logodds(self, L):
+        L = np.ascontiguousarray(L, dtype=np.float32).reshape(self.rows, self.width)
+        with self._lock:
+            check(self._lib.dm_set_logodds(self._handle(), _vp(L)))
+
+    def set_state(self, st):
+        st = np.ascontiguousarray(st, dtype=np.int8).reshape(self.rows, self.width)
+        with self._lock:
+            check(self._lib.dm_set_state(self._handle(), _vp(st)))
+
+    def reset(self):
+        with self._lock:
+            check(self._lib.dm_reset(self._handle()))
+
+    def map_image(self) -> np.ndarray:
+        """get_map_image's grayscale pixels (main.py:256-266), rendered on
+        the GPU: uint8 [rows, W], already flipped."""
+        out = np.empty((self.rows, self.width), np.uint8)
+        with self._lock:
+            check(self._lib.dm_map_image(self._handle(), _vp(out)))
+        return out
+
+    # -- frontiers --------------------------------------------------------
+    def frontiers(self, want_mask=False, want_labels=False, cap=1 << 16) -> Frontiers:
+        mask = np.empty((self.rows, self.width), np.uint8) if want_mask else None
+        labels = np.empty((self.rows, self.width), np.int64) if want_labels else None
+        n = ctypes.c_int64(0)
+        with self._lock:
+            while True:
+                buf = (DmCluster * max(1, cap))()
+                rc = self._lib.dm_frontiers(self._handle(), _vp(mask), _vp(labels),
+                                            ctypes.cast(buf, ctypes.c_void_p), cap, ctypes.byref(n))
+                if rc == _ffi.DM_ERR_CAPACITY and n.value > cap:
+                    cap = int(n.value)
+                    continue
+                check(rc)
+                break
+        k = int(n.value)
+        clusters = np.frombuffer(bytes(buf)[: k * ctypes.sizeof(DmCluster)],
+                                 dtype=np.dtype(CLUSTER_DTYPE)).copy()
+        return Frontiers(clusters=clusters, mask=mask, labels=labels)
+
+    # -- sharding support -------------------------------------------------
+    def set_halo(self, before=None, after=None):
+        b = None if before is None else np.ascontiguousarray(before, np.int8)
+        a = None if after is None else np.ascontiguousarray(after, np.int8)
+        with self._lock:
+            check(self._lib.dm_set_halo(self._handle(), _vp(b), _vp(a)))
+
+    def set_halo_device(self, before_ptr: int | None, after_ptr: int | None):
+        with self._lock:
+            check(self._lib.dm_set_halo_device(self._handle(),
+                                               None if before_ptr is None else ctypes.c_void_p(before_ptr),
+                                               None if after_ptr is None else ctypes.c_void_p(after_ptr)))
+
+    def edge_rows(self):
+        first = np.empty(self.width, np.int8)
+        last = np.empty(self.width, np.int8)
+        with self._lock:
+            check(self._lib.dm_get_edge_rows(self._handle(), _vp(first), _vp(last)))
+        return first, last
+
+    def edge_rows_device(self, first_ptr: int, last_ptr: int):
+        with self._lock:
+            check(self._lib.dm_get_edge_rows_device(self._handle(), ctypes.c_void_p(first_ptr),
+                                                    ctypes.c_void_p(last_ptr)))
+
+    def edge_labels(self):
+        first = np.empty(self.width, np.int64)
+        last = np.empty(self.width, np.int64)
+        with self._lock:
+            check(self._lib.dm_get_edge_labels(self._handle(), _vp(first), _vp(last)))
+        return first, last
+
+    # -- checkpoint / streams / profiling ----------------------------------
+    def save(self, path: str):
+        with self._lock:
+            check(self._lib.dm_save(self._handle(), str(path).encode()))
+
+    def load(self, path: str):
+        with self._lock:
+            check(self._lib.dm_load(self._handle(), str(path).encode()))
+
+    def set_stream(self, stream_ptr: int | None):
+        with self._lock:
+            check(self._lib.dm_set_stream(self._handle(),
+                                          None if not stream_ptr else ctypes.c_void_p(stream_ptr)))
+
+    def synchronize(self):
+        with self._lock:
+            check(self._lib.dm_synchronize(self._handle()))
+
+    def profile(self, enable: bool = True):
+        with self._lock:
+            check(self._lib.dm_profile_enable(self._handle(), 1 if enable else 0))
+
+    def profile_read(self) -> dict:
+        cap = 64
+        arr = (_ffi.DmKernelStat * cap)()
+        n = ctypes.c_int32(0)
+        with self._lock:
+            check(self._lib.dm_profile_read(self._handle(), arr, cap, ctypes.byref(n)))
+        return {arr[i].name.decode(): (int(arr[i].launches), float(arr[i].total_ms))
+                for i in range(min(n.value, cap))}
+
+    def profile_reset(self):
+        with self._lock:
+            check(self._lib.dm_profile_reset(self._handle()))

@@ -1,0 +1,229 @@
+"""Row-band sharding of one map over the GPUs of a node.
+
+One process per GPU (torch.distributed; backend "nccl" is RCCL over xGMI on
+ROCm, "gloo" for CPU tests).  Rank r owns rows [row0_r, row0_r + rows_r) of
+the global map, rows_r a multiple of 64 except for the last band.
+
+* Integration is embarrassingly parallel: every rank integrates the scans
+  whose max-range disk reaches its band; libdm clips rays to the band, so
+  cell writes are disjoint and the union of the bands equals a 1-GPU map
+  bit for bit (tests/test_sharded.py).
+* Frontier extraction has the only real exchange steps:
+  1. halo rows: each band's first/last state rows are all-gathered (W bytes
+     per edge) and installed as the neighbours' halos, so the 8-neighbour
+     frontier test sees across band edges;
+  2. label merge: each band's first/last-row labels (band-local min-index
+     labels, int64) are all-gathered; every rank forms the cross-edge
+     equivalence pairs (8-connectivity: x-1, x, x+1) and resolves them with
+     the same connected-components pass, so the global label = min over the
+     component, identical to the 1-GPU result;
+  3. cluster all-gather: per-band (label, size, sum_x, sum_y) records are
+     all-gathered (counts first, then padded records), merged by final
+     label with exact int64 sums, filtered by min_frontier_size and sorted.
+All messages are KB-MB: latency-bound on xGMI, no ring all-reduce needed.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ._ffi import CLUSTER_DTYPE, DM_TILE, DmParams
+from .grid import Frontiers, OccupancyMapper
+
+
+def band_rows(height: int, world_size: int, rank: int):
+    """(row0, rows) of rank's band: equal multiples of 64, last band ragged."""
+    tiles = -(-height // DM_TILE)
+    per = -(-tiles // world_size) * DM_TILE
+    row0 = min(rank * per, height)
+    rows = max(0, min(per, height - row0))
+    return row0, rows
+
+
+def band_params(params: DmParams, world_size: int, rank: int) -> DmParams:
+    bp = DmParams.from_buffer_copy(params)
+    row0, rows = band_rows(int(params.height), world_size, rank)
+    if rows <= 0:
+        raise ValueError(f"rank {rank}: no rows left for this band (height {params.height}, "
+                         f"{world_size} ranks)")
+    bp.band_row0 = row0
+    bp.band_rows = rows
+    bp.min_frontier_size = 1  # the size filter applies to merged, global clusters
+    return bp
+
+
+def resolve_labels(records: list[np.ndarray], edges: list[tuple[np.ndarray, np.ndarray]]):
+    """Union band-local labels across band edges.
+
+    records[r]: int64 [K_r, 4] (label, size, sum_x, sum_y) of band r
+    edges[r]:   (first_row_labels, last_row_labels) int64 [W] of band r
+    Returns (allrec [K,4], uniq labels (sorted), comp id per uniq label,
+    final label per comp id = min label of the component)."""
+    recs = [np.asarray(r, np.int64).reshape(-1, 4) for r in records]
+    allrec = np.concatenate(recs, 0) if recs else np.zeros((0, 4), np.int64)
+    uniq = np.unique(allrec[:, 0])
+    comp = np.arange(uniq.shape[0])
+    pa, pb = [], []
+    for b in range(len(edges) - 1):  # band b's last row vs band b+1's first row
+        last = np.asarray(edges[b][1], np.int64)
+        first = np.asarray(edges[b + 1][0], np.int64)
+        W = last.shape[0]
+        for d in (-1, 0, 1):
+            lo, hi = max(0, -d), min(W, W - d)
+            a = last[lo:hi]
+            c = first[lo + d:hi + d]
+            ok = (a >= 0) & (c >= 0)
+            pa.append(a[ok])
+            pb.append(c[ok])
+    A = np.concatenate(pa) if pa else np.zeros(0, np.int64)
+    B = np.concatenate(pb) if pb else np.zeros(0, np.int64)
+    if A.size and uniq.size:
+        from scipy.sparse import coo_matrix
+        from scipy.sparse.csgraph import connected_components
+
+        ia = np.searchsorted(uniq, A)
+        ib = np.searchsorted(uniq, B)
+        n = uniq.shape[0]
+        g = coo_matrix((np.ones(ia.size, np.int8), (ia, ib)), shape=(n, n))
+        _, comp = connected_components(g, directed=False)
+    ncomp = int(comp.max()) + 1 if comp.size else 0
+    final = np.full(ncomp, np.iinfo(np.int64).max, np.int64)
+    if ncomp:
+        np.minimum.at(final, comp, uniq)
+    return allrec, uniq, comp, final
+
+
+def merge_clusters(records: list[np.ndarray], edges: list[tuple[np.ndarray, np.ndarray]],
+                   params: DmParams, min_size: int) -> np.ndarray:
+    """Merge per-band cluster records into global clusters: a CLUSTER_DTYPE
+    array sorted by label, exact int64 sums."""
+    allrec, uniq, comp, final = resolve_labels(records, edges)
+    if allrec.shape[0] == 0:
+        return np.zeros(0, dtype=np.dtype(CLUSTER_DTYPE))
+    ncomp = final.shape[0]
+    rec_comp = comp[np.searchsorted(uniq, allrec[:, 0])]
+    size = np.zeros(ncomp, np.int64)
+    sx = np.zeros(ncomp, np.int64)
+    sy = np.zeros(ncomp, np.int64)
+    np.add.at(size, rec_comp, allrec[:, 1])
+    np.add.at(sx, rec_comp, allrec[:, 2])
+    np.add.at(sy, rec_comp, allrec[:, 3])
+    keep = size >= max(1, int(min_size))
+    order = np.argsort(final[keep], kind="stable")
+    out = np.zeros(int(keep.sum()), dtype=np.dtype(CLUSTER_DTYPE))
+    out["label"] = final[keep][order]
+    out["size"] = size[keep][order]
+    out["sum_x"] = sx[keep][order]
+    out["sum_y"] = sy[keep][order]
+    # same double formula as libdm / the SPEC: one division, then + 0.5, * res
+    mx = out["sum_x"].astype(np.float64) / out["size"].astype(np.float64)
+    my = out["sum_y"].astype(np.float64) / out["size"].astype(np.float64)
+    out["cx_m"] = params.origin_x + (mx + 0.5) * params.resolution
+    out["cy_m"] = params.origin_y + (my + 0.5) * params.resolution
+    return out
+
+
+def relabel(band_labels: np.ndarray, records, edges) -> np.ndarray:
+    """Band-local label image -> global labels (parity / debug output)."""
+    _, uniq, comp, final = resolve_labels(records, edges)
+    out = band_labels.copy()
+    m = out >= 0
+    if m.any():
+        out[m] = final[comp[np.searchsorted(uniq, out[m])]]
+    return out
+
+
+class ShardedMapper:
+    """A map split in row bands over `world_size` ranks; this object is
+    rank `rank`'s part.  With world_size == 1 it is a plain OccupancyMapper."""
+
+    def __init__(self, params: DmParams, rank: int = 0, world_size: int = 1, device: int = 0,
+                 group=None, band=None):
+        self.params = DmParams.from_buffer_copy(params)
+        self.rank, self.world_size, self.group = rank, world_size, group
+        self.min_size = int(params.min_frontier_size)
+        if world_size == 1:
+            bp = DmParams.from_buffer_copy(params)
+        else:
+            bp = band_params(params, world_size, rank)
+        self.band = band if band is not None else OccupancyMapper(bp, device)
+        self.row0, self.rows = int(bp.band_row0), int(bp.band_rows or params.height)
+        self.W = int(params.width)
+        self._device = None
+        if world_size > 1:
+            import torch.distributed as dist
+
+            self._dist = dist
+            self._nccl = dist.get_backend(group) == "nccl"
+            if self._nccl:
+                import torch
+
+                self._device = torch.device("cuda", device)
+
+    # -- integration ------------------------------------------------------
+    def scan_mask(self, poses) -> np.ndarray:
+        """Scans whose max-range disk reaches this band's rows."""
+        poses = np.asarray(poses, np.float64).reshape(-1, 3)
+        p = self.params
+        reach = float(p.range_max) + 2 * p.resolution
+        y = poses[:, 1]
+        ylo = p.origin_y + self.row0 * p.resolution - reach
+        yhi = p.origin_y + (self.row0 + self.rows) * p.resolution + reach
+        return ~((y < ylo) | (y > yhi))  # NaN poses are kept (libdm skips them)
+
+    def integrate(self, poses, ranges, angle_min, angle_increment):
+        poses = np.asarray(poses, np.float64).reshape(-1, 3)
+        ranges = np.asarray(ranges, np.float32).reshape(poses.shape[0], -1)
+        if self.world_size > 1:
+            keep = self.scan_mask(poses)
+            poses, ranges = poses[keep], ranges[keep]
+        return self.band.integrate(poses, ranges, angle_min, angle_increment)
+
+    # -- frontiers --------------------------------------------------------
+    def _allgather(self, arr: np.ndarray) -> np.ndarray:
+        """all-gather a same-shape array from every rank -> [P, ...]."""
+        import torch
+
+        t = torch.from_numpy(np.ascontiguousarray(arr))
+        if self._nccl:
+            t = t.to(self._device)
+        t = t.reshape(1, -1)
+        out = torch.empty((self.world_size, t.shape[1]), dtype=t.dtype, device=t.device)
+        self._dist.all_gather_into_tensor(out, t, group=self.group)
+        return out.cpu().numpy().reshape((self.world_size,) + arr.shape)
+
+    def exchange_halos(self):
+        first, last = self.band.edge_rows()
+        rows = self._allgather(np.stack([first, last]))
+        before = rows[self.rank - 1, 1] if self.rank > 0 else None
+        after = rows[self.rank + 1, 0] if self.rank + 1 < self.world_size else None
+        self.band.set_halo(before, after)
+
+    def frontiers(self, want_mask=False, want_labels=False) -> Frontiers:
+        if self.world_size == 1:
+            return self.band.frontiers(want_mask=want_mask, want_labels=want_labels)
+        self.exchange_halos()
+        local = self.band.frontiers(want_mask=want_mask, want_labels=want_labels)
+        first, last = self.band.edge_labels()
+        edges = self._allgather(np.stack([first, last]))
+        rec = np.stack([local.clusters["label"], local.clusters["size"], local.clusters["sum_x"],
+                        local.clusters["sum_y"]], 1).astype(np.int64) if len(local) else \
+            np.zeros((0, 4), np.int64)
+        counts = self._allgather(np.array([rec.shape[0]], np.int64))[:, 0]
+        kmax = int(counts.max()) if counts.size else 0
+        pad = np.zeros((kmax, 4), np.int64)
+        pad[:rec.shape[0]] = rec
+        allrec = self._allgather(pad) if kmax else np.zeros((self.world_size, 0, 4), np.int64)
+        records = [allrec[r, :int(counts[r])] for r in range(self.world_size)]
+        merged = merge_clusters(records, [(edges[r, 0], edges[r, 1]) for r in range(self.world_size)],
+                                self.params, self.min_size)
+        labels = None
+        if want_labels and local.labels is not None:
+            labels = relabel(local.labels, records, [(edges[r, 0], edges[r, 1]) for r in range(self.world_size)])
+        return Frontiers(clusters=merged, mask=local.mask, labels=labels)
+
+    def close(self):
+        self.band.close()
+
+
+__all__ = ["ShardedMapper", "band_rows", "band_params", "merge_clusters", "relabel",
+           "resolve_labels"]

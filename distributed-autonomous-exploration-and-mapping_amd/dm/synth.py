@@ -1,0 +1,222 @@
+"""Seeded synthetic worlds, trajectories and LD06-format scans.
+
+Only workload generation (tests and bench.py); not on the hot path.  Scans
+follow the LD06 driver's LaserScan encoding (ToLaserscanMessagePublish,
+ldlidar_stl_ros2_node @0x7f853):
+
+* ``angle_min = 0.0f``, ``angle_max = 6.2831855f``,
+  ``angle_increment = (angle_max - angle_min) / (float)(N - 1)``;
+* range = (float)distance_mm / 1000.0f on a 1 mm grid;
+* no return -> NaN; LD06 ``range_max = 25.0f``, so targets beyond 25 m give NaN;
+* 2 % random dropout -> NaN.
+
+World: axis-aligned rectangles covering ``density`` of the area (2 % by
+default) plus four boundary walls.  Trajectories: random walk of 0.1 m /
+<= 0.1 rad steps (the slam_toolbox gating, slam_config.yaml:37-38).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+LD06_ANGLE_MIN = np.float32(0.0)
+LD06_ANGLE_MAX = np.float32(6.2831855)
+LD06_RANGE_MAX = 25.0
+LD06_RANGE_MIN = np.float32(0.02)
+
+
+def ld06_angle_increment(n_beams: int) -> np.float32:
+    """angle_increment exactly as the driver computes it (float32)."""
+    return np.float32((LD06_ANGLE_MAX - LD06_ANGLE_MIN) / np.float32(n_beams - 1))
+
+
+@dataclass
+class World:
+    rects: np.ndarray  # [K, 4] xmin, ymin, xmax, ymax (metres)
+    xmin: float
+    ymin: float
+    xmax: float
+    ymax: float
+    cell: float = 8.0  # spatial-hash bucket (m)
+
+    def __post_init__(self):
+        self._build_hash()
+
+    def _build_hash(self):
+        c = self.cell
+        self._nx = max(1, int(math.ceil((self.xmax - self.xmin) / c)))
+        self._ny = max(1, int(math.ceil((self.ymax - self.ymin) / c)))
+        buckets: dict[int, list[int]] = {}
+        for k, (x0, y0, x1, y1) in enumerate(self.rects):
+            bx0 = int(np.clip((x0 - self.xmin) // c, 0, self._nx - 1))
+            bx1 = int(np.clip((x1 - self.xmin) // c, 0, self._nx - 1))
+            by0 = int(np.clip((y0 - self.ymin) // c, 0, self._ny - 1))
+            by1 = int(np.clip((y1 - self.ymin) // c, 0, self._ny - 1))
+            for by in range(by0, by1 + 1):
+                for bx in range(bx0, bx1 + 1):
+                    buckets.setdefault(by * self._nx + bx, []).append(k)
+        self._buckets = {k: np.array(v, np.int64) for k, v in buckets.items()}
+
+    def near(self, x: float, y: float, radius: float) -> np.ndarray:
+        c = self.cell
+        bx0 = int(np.clip((x - radius - self.xmin) // c, 0, self._nx - 1))
+        bx1 = int(np.clip((x + radius - self.xmin) // c, 0, self._nx - 1))
+        by0 = int(np.clip((y - radius - self.ymin) // c, 0, self._ny - 1))
+        by1 = int(np.clip((y + radius - self.ymin) // c, 0, self._ny - 1))
+        parts = [self._buckets[b] for by in range(by0, by1 + 1)
+                 for b in range(by * self._nx + bx0, by * self._nx + bx1 + 1) if b in self._buckets]
+        if not parts:
+            return np.zeros(0, np.int64)
+        return np.unique(np.concatenate(parts))
+
+    def occupied(self, x: float, y: float, margin: float = 0.0) -> bool:
+        if not (self.xmin + 0.5 <= x <= self.xmax - 0.5 and self.ymin + 0.5 <= y <= self.ymax - 0.5):
+            return True
+        idx = self.near(x, y, margin + 0.01)
+        if idx.size == 0:
+            return False
+        r = self.rects[idx]
+        return bool(np.any((x >= r[:, 0] - margin) & (x <= r[:, 2] + margin)
+                           & (y >= r[:, 1] - margin) & (y <= r[:, 3] + margin)))
+
+
+def make_world(seed: int, xmin: float, ymin: float, xmax: float, ymax: float,
+               density: float = 0.02, size_lo: float = 0.2, size_hi: float = 1.5,
+               walls: bool = True) -> World:
+    rng = np.random.Generator(np.random.PCG64(seed))
+    area = (xmax - xmin) * (ymax - ymin)
+    mean_area = ((size_lo + size_hi) / 2.0) ** 2
+    k = int(round(density * area / mean_area))
+    w = rng.uniform(size_lo, size_hi, k)
+    h = rng.uniform(size_lo, size_hi, k)
+    cx = rng.uniform(xmin, xmax, k)
+    cy = rng.uniform(ymin, ymax, k)
+    rects = np.stack([cx - w / 2, cy - h / 2, cx + w / 2, cy + h / 2], axis=1)
+    if walls:
+        t = 0.1
+        wall = np.array([
+            [xmin + 0.2, ymin + 0.2, xmax - 0.2, ymin + 0.2 + t],
+            [xmin + 0.2, ymax - 0.2 - t, xmax - 0.2, ymax - 0.2],
+            [xmin + 0.2, ymin + 0.2, xmin + 0.2 + t, ymax - 0.2],
+            [xmax - 0.2 - t, ymin + 0.2, xmax - 0.2, ymax - 0.2],
+        ])
+        rects = np.concatenate([rects, wall], axis=0)
+    return World(rects=rects, xmin=xmin, ymin=ymin, xmax=xmax, ymax=ymax)
+
+
+def ray_distances(world: World, x: float, y: float, theta: np.ndarray,
+                  max_dist: float = LD06_RANGE_MAX) -> np.ndarray:
+    """Exact float64 distance along each ray to the nearest rectangle (inf if
+    none within max_dist)."""
+    idx = world.near(x, y, max_dist)
+    out = np.full(theta.shape, np.inf)
+    if idx.size == 0:
+        return out
+    r = world.rects[idx]
+    # keep rectangles whose nearest point is within max_dist
+    px = np.clip(x, r[:, 0], r[:, 2])
+    py = np.clip(y, r[:, 1], r[:, 3])
+    r = r[(px - x) ** 2 + (py - y) ** 2 <= max_dist * max_dist]
+    if r.shape[0] == 0:
+        return out
+    dx = np.cos(theta)[:, None]
+    dy = np.sin(theta)[:, None]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        inv_x = 1.0 / dx
+        inv_y = 1.0 / dy
+        tx1 = (r[None, :, 0] - x) * inv_x
+        tx2 = (r[None, :, 2] - x) * inv_x
+        ty1 = (r[None, :, 1] - y) * inv_y
+        ty2 = (r[None, :, 3] - y) * inv_y
+        tmin = np.maximum(np.minimum(tx1, tx2), np.minimum(ty1, ty2))
+        tmax = np.minimum(np.maximum(tx1, tx2), np.maximum(ty1, ty2))
+    ok = (tmax >= np.maximum(tmin, 0.0)) & np.isfinite(tmin)
+    t = np.where(ok, np.maximum(tmin, 0.0), np.inf)
+    return t.min(axis=1)
+
+
+def ld06_scan(world: World, x: float, y: float, yaw: float, n_beams: int,
+              rng: np.random.Generator, dropout: float = 0.02) -> np.ndarray:
+    """One LaserScan.ranges array (float32[N]) in the LD06 encoding."""
+    inc = ld06_angle_increment(n_beams)
+    phi = np.float64(LD06_ANGLE_MIN) + np.arange(n_beams, dtype=np.float64) * np.float64(inc)
+    d = ray_distances(world, x, y, yaw + phi)
+    mm = np.round(d * 1000.0)
+    rng_out = np.where(np.isfinite(d) & (d <= LD06_RANGE_MAX),
+                       (mm.astype(np.float32) / np.float32(1000.0)), np.float32(np.nan))
+    rng_out = rng_out.astype(np.float32)
+    drop = rng.random(n_beams) < dropout
+    rng_out[drop] = np.float32(np.nan)
+    # the LD06 publishes distance 0 with intensity 0 as NaN; a 0 mm return
+    # with intensity is a 0.0 range (below range_min, skipped downstream)
+    return rng_out
+
+
+class ScanStream:
+    """n_robots random-walking robots; each next_batch() advances every robot
+    one step and returns their poses (S,3) and scans (S,N)."""
+
+    def __init__(self, world: World, n_robots: int, n_beams: int, seed: int,
+                 step: float = 0.1, turn: float = 0.1, region=None):
+        self.world = world
+        self.n_beams = n_beams
+        self.rng = np.random.Generator(np.random.PCG64(seed))
+        self.step = step
+        self.turn = turn
+        x0, y0, x1, y1 = region if region is not None else (world.xmin, world.ymin,
+                                                             world.xmax, world.ymax)
+        poses = []
+        while len(poses) < n_robots:
+            x = self.rng.uniform(x0 + 1.0, x1 - 1.0)
+            y = self.rng.uniform(y0 + 1.0, y1 - 1.0)
+            if world.occupied(x, y, margin=0.3):
+                continue
+            poses.append([x, y, self.rng.uniform(-math.pi, math.pi)])
+        self.poses = np.array(poses, np.float64)
+
+    def advance(self):
+        for r in range(self.poses.shape[0]):
+            x, y, yaw = self.poses[r]
+            yaw = yaw + self.rng.uniform(-self.turn, self.turn)
+            nx, ny = x + self.step * math.cos(yaw), y + self.step * math.sin(yaw)
+            if self.world.occupied(nx, ny, margin=0.2):
+                yaw += math.pi / 2
+                nx, ny = x, y
+            yaw = math.atan2(math.sin(yaw), math.cos(yaw))
+            self.poses[r] = (nx, ny, yaw)
+
+    def scans(self) -> np.ndarray:
+        return np.stack([ld06_scan(self.world, p[0], p[1], p[2], self.n_beams, self.rng)
+                         for p in self.poses]).astype(np.float32)
+
+    def next_batch(self):
+        self.advance()
+        return self.poses.copy(), self.scans()
+
+
+def config_world(cfg: str, seed: int = 0):
+    """Worlds and map parameters for BASELINE.json configs.
+    Returns (world, width, height, resolution, origin_x, origin_y)."""
+    table = {
+        "C1": (400, 0.05),
+        "C2": (4096, 0.05),
+        "C3": (16384, 0.05),
+        "C4": (32768, 0.05),
+        "C5": (65536, 0.01),
+    }
+    n, res = table[cfg]
+    half = n * res / 2.0
+    world = make_world(seed, -half, -half, half, half)
+    return world, n, n, res, -half, -half
+
+
+def pose4(poses: np.ndarray) -> np.ndarray:
+    """(x, y, yaw) -> (x, y, cos yaw, sin yaw) with the C library's cos/sin
+    (math.cos), the device-resident pose format of dm_integrate_device."""
+    poses = np.asarray(poses, np.float64).reshape(-1, 3)
+    out = np.empty((poses.shape[0], 4), np.float64)
+    for i, (x, y, yaw) in enumerate(poses):
+        out[i] = (x, y, math.cos(yaw), math.sin(yaw))
+    return out

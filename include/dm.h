@@ -1,0 +1,184 @@
+/*
+ * dm.h — C-ABI of libdm.so: MI355X-native occupancy-grid integration and
+ * exploration-frontier extraction (the BASELINE.json north-star hot path).
+ *
+ * WHAT THIS REPLACES
+ *   The reference has no FFI for this path: its boundary is ROS 2 topics.
+ *   `/scan` (sensor_msgs/LaserScan, produced by the LD06 driver's
+ *   ToLaserscanMessagePublish, pi/src/ldlidar_ros2_ws/install/ldlidar_stl_ros2/
+ *   lib/ldlidar_stl_ros2/ldlidar_stl_ros2_node @0x7f853) goes into slam_toolbox
+ *   (launched at server/thymio_project/launch/pc_server.launch.py:12-19,
+ *   configured by server/thymio_project/config/slam_config.yaml:16-28), which
+ *   publishes `/map` (nav_msgs/OccupancyGrid, int8 -1/0/100 row-major) consumed
+ *   by ThymioBrain.map_cb (server/thymio_project/thymio_project/main.py:46,80-81)
+ *   and get_map_image (main.py:241-279).  Frontier extraction exists nowhere in
+ *   the reference; its contract is SURVEY.md §8(a) rows a8-a10.
+ *   Each entry point below names the step of that pipeline it takes over.  The
+ *   ctypes binding a ROS node would add is shown in INTEGRATION.md.
+ *
+ * CONVENTIONS
+ *   - Every function returns int: DM_OK (0) or a negative DM_ERR_* code; on
+ *     error dm_last_error() (thread-local) describes it.  Nothing aborts.
+ *   - Host pointers are caller-owned, C-contiguous, borrowed for the call only.
+ *   - Functions without a `_device` suffix are synchronous: they return after
+ *     their outputs are in host memory.  `_device` functions take device
+ *     pointers, enqueue on the handle's stream and return immediately.
+ *   - A handle is NOT internally thread-safe (the Python wrapper locks).
+ *   - Grid layout: row-major, idx = (cy - band_row0) * width + cx, row 0 at the
+ *     map origin (bottom-left), exactly the OccupancyGrid.data layout read by
+ *     get_map_image (main.py:256, flipud at :266).
+ */
+#ifndef DM_H
+#define DM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DM_OK 0
+#define DM_ERR_INVALID_ARG (-1)
+#define DM_ERR_SHAPE (-2)
+#define DM_ERR_HIP (-3)
+#define DM_ERR_OOM (-4)
+#define DM_ERR_CAPACITY (-5)
+#define DM_ERR_IO (-6)
+#define DM_ERR_STATE (-7)
+
+/* Tile edge (cells) used by the kernels; band_row0 must be a multiple of it. */
+#define DM_TILE 64
+
+/* Map parameters.  Defaults (dm_default_params) come from the reference where
+ * it has them: resolution 0.05 (slam_config.yaml:26), max range 12.0
+ * (slam_config.yaml:27), LD06 range_min 0.02f (driver rodata 0xbc840).  The
+ * log-odds constants are this build's SPEC. */
+typedef struct dm_params {
+  int64_t width;            /* cells along x (columns), global */
+  int64_t height;           /* cells along y (rows), global */
+  double resolution;        /* metres per cell */
+  double origin_x;          /* world x of the lower-left corner of cell (0,0) */
+  double origin_y;          /* world y of the lower-left corner of cell (0,0) */
+  float range_min;          /* beams with r < range_min (or NaN) are skipped */
+  float range_max;          /* r > range_max: ray truncated there, no hit */
+  float l_occ;              /* log-odds added per hit */
+  float l_free;             /* log-odds added per miss (negative) */
+  float l_min;              /* clamp low */
+  float l_max;              /* clamp high */
+  float occ_thresh;         /* L >= occ_thresh (and L != 0) -> 100 */
+  float free_thresh;        /* L <= free_thresh (and L != 0) -> 0 */
+  int64_t min_frontier_size;/* clusters smaller than this are dropped */
+  int64_t band_row0;        /* first global row owned by this handle */
+  int64_t band_rows;        /* rows owned; 0 means height - band_row0 */
+} dm_params;
+
+/* One frontier cluster.  label = min global row-major
+ * linear index (cy*width+cx) of the component; sums are over global cell
+ * coordinates; cx_m = origin_x + ((double)sum_x/(double)size + 0.5)*resolution. */
+typedef struct dm_cluster {
+  int64_t label;
+  int64_t size;
+  int64_t sum_x;
+  int64_t sum_y;
+  double cx_m;
+  double cy_m;
+} dm_cluster;
+
+/* Per-kernel timing collected with HIP events when profiling is enabled. */
+typedef struct dm_kernel_stat {
+  char name[32];
+  uint64_t launches;
+  double total_ms;
+} dm_kernel_stat;
+
+typedef struct dm_grid dm_grid;
+
+/* Fill p with defaults for a width x height map centred on the world origin. */
+int dm_default_params(dm_params* p, int64_t width, int64_t height);
+
+/* Create a grid on HIP device `device`: L = 0, state = -1 everywhere.
+ * Replaces slam_toolbox's map allocation (grid sized from the scan bounding
+ * box on every rebuild upstream; here fixed, device-resident). */
+int dm_create(dm_grid** out, const dm_params* p, int device);
+int dm_destroy(dm_grid* g);
+/* Reset to the empty map (L = 0, state = -1). */
+int dm_reset(dm_grid* g);
+int dm_get_params(const dm_grid* g, dm_params* out);
+
+/* Integrate S scans of N beams.  poses: [S][3] =
+ * (x_m, y_m, yaw_rad) of the laser in the map frame (main.py:202-215 TF chain
+ * + pi_hardware.launch.py:26-30 static offset); ranges: [S][N] metres as
+ * LaserScan.ranges (NaN = no return); beam i angle = angle_min + i*angle_increment
+ * (LaserScan.angle_min / angle_increment).  cos/sin are evaluated on the host
+ * with the C library.  out_updates (may be NULL) receives the number of
+ * in-band beam-cell updates U; out_touched (may be NULL) the touched cells T.
+ * Replaces: slam_toolbox's per-scan ray trace + grid update that produces /map. */
+int dm_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N,
+                 const float* ranges, float angle_min, float angle_increment,
+                 uint64_t* out_updates, uint64_t* out_touched);
+
+/* Device-resident variant (asynchronous on the handle's stream).
+ * d_pose4: [S][4] = (x, y, cos(yaw), sin(yaw)) doubles in device memory;
+ * d_ranges: [S][N] floats in device memory.  Counters for the call are
+ * accumulated on the device; read them with dm_last_counts. */
+int dm_integrate_device(dm_grid* g, int32_t S, const double* d_pose4,
+                        int32_t N, const float* d_ranges, float angle_min,
+                        float angle_increment);
+/* U and T of the most recent integrate call (synchronises the stream). */
+int dm_last_counts(dm_grid* g, uint64_t* updates, uint64_t* touched);
+
+/* OccupancyGrid.data for the band: int8[band_rows*width] (-1 / 0 / 100). */
+int dm_get_state(dm_grid* g, int8_t* out);
+/* Log-odds for the band: float[band_rows*width]. */
+int dm_get_logodds(dm_grid* g, float* out);
+/* Overwrite L (and derived state / tile summaries) from host floats. */
+int dm_set_logodds(dm_grid* g, const float* in);
+/* Same as dm_set_logodds but from a host int8 state image: L := +l_occ for
+ * 100, l_free for 0, 0 for -1 (testing and map import). */
+int dm_set_state(dm_grid* g, const int8_t* in);
+
+/* Frontier extraction: mask (uint8[band_rows*width],
+ * may be NULL), labels (int64[band_rows*width], -1 off-frontier, may be NULL),
+ * clusters sorted by label (capacity cap).  *n_out receives the number of
+ * clusters; if it exceeds cap, DM_ERR_CAPACITY is returned and only cap were
+ * written.  For a band, labels are band-local (the min index within the band's
+ * part of a component); the sharded layer merges them across bands. */
+int dm_frontiers(dm_grid* g, uint8_t* mask, int64_t* labels, dm_cluster* out,
+                 int64_t cap, int64_t* n_out);
+
+/* Sharding support (row bands).  Halo rows are the global
+ * rows band_row0-1 (top, "above" = lower row index) and band_row0+band_rows
+ * (bottom); NULL = no neighbour there.  Host and device variants. */
+int dm_set_halo(dm_grid* g, const int8_t* row_before, const int8_t* row_after);
+int dm_set_halo_device(dm_grid* g, const int8_t* d_row_before,
+                       const int8_t* d_row_after);
+/* Copy the band's first and last state rows (W bytes each). */
+int dm_get_edge_rows(dm_grid* g, int8_t* first_row, int8_t* last_row);
+int dm_get_edge_rows_device(dm_grid* g, int8_t* d_first_row, int8_t* d_last_row);
+/* After dm_frontiers: band-local labels of the first/last rows (int64[W]). */
+int dm_get_edge_labels(dm_grid* g, int64_t* first_row, int64_t* last_row);
+
+/* Checkpoint: raw little-endian {magic, params, float L[band]} . */
+int dm_save(dm_grid* g, const char* path);
+int dm_load(dm_grid* g, const char* path);
+
+/* Streams and profiling. stream is a hipStream_t (NULL = library's own). */
+int dm_set_stream(dm_grid* g, void* stream);
+int dm_synchronize(dm_grid* g);
+int dm_profile_enable(dm_grid* g, int enable);
+int dm_profile_read(dm_grid* g, dm_kernel_stat* out, int32_t cap, int32_t* n_out);
+int dm_profile_reset(dm_grid* g);
+
+/* PNG-ready grayscale image of the band's state (f2, main.py:256-266):
+ * 0 -> 255, 100 -> 0, anything else -> 127, rows flipped (flipud).
+ * out: uint8[band_rows*width]. */
+int dm_map_image(dm_grid* g, uint8_t* out);
+
+const char* dm_last_error(void);
+const char* dm_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DM_H */

@@ -1,0 +1,253 @@
+"""GPU parity: libdm (HIP, gfx950) vs the CPU oracle, bit-exact.
+
+L is compared bit for bit (the north-star tolerance is 1e-5 absolute; the
+SPEC's fixed float32 op order without FMA makes it exact), state / mask /
+labels / cluster integers exactly, centroids exactly (same double formula).
+Run on the GPU box: python -m pytest tests -m gpu
+"""
+import os
+
+import numpy as np
+import pytest
+
+import cases
+import dm
+from golden_io import load_case
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+LOGODDS_ATOL = 1e-5  # north_star; the comparison below is exact, which implies it
+
+
+def assert_map_equal(m, om):
+    L = m.logodds()
+    np.testing.assert_allclose(L, om.L, rtol=0, atol=LOGODDS_ATOL)
+    np.testing.assert_array_equal(L.view(np.uint32), om.L.view(np.uint32))
+    np.testing.assert_array_equal(m.state(), om.state)
+
+
+def assert_frontiers_equal(fr, mask, labels, clusters):
+    if fr.mask is not None:
+        np.testing.assert_array_equal(fr.mask, mask)
+    if fr.labels is not None:
+        np.testing.assert_array_equal(fr.labels, labels)
+    np.testing.assert_array_equal(fr.clusters, clusters)
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return np.load(os.path.join(GOLD, "oracle_golden.npz"))
+
+
+@pytest.mark.parametrize("name", ["tiny64", "c1_room", "ragged", "offgrid"])
+def test_golden_fixture(golden, name):
+    c = load_case(golden, name)
+    with dm.OccupancyMapper(c["params"]) as m:
+        for k, (poses, ranges) in enumerate(c["batches"]):
+            assert m.integrate(poses, ranges, c["amin"], c["inc"]) == tuple(c["counts"][k])
+        L = m.logodds()
+        np.testing.assert_array_equal(L.view(np.uint32), c["L"].view(np.uint32))
+        np.testing.assert_array_equal(m.state(), c["state"])
+        fr = m.frontiers(want_mask=True, want_labels=True)
+        assert_frontiers_equal(fr, c["mask"], c["labels"], c["clusters"])
+
+
+@pytest.mark.parametrize("W,H,S,N,res,seed", [
+    (64, 64, 1, 1, 0.05, 1),
+    (400, 400, 8, 360, 0.05, 2),
+    (130, 70, 5, 500, 0.05, 3),     # W % 4 != 0: scalar apply path, ragged tiles
+    (257, 513, 16, 1024, 0.05, 4),  # ragged tiles in both axes
+    (1000, 300, 32, 4096, 0.02, 5), # 12 m = 600 cells: long rays, many tiles per ray
+    (96, 96, 12, 256, 0.1, 6),      # sensors far outside the map
+])
+def test_random_scans_vs_oracle(oracle_lib, W, H, S, N, res, seed):
+    p = cases.make_params(W, H, resolution=res)
+    om = oracle_lib.OracleMap(p)
+    with dm.OccupancyMapper(p) as m:
+        for k in range(3):
+            poses, ranges, amin, inc = cases.random_scans(seed * 100 + k, p, S, N,
+                                                          spread=4.0 if seed == 6 else 1.0)
+            assert m.integrate(poses, ranges, amin, inc) == om.integrate(poses, ranges, amin, inc)
+        assert_map_equal(m, om)
+        fr = m.frontiers(want_mask=True, want_labels=True)
+        assert_frontiers_equal(fr, *om.frontiers())
+
+
+def test_world_stream_c2_scale(oracle_lib):
+    """C2 geometry (4096^2 @ 5 cm), single robot, scan-by-scan replay."""
+    p, batches, amin, inc = cases.world_case(21, 4096, 4096, 0.05, 1, 450, 30, region_frac=0.05)
+    om = oracle_lib.OracleMap(p)
+    with dm.OccupancyMapper(p) as m:
+        for poses, ranges in batches:
+            assert m.integrate(poses, ranges, amin, inc) == om.integrate(poses, ranges, amin, inc)
+            fr = m.frontiers()
+        assert_map_equal(m, om)
+        assert_frontiers_equal(m.frontiers(want_mask=True, want_labels=True), *om.frontiers())
+        assert len(fr) > 0
+
+
+def test_c3_full_size_batch(oracle_lib):
+    """BASELINE C3 at full size: 16384^2 @ 5 cm, one 64-scan x 4096-beam batch
+    from 64 robots; the oracle does this in seconds."""
+    p, batches, amin, inc = cases.world_case(31, 16384, 16384, 0.05, 64, 4096, 1)
+    om = oracle_lib.OracleMap(p)
+    with dm.OccupancyMapper(p) as m:
+        poses, ranges = batches[0]
+        got = m.integrate(poses, ranges, amin, inc)
+        exp = om.integrate(poses, ranges, amin, inc)
+        assert got == exp and got[0] > 10_000_000
+        assert_map_equal(m, om)
+        fr = m.frontiers()
+        _, _, clusters = om.frontiers(want_mask=False, want_labels=False)
+        np.testing.assert_array_equal(fr.clusters, clusters)
+
+
+@pytest.mark.parametrize("kind,R,W,seed", [("random", 64, 64, 1), ("random", 200, 333, 2),
+                                           ("blob", 700, 650, 3), ("blob", 1, 300, 4),
+                                           ("blob", 300, 1, 5), ("checker", 128, 192, 6),
+                                           ("stripes", 256, 256, 7)])
+def test_frontiers_on_states(oracle_lib, kind, R, W, seed):
+    if kind == "random":
+        st = cases.random_state(seed, R, W)
+    elif kind == "blob":
+        st = cases.blob_state(seed, R, W, n_blobs=40)
+    elif kind == "checker":
+        yy, xx = np.mgrid[0:R, 0:W]
+        st = np.where((yy + xx) % 2 == 0, 0, -1).astype(np.int8)
+    else:  # long diagonal frontier stripes crossing many tiles
+        yy, xx = np.mgrid[0:R, 0:W]
+        st = np.where(((xx + yy) // 3) % 4 == 0, -1, 0).astype(np.int8)
+    p = cases.make_params(W, R)
+    om = oracle_lib.OracleMap(p)
+    om.state[...] = st
+    with dm.OccupancyMapper(p) as m:
+        m.set_state(st)
+        np.testing.assert_array_equal(m.state(), st)
+        fr = m.frontiers(want_mask=True, want_labels=True)
+        assert_frontiers_equal(fr, *om.frontiers())
+
+
+def test_frontier_band_with_halo(oracle_lib):
+    W, H = 300, 640
+    full = cases.blob_state(8, H, W, n_blobs=30)
+    for r0, rows in [(0, 192), (192, 256), (448, 192)]:
+        p = cases.make_params(W, H, band_row0=r0, band_rows=rows)
+        om = oracle_lib.OracleMap(p)
+        om.state[...] = full[r0:r0 + rows]
+        hb = full[r0 - 1] if r0 > 0 else None
+        ha = full[r0 + rows] if r0 + rows < H else None
+        with dm.OccupancyMapper(p) as m:
+            m.set_state(full[r0:r0 + rows])
+            m.set_halo(hb, ha)
+            fr = m.frontiers(want_mask=True, want_labels=True)
+            mask, labels, clusters = om.frontiers(hb, ha)
+            assert_frontiers_equal(fr, mask, labels, clusters)
+            first, last = m.edge_labels()
+            np.testing.assert_array_equal(first, labels[0])
+            np.testing.assert_array_equal(last, labels[-1])
+
+
+def test_edge_cases(oracle_lib):
+    p = cases.make_params(200, 120)
+    om = oracle_lib.OracleMap(p)
+    with dm.OccupancyMapper(p) as m:
+        # empty batch, then empty map: no frontiers
+        assert m.integrate(np.zeros((0, 3)), np.zeros((0, 5), np.float32), 0.0, 0.1) == (0, 0)
+        assert len(m.frontiers()) == 0
+        # all-NaN / too-short ranges: skipped
+        poses = np.array([[0.0, 0.0, 0.3]])
+        for bad in (np.nan, 0.0, 0.019):
+            assert m.integrate(poses, np.full((1, 50), bad, np.float32), 0.0, 0.1) == (0, 0)
+        # single beam, non-finite pose skipped
+        poses = np.array([[0.1, 0.2, 0.0], [np.nan, 0.0, 0.0], [0.0, 0.0, np.inf]])
+        r = np.full((3, 1), 3.0, np.float32)
+        assert m.integrate(poses, r, 0.0, 0.0) == om.integrate(poses, r, 0.0, 0.0)
+        # exactly range_max (hit) and just beyond (truncated, no hit)
+        r = np.array([[12.0, np.nextafter(np.float32(12.0), np.float32(20.0)), np.inf]], np.float32)
+        poses = np.array([[-1.0, 0.5, 0.2]])
+        assert m.integrate(poses, r, 0.1, 2.0) == om.integrate(poses, r, 0.1, 2.0)
+        assert_map_equal(m, om)
+        # saturation: many hits on the same cells clamp at l_max / l_min
+        poses = np.tile(np.array([[0.0, 0.0, 0.0]]), (64, 1))
+        r = np.full((64, 64), 1.0, np.float32)
+        for _ in range(3):
+            assert m.integrate(poses, r, 0.0, 0.01) == om.integrate(poses, r, 0.0, 0.01)
+        assert_map_equal(m, om)
+        assert m.logodds().max() == np.float32(3.5) and m.logodds().min() == np.float32(-2.0)
+        assert_frontiers_equal(m.frontiers(want_mask=True, want_labels=True), *om.frontiers())
+
+
+def test_deterministic_and_order_independent(oracle_lib):
+    p = cases.make_params(512, 512)
+    poses, ranges, amin, inc = cases.random_scans(77, p, 32, 1024)
+    perm = np.random.Generator(np.random.PCG64(1)).permutation(32)
+    outs = []
+    for order in (np.arange(32), np.arange(32), perm):
+        with dm.OccupancyMapper(p) as m:
+            m.integrate(poses[order], ranges[order], amin, inc)
+            outs.append((m.logodds(), m.state(), m.frontiers(want_labels=True)))
+    for L, st, fr in outs[1:]:
+        np.testing.assert_array_equal(L.view(np.uint32), outs[0][0].view(np.uint32))
+        np.testing.assert_array_equal(st, outs[0][1])
+        np.testing.assert_array_equal(fr.labels, outs[0][2].labels)
+        np.testing.assert_array_equal(fr.clusters, outs[0][2].clusters)
+
+
+def test_device_entry_point_matches_host(oracle_lib):
+    import torch
+
+    p = cases.make_params(640, 480)
+    poses, ranges, amin, inc = cases.random_scans(5, p, 16, 720)
+    from dm import synth
+    pose4 = torch.from_numpy(synth.pose4(poses)).cuda()
+    rng_d = torch.from_numpy(ranges).cuda()
+    om = oracle_lib.OracleMap(p)
+    exp = om.integrate(poses, ranges, amin, inc)
+    with dm.OccupancyMapper(p) as m:
+        torch.cuda.synchronize()
+        m.integrate_device(pose4.data_ptr(), 16, rng_d.data_ptr(), 720, amin, inc)
+        assert m.last_counts() == exp
+        assert_map_equal(m, om)
+
+
+def test_checkpoint_roundtrip(tmp_path, oracle_lib):
+    p = cases.make_params(300, 200)
+    poses, ranges, amin, inc = cases.random_scans(9, p, 8, 300)
+    with dm.OccupancyMapper(p) as a:
+        a.integrate(poses, ranges, amin, inc)
+        a.save(str(tmp_path / "m.dmap"))
+        poses2, ranges2, _, _ = cases.random_scans(10, p, 8, 300)
+        a.integrate(poses2, ranges2, amin, inc)
+        with dm.OccupancyMapper(p) as b:
+            b.load(str(tmp_path / "m.dmap"))
+            b.integrate(poses2, ranges2, amin, inc)
+            np.testing.assert_array_equal(a.logodds().view(np.uint32), b.logodds().view(np.uint32))
+            np.testing.assert_array_equal(a.frontiers().clusters, b.frontiers().clusters)
+    with dm.OccupancyMapper(cases.make_params(100, 100)) as c:
+        with pytest.raises(dm.DmError):
+            c.load(str(tmp_path / "m.dmap"))
+
+
+def test_map_image_matches_reference_golden():
+    d = np.load(os.path.join(GOLD, "map_image_golden.npz"))
+    n = len([k for k in d.files if k.startswith("state_")])
+    for i in range(n):
+        st = d[f"state_{i}"]
+        with dm.OccupancyMapper(cases.make_params(st.shape[1], st.shape[0])) as m:
+            m.set_state(np.where(np.isin(st, (-1, 0, 100)), st, -1).astype(np.int8))
+            img = m.map_image()
+        exp = d[f"image_{i}"]
+        ok = np.isin(st, (-1, 0, 100))  # set_state stores only the three states
+        np.testing.assert_array_equal(img[np.flipud(ok)], exp[np.flipud(ok)])
+
+
+def test_profiling_counters():
+    p = cases.make_params(256, 256)
+    poses, ranges, amin, inc = cases.random_scans(3, p, 4, 256)
+    with dm.OccupancyMapper(p) as m:
+        m.profile(True)
+        m.integrate(poses, ranges, amin, inc)
+        m.frontiers()
+        st = m.profile_read()
+    assert st["tile_apply"][0] == 1 and st["tile_apply"][1] > 0
+    assert "frontier_tile" in st
