@@ -29,117 +29,15 @@ constexpr int kApplyThreads = 256;
 constexpr int kLdsPitch = DM_TS + 1;  // +1 dword: y-major pieces hit distinct banks
 
 struct Geom {
-  int32_t W, R, row0, TX, TY;
+  RayGeom r;
   int32_t act_cap;
   int64_t seg_cap;
-};
-
-struct PrepArgs {
-  int32_t S, N;
-  double ox, oy, res;
-  float range_min, range_max;
+  int64_t nb;  // beams in this call
 };
 
 __device__ inline int lane_id() { return __lane_id(); }
 
-// Enumerate the pieces of a beam's line that fall in in-band tiles, in order
-// of k.  emit(tile, k0, k1).  Closed form: the major coordinate moves one cell
-// per k, the minor one is monotone, so the k at which each coordinate leaves
-// its tile is computed exactly.
-template <class Emit>
-__device__ inline void for_each_piece(const Beam& b, const Geom& g, Emit&& emit) {
-  const int32_t n = b.n;
-  const int32_t off_a = b.xmajor ? 0 : g.row0;
-  const int32_t off_b = b.xmajor ? g.row0 : 0;
-  const int32_t lim_a = b.xmajor ? g.TX : g.TY;
-  const int32_t lim_b = b.xmajor ? g.TY : g.TX;
-  int32_t k = 0;
-  // iteration cap: every pass advances k by >= 1 and crosses a tile edge or
-  // ends the line, so (n/64 + 2) + (adb/64 + 2) passes suffice
-  const int32_t max_iter = 2 * (n / DM_TS) + 8;
-  for (int32_t it = 0; k <= n && it < max_iter; ++it) {
-    const int32_t q = n > 0 ? dm_udiv(2 * k * b.adb + n, 2 * n, b.rden) : 0;
-    const int32_t ma = b.sa + k * b.ia - off_a;
-    const int32_t mb = b.sb + b.ib * q - off_b;
-    const int32_t ta = (int32_t)dm_floordiv(ma, DM_TS);
-    const int32_t tb = (int32_t)dm_floordiv(mb, DM_TS);
-    int64_t ka;
-    if (b.ia > 0) ka = (int64_t)k + (DM_TS * (ta + 1) - ma);
-    else if (b.ia < 0) ka = (int64_t)k + (ma - DM_TS * ta) + 1;
-    else ka = (int64_t)n + 1;
-    int64_t kb;
-    if (b.ib == 0) {
-      kb = (int64_t)n + 1;
-    } else {
-      const int64_t Q = (int64_t)q + (b.ib > 0 ? (DM_TS * (tb + 1) - mb) : (mb - DM_TS * tb) + 1);
-      const int64_t num = (int64_t)n * (2 * Q - 1);
-      const int64_t den = 2 * (int64_t)b.adb;
-      kb = (num + den - 1) / den;
-    }
-    int64_t ke = ka < kb ? ka : kb;
-    if (ke > (int64_t)n + 1) ke = (int64_t)n + 1;
-    ke -= 1;
-    if (ta >= 0 && ta < lim_a && tb >= 0 && tb < lim_b) {
-      const int32_t tx = b.xmajor ? ta : tb;
-      const int32_t ty = b.xmajor ? tb : ta;
-      emit(ty * g.TX + tx, k, (int32_t)ke);
-    }
-    k = (int32_t)ke + 1;
-  }
-}
-
-// SPEC a4: endpoint cells of beam (s, i).  Double precision, every product
-// rounded separately (compiled with -ffp-contract=off), glibc cos/sin of the
-// beam angle table and of the scan yaw come from the host.
-__device__ inline Beam make_beam(const PrepArgs& a, const double* pose4, const float* ranges,
-                                 const double* trig, int32_t s, int32_t i) {
-  Beam bm;
-  bm.sa = bm.sb = bm.n = bm.adb = 0;
-  bm.ia = bm.ib = 0;
-  bm.xmajor = 1;
-  bm.flags = 0;
-  bm.pad = 0;
-  bm.rden = 0.0;
-  const double x = pose4[4 * s + 0], y = pose4[4 * s + 1];
-  const double cyaw = pose4[4 * s + 2], syaw = pose4[4 * s + 3];
-  const float r = ranges[(int64_t)s * a.N + i];
-  if (!(isfinite(x) && isfinite(y) && isfinite(cyaw) && isfinite(syaw))) return bm;
-  if (!(r >= a.range_min)) return bm;
-  const bool hit = r <= a.range_max;
-  const double rr = hit ? (double)r : (double)a.range_max;
-  const double cphi = trig[2 * i], sphi = trig[2 * i + 1];
-  const double a1 = cyaw * cphi;
-  const double a2 = syaw * sphi;
-  const double dcx = a1 - a2;
-  const double b1 = syaw * cphi;
-  const double b2 = cyaw * sphi;
-  const double dcy = b1 + b2;
-  const double t1 = rr * dcx;
-  const double ex = x + t1;
-  const double t2 = rr * dcy;
-  const double ey = y + t2;
-  const double fsx = floor((x - a.ox) / a.res);
-  const double fsy = floor((y - a.oy) / a.res);
-  const double fex = floor((ex - a.ox) / a.res);
-  const double fey = floor((ey - a.oy) / a.res);
-  const double lim = 1073741824.0;
-  if (!(fabs(fsx) < lim && fabs(fsy) < lim && fabs(fex) < lim && fabs(fey) < lim)) return bm;
-  const int32_t sx = (int32_t)fsx, sy = (int32_t)fsy, ex_c = (int32_t)fex, ey_c = (int32_t)fey;
-  const int32_t dx = ex_c - sx, dy = ey_c - sy;
-  const int32_t adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
-  const int8_t ix = dx > 0 ? 1 : (dx < 0 ? -1 : 0);
-  const int8_t iy = dy > 0 ? 1 : (dy < 0 ? -1 : 0);
-  if (adx >= ady) {
-    bm.xmajor = 1; bm.sa = sx; bm.sb = sy; bm.n = adx; bm.adb = ady; bm.ia = ix; bm.ib = iy;
-  } else {
-    bm.xmajor = 0; bm.sa = sy; bm.sb = sx; bm.n = ady; bm.adb = adx; bm.ia = iy; bm.ib = ix;
-  }
-  bm.rden = bm.n > 0 ? 1.0 / (double)(2 * bm.n) : 0.0;
-  bm.flags = (uint8_t)(1u | (hit ? 2u : 0u));
-  return bm;
-}
-
-__global__ __launch_bounds__(256) void k_beam_prep(PrepArgs a, Geom g, const double* __restrict__ pose4,
+__global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const double* __restrict__ pose4,
                                                    const float* __restrict__ ranges,
                                                    const double* __restrict__ trig,
                                                    Beam* __restrict__ beams, int32_t* tile_count,
@@ -149,32 +47,19 @@ __global__ __launch_bounds__(256) void k_beam_prep(PrepArgs a, Geom g, const dou
   const int64_t nb = (int64_t)a.S * a.N;
   if (b >= nb) return;
   const int32_t s = (int32_t)(b / a.N), i = (int32_t)(b % a.N);
-  const Beam bm = make_beam(a, pose4, ranges, trig, s, i);
+  const Beam bm = dm_make_beam(a, pose4, ranges, trig, s, i);
   beams[b] = bm;
   if (!(bm.flags & 1)) return;
-  const int lane = lane_id();
-  for_each_piece(bm, g, [&](int32_t tile, int32_t, int32_t) {
-    // wave-aggregated increment: one atomic per distinct tile among the
-    // lanes emitting now (neighbouring beams share tiles)
-    while (true) {
-      const unsigned long long act = __ballot(1);
-      const int leader = __ffsll(act) - 1;
-      const int32_t lt = __shfl(tile, leader);
-      if (tile == lt) {
-        const unsigned long long m = __ballot(1);
-        if (lane == leader) {
-          const int32_t old = atomicAdd(&tile_count[lt], (int32_t)__popcll(m));
-          if (old == 0) {
-            const unsigned long long slot = atomicAdd(&cnt[CNT_ACTIVE], 1ull);
-            if (slot < (unsigned long long)g.act_cap) {
-              act_tiles[slot] = lt;
-              tile_slot[lt] = (int32_t)slot;
-            } else {
-              atomicOr(&cnt[CNT_OVERFLOW], 1ull);
-            }
-          }
-        }
-        break;
+  dm_for_each_piece(bm, g.r, [&](int32_t tile, int32_t, int32_t) {
+    const int32_t old = atomicAdd(&tile_count[tile], 1);
+    if (old == 0) {
+      const unsigned long long slot = atomicAdd(&cnt[CNT_ACTIVE], 1ull);
+      if (slot < (unsigned long long)g.act_cap) {
+        act_tiles[slot] = tile;
+        tile_slot[tile] = (int32_t)slot;
+      } else {
+        tile_slot[tile] = -1;
+        atomicOr(&cnt[CNT_OVERFLOW], 1ull);
       }
     }
   });
@@ -215,7 +100,7 @@ __global__ __launch_bounds__(1024) void k_scan_active(Geom g, const int32_t* __r
   }
 }
 
-__global__ __launch_bounds__(256) void k_scatter(PrepArgs a, Geom g, const Beam* __restrict__ beams,
+__global__ __launch_bounds__(256) void k_scatter(RayArgs a, Geom g, const Beam* __restrict__ beams,
                                                  const int32_t* __restrict__ tile_slot,
                                                  int32_t* act_cur, Seg* __restrict__ segs,
                                                  unsigned long long* cnt) {
@@ -224,33 +109,17 @@ __global__ __launch_bounds__(256) void k_scatter(PrepArgs a, Geom g, const Beam*
   if (b >= nb) return;
   const Beam bm = beams[b];
   if (!(bm.flags & 1)) return;
-  const int lane = lane_id();
-  for_each_piece(bm, g, [&](int32_t tile, int32_t k0, int32_t k1) {
-    while (true) {
-      const unsigned long long act = __ballot(1);
-      const int leader = __ffsll(act) - 1;
-      const int32_t lt = __shfl(tile, leader);
-      if (tile == lt) {
-        const unsigned long long m = __ballot(1);
-        int32_t base = 0;
-        if (lane == leader) {
-          const int32_t slot = tile_slot[lt];
-          base = atomicAdd(&act_cur[slot], (int32_t)__popcll(m));
-        }
-        base = __shfl(base, leader);
-        const int32_t rank = (int32_t)__popcll(m & ((1ull << lane) - 1ull));
-        const int64_t idx = (int64_t)base + rank;
-        if (idx < g.seg_cap) {
-          Seg sg;
-          sg.beam = (uint32_t)b;
-          sg.k0 = (uint16_t)k0;
-          sg.k1 = (uint16_t)k1;
-          segs[idx] = sg;
-        } else {
-          atomicOr(&cnt[CNT_OVERFLOW], 2ull);
-        }
-        break;
-      }
+  dm_for_each_piece(bm, g.r, [&](int32_t tile, int32_t k0, int32_t k1) {
+    const int32_t slot = tile_slot[tile];
+    const int64_t idx = (slot >= 0 && slot < g.act_cap) ? (int64_t)atomicAdd(&act_cur[slot], 1) : -1;
+    if (idx >= 0 && idx < g.seg_cap) {
+      Seg sg;
+      sg.beam = (uint32_t)b;
+      sg.k0 = (uint16_t)k0;
+      sg.k1 = (uint16_t)k1;
+      segs[idx] = sg;
+    } else {
+      atomicOr(&cnt[CNT_OVERFLOW], 2ull);
     }
   });
 }
@@ -296,21 +165,19 @@ __global__ __launch_bounds__(kApplyThreads) void k_tile_apply(
     for (int e = tid; e < DM_TS * kLdsPitch; e += kApplyThreads) { hit[e] = 0u; miss[e] = 0u; }
     if (tid == 0) { sh_free = 0; sh_T = 0; sh_U = 0u; }
     __syncthreads();
-    const int32_t tx0 = (tile % g.TX) * DM_TS;
-    const int32_t ty0 = (tile / g.TX) * DM_TS;  // band-local
+    const int32_t tx0 = (tile % g.r.TX) * DM_TS;
+    const int32_t ty0 = (tile / g.r.TX) * DM_TS;  // band-local
     uint32_t myU = 0;
     for (int32_t sidx = off + wid; sidx < off + count; sidx += kApplyThreads / 64) {
       const Seg sg = segs[sidx];
+      if ((int64_t)sg.beam >= g.nb) continue;  // cannot happen; keeps a logic error in-bounds
       const Beam bm = beams[sg.beam];
       const int32_t k = (int32_t)sg.k0 + lane;
       if (k <= (int32_t)sg.k1) {
-        const int32_t q = bm.n > 0 ? dm_udiv(2 * k * bm.adb + bm.n, 2 * bm.n, bm.rden) : 0;
-        const int32_t ma = bm.sa + k * bm.ia;
-        const int32_t mb = bm.sb + bm.ib * q;
-        const int32_t x = bm.xmajor ? ma : mb;
-        const int32_t yl = (bm.xmajor ? mb : ma) - g.row0;
+        int32_t x, yl;
+        dm_cell(bm, k, g.r.row0, &x, &yl);
         const int32_t lx = x - tx0, ly = yl - ty0;
-        if (x >= 0 && x < g.W && yl >= 0 && yl < g.R && (uint32_t)lx < DM_TS && (uint32_t)ly < DM_TS) {
+        if (x >= 0 && x < g.r.W && yl >= 0 && yl < g.r.R && (uint32_t)lx < DM_TS && (uint32_t)ly < DM_TS) {
           const bool is_hit = (k == bm.n) && (bm.flags & 2);
           atomicAdd(is_hit ? &hit[ly * kLdsPitch + lx] : &miss[ly * kLdsPitch + lx], 1u);
           ++myU;
@@ -324,7 +191,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_tile_apply(
     for (int rr = 0; rr < DM_TS / 16; ++rr) {
       const int ly = (tid >> 4) + 16 * rr;
       const int64_t gy = ty0 + ly;
-      if (gy >= g.R) break;
+      if (gy >= g.r.R) break;
       uint32_t h4[4], m4[4];
       bool any = false;
       for (int e = 0; e < 4; ++e) {
@@ -333,8 +200,8 @@ __global__ __launch_bounds__(kApplyThreads) void k_tile_apply(
         any |= (h4[e] | m4[e]) != 0u;
       }
       if (!any) continue;
-      const int64_t base = gy * (int64_t)g.W + tx0 + cx;
-      if (vec_ok && tx0 + cx + 4 <= g.W) {
+      const int64_t base = gy * (int64_t)g.r.W + tx0 + cx;
+      if (vec_ok && tx0 + cx + 4 <= g.r.W) {
         float4 l4 = *reinterpret_cast<const float4*>(L + base);
         char4 s4 = *reinterpret_cast<const char4*>(state + base);
         float lv[4] = {l4.x, l4.y, l4.z, l4.w};
@@ -352,7 +219,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_tile_apply(
       } else {
         for (int e = 0; e < 4; ++e) {
           if ((h4[e] | m4[e]) == 0u) continue;
-          if (tx0 + cx + e >= g.W) continue;
+          if (tx0 + cx + e >= g.r.W) continue;
           const int8_t old = state[base + e];
           const float nl = apply_one(p, L[base + e], h4[e], m4[e]);
           const int8_t ns = state_of(p, nl);
@@ -382,14 +249,14 @@ __global__ __launch_bounds__(kApplyThreads) void k_tile_apply(
 __global__ __launch_bounds__(256) void k_recount(Geom g, const int8_t* __restrict__ state,
                                                  int32_t* __restrict__ tile_free) {
   const int64_t tile = blockIdx.x;
-  const int32_t tx0 = (int32_t)(tile % g.TX) * DM_TS, ty0 = (int32_t)(tile / g.TX) * DM_TS;
+  const int32_t tx0 = (int32_t)(tile % g.r.TX) * DM_TS, ty0 = (int32_t)(tile / g.r.TX) * DM_TS;
   __shared__ int32_t acc;
   if (threadIdx.x == 0) acc = 0;
   __syncthreads();
   int32_t c = 0;
   for (int e = threadIdx.x; e < DM_TS * DM_TS; e += 256) {
     const int32_t x = tx0 + (e & 63), y = ty0 + (e >> 6);
-    if (x < g.W && y < g.R) c += state[(int64_t)y * g.W + x] == 0;
+    if (x < g.r.W && y < g.r.R) c += state[(int64_t)y * g.r.W + x] == 0;
   }
   if (c) atomicAdd(&acc, c);
   __syncthreads();
@@ -429,13 +296,14 @@ __global__ __launch_bounds__(256) void k_map_image(int64_t R, int64_t W, const i
 
 Geom make_geom(const dm_grid* g) {
   Geom ge;
-  ge.W = (int32_t)g->W;
-  ge.R = (int32_t)g->R;
-  ge.row0 = (int32_t)g->row0;
-  ge.TX = (int32_t)g->TX;
-  ge.TY = (int32_t)g->TY;
+  ge.r.W = (int32_t)g->W;
+  ge.r.R = (int32_t)g->R;
+  ge.r.row0 = (int32_t)g->row0;
+  ge.r.TX = (int32_t)g->TX;
+  ge.r.TY = (int32_t)g->TY;
   ge.act_cap = (int32_t)g->act_cap;
   ge.seg_cap = g->segs_cap;
+  ge.nb = 0;
   return ge;
 }
 
@@ -464,7 +332,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   const int64_t nb = (int64_t)S * N;
   DM_HIP(hipMemsetAsync(g->cnt, 0, sizeof(unsigned long long) * CNT_N, g->stream));
   if (nb == 0) return DM_OK;
-  PrepArgs a;
+  RayArgs a;
   a.S = S;
   a.N = N;
   a.ox = g->p.origin_x;
@@ -472,7 +340,8 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   a.res = g->p.resolution;
   a.range_min = g->p.range_min;
   a.range_max = g->p.range_max;
-  const Geom ge = make_geom(g);
+  Geom ge = make_geom(g);
+  ge.nb = nb;
   const int nblk = (int)((nb + 255) / 256);
   KernelTimer t;
   dm_timer_begin(g, "beam_prep", &t);

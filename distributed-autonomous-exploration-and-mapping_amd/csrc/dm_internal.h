@@ -20,22 +20,7 @@
 
 #include "../../include/dm.h"
 
-#define DM_TS 64  // tile edge; == DM_TILE
-
-// Bresenham parameters of one beam, in global cell coordinates.  The line is
-// parametrised along its major axis: cell k (0..n) has
-//   major = sa + k*ia,  minor = sb + ib * floor((2*k*adb + n) / (2*n))
-// (n = |d major| > 0), or just (sa, sb) for n == 0.  SPEC a5.
-struct Beam {
-  int32_t sa, sb;   // start cell, major / minor axis
-  int32_t n, adb;   // |d major|, |d minor|
-  int8_t ia, ib;    // unit steps along major / minor
-  uint8_t xmajor;   // 1 if major axis is x
-  uint8_t flags;    // bit0 valid, bit1 hit
-  int32_t pad;
-  double rden;      // 1.0 / (2n), 0 for n == 0
-};
-static_assert(sizeof(Beam) == 32, "Beam layout");
+#include "dm_ray.h"
 
 // One ray piece inside one tile: cells k0..k1 of beam `beam`.
 struct Seg {
@@ -117,22 +102,6 @@ struct dm_grid {
   std::vector<KernelTimer> pending;
   std::vector<dm_kernel_stat> stats;
 };
-
-// ---- device helpers ------------------------------------------------------
-__host__ __device__ inline int64_t dm_floordiv(int64_t a, int64_t b) {
-  int64_t q = a / b;
-  if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
-  return q;
-}
-
-// floor(num / den) for 0 <= num < 2^31, den > 0, via a double reciprocal and
-// one integer correction (exact).
-__device__ inline int32_t dm_udiv(int32_t num, int32_t den, double rden) {
-  int32_t q = (int32_t)((double)num * rden);
-  if ((int64_t)(q + 1) * den <= num) ++q;
-  else if ((int64_t)q * den > num) --q;
-  return q;
-}
 
 // ---- launchers (dm_integrate.hip / dm_frontier.hip) -----------------------
 int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,

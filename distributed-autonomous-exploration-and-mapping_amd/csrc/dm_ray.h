@@ -1,0 +1,168 @@
+// dm_ray.h — per-beam geometry shared by the HIP kernels (dm_integrate.hip)
+// and the host-side emulation used by the CPU tests (tests/native/).
+//
+// SPEC a4 (endpoint cells) and a5 (closed-form Bresenham) of SURVEY.md §8(a),
+// restated in DESIGN.md §2; compiled with -ffp-contract=off everywhere.
+#pragma once
+
+#include <math.h>
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define DM_HD __host__ __device__
+#else
+#define DM_HD
+#endif
+
+#define DM_TS 64  // tile edge; == DM_TILE of include/dm.h
+
+// Bresenham parameters of one beam, in global cell coordinates.  The line is
+// parametrised along its major axis: cell k (0..n) has
+//   major = sa + k*ia,  minor = sb + ib * floor((2*k*adb + n) / (2*n))
+// (n = |d major| > 0), or just (sa, sb) for n == 0.
+struct Beam {
+  int32_t sa, sb;   // start cell, major / minor axis
+  int32_t n, adb;   // |d major|, |d minor|
+  int8_t ia, ib;    // unit steps along major / minor
+  uint8_t xmajor;   // 1 if major axis is x
+  uint8_t flags;    // bit0 valid, bit1 hit
+  int32_t pad;
+  double rden;      // 1.0 / (2n), 0 for n == 0
+};
+static_assert(sizeof(Beam) == 32, "Beam layout");
+
+struct RayGeom {
+  int32_t W, R, row0, TX, TY;
+};
+
+struct RayArgs {
+  int32_t S, N;
+  double ox, oy, res;
+  float range_min, range_max;
+};
+
+DM_HD inline int32_t dm_floordiv32(int32_t a, int32_t b) {
+  int32_t q = a / b;
+  if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+  return q;
+}
+
+// floor(num / den) for 0 <= num < 2^31, den > 0, rden = 1.0/den: a double
+// estimate, then one exact integer correction.
+DM_HD inline int32_t dm_udiv(int32_t num, int32_t den, double rden) {
+  int32_t q = (int32_t)((double)num * rden);
+  if ((int64_t)(q + 1) * den <= num) ++q;
+  else if ((int64_t)q * den > num) --q;
+  return q;
+}
+
+// minor-axis step count of cell k
+DM_HD inline int32_t dm_minor_steps(const Beam& b, int32_t k) {
+  return b.n > 0 ? dm_udiv(2 * k * b.adb + b.n, 2 * b.n, b.rden) : 0;
+}
+
+// SPEC a4: endpoint cells of beam (s, i).  Double precision, every product
+// rounded separately, C-library cos/sin of the beam angle table (trig) and of
+// the scan yaw (pose4[2..3]) computed on the host.
+DM_HD inline Beam dm_make_beam(const RayArgs& a, const double* pose4, const float* ranges,
+                               const double* trig, int32_t s, int32_t i) {
+  Beam bm;
+  bm.sa = bm.sb = bm.n = bm.adb = 0;
+  bm.ia = bm.ib = 0;
+  bm.xmajor = 1;
+  bm.flags = 0;
+  bm.pad = 0;
+  bm.rden = 0.0;
+  const double x = pose4[4 * s + 0], y = pose4[4 * s + 1];
+  const double cyaw = pose4[4 * s + 2], syaw = pose4[4 * s + 3];
+  const float r = ranges[(int64_t)s * a.N + i];
+  if (!(isfinite(x) && isfinite(y) && isfinite(cyaw) && isfinite(syaw))) return bm;
+  if (!(r >= a.range_min)) return bm;
+  const bool hit = r <= a.range_max;
+  const double rr = hit ? (double)r : (double)a.range_max;
+  const double cphi = trig[2 * i], sphi = trig[2 * i + 1];
+  const double a1 = cyaw * cphi;
+  const double a2 = syaw * sphi;
+  const double dcx = a1 - a2;
+  const double b1 = syaw * cphi;
+  const double b2 = cyaw * sphi;
+  const double dcy = b1 + b2;
+  const double t1 = rr * dcx;
+  const double ex = x + t1;
+  const double t2 = rr * dcy;
+  const double ey = y + t2;
+  const double fsx = floor((x - a.ox) / a.res);
+  const double fsy = floor((y - a.oy) / a.res);
+  const double fex = floor((ex - a.ox) / a.res);
+  const double fey = floor((ey - a.oy) / a.res);
+  const double lim = 1073741824.0;
+  if (!(fabs(fsx) < lim && fabs(fsy) < lim && fabs(fex) < lim && fabs(fey) < lim)) return bm;
+  const int32_t sx = (int32_t)fsx, sy = (int32_t)fsy, ex_c = (int32_t)fex, ey_c = (int32_t)fey;
+  const int32_t dx = ex_c - sx, dy = ey_c - sy;
+  const int32_t adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
+  const int8_t ix = dx > 0 ? 1 : (dx < 0 ? -1 : 0);
+  const int8_t iy = dy > 0 ? 1 : (dy < 0 ? -1 : 0);
+  if (adx >= ady) {
+    bm.xmajor = 1; bm.sa = sx; bm.sb = sy; bm.n = adx; bm.adb = ady; bm.ia = ix; bm.ib = iy;
+  } else {
+    bm.xmajor = 0; bm.sa = sy; bm.sb = sx; bm.n = ady; bm.adb = adx; bm.ia = iy; bm.ib = ix;
+  }
+  bm.rden = bm.n > 0 ? 1.0 / (double)(2 * bm.n) : 0.0;
+  bm.flags = (uint8_t)(1u | (hit ? 2u : 0u));
+  return bm;
+}
+
+// Enumerate the pieces of a beam's line that fall in in-band tiles, in order
+// of k: emit(tile, k0, k1).  The major coordinate moves one cell per k and
+// the minor one is monotone in k, so the k at which each coordinate leaves
+// its tile is exact integer arithmetic.  Every pass advances
+// k by >= 1; the pass cap only guards against a logic error.
+template <class Emit>
+DM_HD inline void dm_for_each_piece(const Beam& b, const RayGeom& g, Emit&& emit) {
+  const int32_t n = b.n;
+  const int32_t off_a = b.xmajor ? 0 : g.row0;
+  const int32_t off_b = b.xmajor ? g.row0 : 0;
+  const int32_t lim_a = b.xmajor ? g.TX : g.TY;
+  const int32_t lim_b = b.xmajor ? g.TY : g.TX;
+  const int32_t max_iter = 2 * (n / DM_TS) + 8;
+  int32_t k = 0;
+  for (int32_t it = 0; k <= n && it < max_iter; ++it) {
+    const int32_t q = dm_minor_steps(b, k);
+    const int32_t ma = b.sa + k * b.ia - off_a;
+    const int32_t mb = b.sb + b.ib * q - off_b;
+    const int32_t ta = dm_floordiv32(ma, DM_TS);
+    const int32_t tb = dm_floordiv32(mb, DM_TS);
+    int64_t ka;
+    if (b.ia > 0) ka = (int64_t)k + (DM_TS * (ta + 1) - ma);
+    else if (b.ia < 0) ka = (int64_t)k + (ma - DM_TS * ta) + 1;
+    else ka = (int64_t)n + 1;
+    int64_t kb;
+    if (b.ib == 0) {
+      kb = (int64_t)n + 1;
+    } else {
+      const int64_t Q = (int64_t)q + (b.ib > 0 ? (DM_TS * (tb + 1) - mb) : (mb - DM_TS * tb) + 1);
+      const int64_t num = (int64_t)n * (2 * Q - 1);
+      const int64_t den = 2 * (int64_t)b.adb;
+      kb = (num + den - 1) / den;
+    }
+    int64_t ke = ka < kb ? ka : kb;
+    if (ke > (int64_t)n + 1) ke = (int64_t)n + 1;
+    ke -= 1;
+    if (ke < k) ke = k;  // never step backwards
+    if (ta >= 0 && ta < lim_a && tb >= 0 && tb < lim_b) {
+      const int32_t tx = b.xmajor ? ta : tb;
+      const int32_t ty = b.xmajor ? tb : ta;
+      emit(ty * g.TX + tx, k, (int32_t)ke);
+    }
+    k = (int32_t)ke + 1;
+  }
+}
+
+// Cell (x, band-local y) of step k.
+DM_HD inline void dm_cell(const Beam& b, int32_t k, int32_t row0, int32_t* x, int32_t* yl) {
+  const int32_t q = dm_minor_steps(b, k);
+  const int32_t ma = b.sa + k * b.ia;
+  const int32_t mb = b.sb + b.ib * q;
+  *x = b.xmajor ? ma : mb;
+  *yl = (b.xmajor ? mb : ma) - row0;
+}

@@ -110,7 +110,9 @@ class OccupancyMapper:
         """Integrate S scans: poses [S,3] (x, y, yaw), ranges [S,N] float32.
         Returns (updates U, touched cells T)."""
         poses = np.ascontiguousarray(poses, dtype=np.float64).reshape(-1, 3)
-        ranges = np.ascontiguousarray(ranges, dtype=np.float32).reshape(poses.shape[0], -1)
+        ranges = np.ascontiguousarray(ranges, dtype=np.float32)
+        if ranges.ndim != 2:
+            ranges = ranges.reshape(poses.shape[0], -1)
         S, N = ranges.shape
         U = ctypes.c_uint64(0)
         T = ctypes.c_uint64(0)

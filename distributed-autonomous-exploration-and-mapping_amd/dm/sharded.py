@@ -172,7 +172,9 @@ class ShardedMapper:
 
     def integrate(self, poses, ranges, angle_min, angle_increment):
         poses = np.asarray(poses, np.float64).reshape(-1, 3)
-        ranges = np.asarray(ranges, np.float32).reshape(poses.shape[0], -1)
+        ranges = np.asarray(ranges, np.float32)
+        if ranges.ndim != 2:
+            ranges = ranges.reshape(poses.shape[0], -1)
         if self.world_size > 1:
             keep = self.scan_mask(poses)
             poses, ranges = poses[keep], ranges[keep]
