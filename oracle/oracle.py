@@ -66,8 +66,8 @@ def band_rows(p: DmParams) -> int:
 def endpoints(p: DmParams, poses, ranges, angle_min, angle_increment):
     poses = np.ascontiguousarray(poses, dtype=np.float64).reshape(-1, 3)
     ranges = np.ascontiguousarray(ranges, dtype=np.float32)
-        if ranges.ndim != 2:
-            ranges = ranges.reshape(poses.shape[0], -1)
+    if ranges.ndim != 2:
+        ranges = ranges.reshape(poses.shape[0], -1)
     S, N = ranges.shape
     cells = np.zeros((S * N, 4), np.int64)
     flags = np.zeros(S * N, np.uint8)
