@@ -99,6 +99,23 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
     if (!rc) rc = dev_alloc(&g->act_cur, act, "active cursors");
     if (rc) return rc;
     g->act_cap = act;
+    if ((rc = dev_alloc(&g->act_heavy, act, "heavy map"))) return rc;
+  }
+  // work items / heavy tiles of the apply phase (exact bounds, see k_plan)
+  const int64_t chunk = 256;
+  const int64_t heavy = std::max<int64_t>(1, std::min<int64_t>(g->act_cap, segs / (chunk + 1) + 1));
+  const int64_t items = segs / chunk + g->act_cap + 1;
+  if (items > g->item_cap) {
+    int rc = dev_alloc(&g->items, items, "apply work items");
+    if (rc) return rc;
+    g->item_cap = items;
+  }
+  if (heavy > g->heavy_cap) {
+    int rc = dev_alloc(&g->heavy_list, heavy, "heavy tiles");
+    if (!rc) rc = dev_alloc(&g->slabs, heavy * 2 * DM_TILE * DM_TILE, "heavy-tile slabs");
+    if (rc) return rc;
+    DM_HIP(hipMemset(g->slabs, 0, sizeof(uint32_t) * (size_t)(heavy * 2 * DM_TILE * DM_TILE)));
+    g->heavy_cap = heavy;
   }
   if (2 * (int64_t)N > g->trig_cap) {
     int rc = dev_alloc(&g->trig, 2 * (int64_t)N, "trig table");
@@ -163,7 +180,7 @@ int finish_counts(dm_grid* g, uint64_t* U, uint64_t* T) {
   DM_HIP(hipMemcpyAsync(g->h_cnt, g->cnt, sizeof(unsigned long long) * CNT_N,
                         hipMemcpyDeviceToHost, g->stream));
   DM_HIP(hipStreamSynchronize(g->stream));
-  if (g->h_cnt[CNT_OVERFLOW] & 3ull) {
+  if (g->h_cnt[CNT_OVERFLOW] & 11ull) {
     // cannot happen with the bounds in grow_integrate; keep the map consistent anyway
     (void)hipMemset(g->tile_count, 0, sizeof(int32_t) * (size_t)g->NT);
     return dm_set_error(DM_ERR_CAPACITY, "integrate workspace overflow (flags %llu)",
@@ -297,6 +314,7 @@ int dm_destroy(dm_grid* g) {
   dev_free(g->L); dev_free(g->state); dev_free(g->tile_count); dev_free(g->tile_slot);
   dev_free(g->tile_free); dev_free(g->cnt); dev_free(g->beams); dev_free(g->segs);
   dev_free(g->act_tiles); dev_free(g->act_off); dev_free(g->act_cur); dev_free(g->trig);
+  dev_free(g->act_heavy); dev_free(g->heavy_list); dev_free(g->items); dev_free(g->slabs);
   dev_free(g->pose4); dev_free(g->ranges); dev_free(g->ftiles); dev_free(g->fmap);
   dev_free(g->border); dev_free(g->slot_label); dev_free(g->slot_parent); dev_free(g->slot_root);
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);

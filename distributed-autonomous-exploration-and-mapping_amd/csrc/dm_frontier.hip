@@ -77,6 +77,40 @@ __device__ inline void lds_unite(int32_t* par, int32_t a, int32_t b) {
   }
 }
 
+constexpr int kMaxRuns = 2048;        // <= 32 runs per 64-bit row x 64 rows
+
+__device__ inline uint64_t upto_mask(int p) {  // bits 0..p inclusive
+  return p >= 63 ? ~0ull : ((2ull << p) - 1ull);
+}
+
+// Run id of frontier bit p of tile row y (p must be set): runs are numbered
+// in row-major order of their first cell.
+__device__ inline int run_of(const int32_t* rbase, const uint64_t* starts, int y, int p) {
+  return rbase[y] + __popcll(starts[y] & upto_mask(p)) - 1;
+}
+
+// Unknown-cell bit of one halo cell (global column x, band-local row y);
+// out-of-grid cells and missing halos are "not unknown".
+__device__ inline uint32_t halo_unknown(const FGeom& g, const int8_t* state, const int8_t* halo,
+                                        int32_t x, int32_t y) {
+  if (x < 0 || x >= g.W) return 0u;
+  int8_t v = 0;
+  if (y >= 0 && y < g.R) v = state[(int64_t)y * g.W + x];
+  else if (y == -1 && g.has_before) v = halo[x];
+  else if (y == g.R && g.has_after) v = halo[g.W + x];
+  return v == -1 ? 1u : 0u;
+}
+
+// One workgroup per listed tile.  Each 64-cell tile row is a 64-bit word:
+//  1. state -> bit rows: interior 16 B per thread (one uint4 load), the 260
+//     halo cells one load per thread, all issued together;
+//  2. frontier row y = free[y] & dilate(unknown[y-1] | unknown[y] | unknown[y+1]);
+//  3. 8-connected CCL on runs of set bits: runs numbered row-major, a run is
+//     joined with every run of the row above that overlaps it extended by one
+//     cell each side (LDS union-find, atomicMin hooking: a root is its set's
+//     first run, whose first cell is the component's min linear index);
+//  4. per-component sums from run lengths, one slot per component, border
+//     slot ids for k_frontier_merge.
 __global__ __launch_bounds__(kFT) void k_frontier_tile(
     FGeom g, const int8_t* __restrict__ state, const int8_t* __restrict__ halo,
     const int32_t* __restrict__ ftiles, int32_t* __restrict__ border,
@@ -84,48 +118,104 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
     long long* __restrict__ slot_own, long long* __restrict__ slot_acc,
     uint8_t* __restrict__ mask, int32_t* __restrict__ cell_slot, int32_t* __restrict__ edge_slot,
     unsigned long long* cnt) {
-  __shared__ int8_t st[kHP * kHP];
-  __shared__ int32_t par[DM_TS * DM_TS];
-  __shared__ int16_t rid[DM_TS * DM_TS];
-  __shared__ int16_t rcell[kMaxRoots];
+  __shared__ uint64_t s_unk[DM_TS + 2];    // row y at index y+1, bit c = column c
+  __shared__ uint8_t s_unkL[DM_TS + 2];    // column -1
+  __shared__ uint8_t s_unkR[DM_TS + 2];    // column 64
+  __shared__ uint64_t s_free[DM_TS];
+  __shared__ uint64_t s_F[DM_TS];
+  __shared__ uint64_t s_start[DM_TS];
+  __shared__ int32_t s_rbase[DM_TS + 1];
+  __shared__ int32_t r_par[kMaxRuns];
+  __shared__ uint8_t r_s[kMaxRuns], r_e[kMaxRuns], r_y[kMaxRuns];
+  __shared__ int16_t r_rid[kMaxRuns];
+  __shared__ int16_t c_run[kMaxRoots];
   __shared__ uint32_t ssz[kMaxRoots], ssx[kMaxRoots], ssy[kMaxRoots];
   __shared__ int32_t nroots;
   __shared__ long long sbase;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = __lane_id();
   const int64_t nft = (int64_t)cnt[CNT_FTILES];
   for (int64_t j = blockIdx.x; j < nft; j += gridDim.x) {
     const int32_t tile = ftiles[j];
     const int32_t tx0 = (tile % g.TX) * DM_TS;
     const int32_t ty0 = (tile / g.TX) * DM_TS;  // band-local
-    if (tid == 0) nroots = 0;
-    // state tile + halo; out-of-grid (and missing-halo) cells read as 0,
-    // which is "not unknown" (out-of-bounds neighbours do not count)
-    for (int e = tid; e < kHP * kHP; e += kFT) {
-      const int hy = e / kHP, hx = e - hy * kHP;
-      const int32_t y = ty0 + hy - 1, x = tx0 + hx - 1;
-      int8_t v = 0;
-      if (x >= 0 && x < g.W) {
-        if (y >= 0 && y < g.R) v = state[(int64_t)y * g.W + x];
-        else if (y == -1 && g.has_before) v = halo[x];
-        else if (y == g.R && g.has_after) v = halo[g.W + x];
-      }
-      st[e] = v;
-    }
-    __syncthreads();
-    int any = 0;
-    for (int c = tid; c < DM_TS * DM_TS; c += kFT) {
-      const int ly = c >> 6, lx = c & 63;
-      int f = 0;
-      if (tx0 + lx < g.W && ty0 + ly < g.R) {
-        const int h = (ly + 1) * kHP + lx + 1;
-        if (st[h] == 0) {
-          f = (st[h - kHP - 1] == -1) | (st[h - kHP] == -1) | (st[h - kHP + 1] == -1) |
-              (st[h - 1] == -1) | (st[h + 1] == -1) | (st[h + kHP - 1] == -1) |
-              (st[h + kHP] == -1) | (st[h + kHP + 1] == -1);
+    // ---- 1. bit rows ------------------------------------------------------
+    {
+      const int y = tid >> 2, q = tid & 3;
+      const int32_t gy = ty0 + y;
+      uint32_t unk = 0u, fre = 0u;
+      if (gy < g.R) {
+        const int32_t x0 = tx0 + q * 16;
+        const int64_t off = (int64_t)gy * g.W + x0;
+        if (x0 + 16 <= g.W && (off & 15) == 0) {
+          const uint4 v = *reinterpret_cast<const uint4*>(state + off);
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+          for (int k = 0; k < 16; ++k) {
+            const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xFFu;
+            unk |= (b == 0xFFu ? 1u : 0u) << k;
+            fre |= (b == 0u ? 1u : 0u) << k;
+          }
+        } else {
+          for (int k = 0; k < 16; ++k) {
+            if (x0 + k >= g.W) break;
+            const int8_t b = state[off + k];
+            unk |= (b == -1 ? 1u : 0u) << k;
+            fre |= (b == 0 ? 1u : 0u) << k;
+          }
+        }
+      } else if (gy == g.R && g.has_after) {  // ragged band: the halo row falls inside the tile
+        const int32_t x0 = tx0 + q * 16;
+        for (int k = 0; k < 16; ++k) {
+          if (x0 + k >= g.W) break;
+          unk |= (halo[g.W + x0 + k] == -1 ? 1u : 0u) << k;
         }
       }
-      par[c] = f ? c : -1;
-      any |= f;
+      reinterpret_cast<uint16_t*>(&s_unk[y + 1])[q] = (uint16_t)unk;
+      reinterpret_cast<uint16_t*>(&s_free[y])[q] = (uint16_t)fre;
+      // halo, issued together with the interior loads: waves 0/1 the row above
+      // / below (one ballot each), threads 128..255 the columns left / right,
+      // threads 0..3 the four corners
+      const int hr = (tid - 128) & 63;
+      const bool left = tid < 192;
+      uint32_t hu = 0u, su = 0u, cu = 0u;
+      if (tid < 128) hu = halo_unknown(g, state, halo, tx0 + lane, tid < 64 ? ty0 - 1 : ty0 + DM_TS);
+      else su = halo_unknown(g, state, halo, left ? tx0 - 1 : tx0 + DM_TS, ty0 + hr);
+      if (tid < 4)
+        cu = halo_unknown(g, state, halo, tx0 + ((tid & 1) ? DM_TS : -1), (tid & 2) ? ty0 + DM_TS : ty0 - 1);
+      const uint64_t hm = __ballot(hu != 0u);
+      if (tid == 0) s_unk[0] = hm;
+      if (tid == 64) s_unk[DM_TS + 1] = hm;
+      if (tid >= 128) {
+        if (left) s_unkL[hr + 1] = (uint8_t)su; else s_unkR[hr + 1] = (uint8_t)su;
+      }
+      if (tid < 4) {
+        const int idx = (tid & 2) ? DM_TS + 1 : 0;
+        if (tid & 1) s_unkR[idx] = (uint8_t)cu; else s_unkL[idx] = (uint8_t)cu;
+      }
+    }
+    __syncthreads();
+    // ---- 2. frontier bits + runs -------------------------------------------
+    int any = 0;
+    if (tid < DM_TS) {
+      const int y = tid;
+      uint64_t D = 0;
+      for (int d = 0; d < 3; ++d) {
+        const uint64_t ui = s_unk[y + d];
+        D |= ui | (ui << 1) | (uint64_t)s_unkL[y + d] | (ui >> 1) | ((uint64_t)s_unkR[y + d] << 63);
+      }
+      const uint64_t F = s_free[y] & D;
+      const uint64_t st = F & ~(F << 1);
+      s_F[y] = F;
+      s_start[y] = st;
+      any = F != 0ull;
+      // exclusive scan of run counts over the 64 rows (wave 0)
+      const int c = __popcll(st);
+      int incl = c;
+      for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
+      }
+      s_rbase[y] = incl - c;
+      if (y == 63) s_rbase[DM_TS] = incl;
     }
     any = __syncthreads_or(any);
     if (!any) {
@@ -133,80 +223,115 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
       __syncthreads();
       continue;
     }
-    // union with the already-defined neighbours W, NW, N, NE
-    for (int c = tid; c < DM_TS * DM_TS; c += kFT) {
-      if (par[c] < 0) continue;
-      const int ly = c >> 6, lx = c & 63;
-      if (lx > 0 && par[c - 1] >= 0) lds_unite(par, c, c - 1);
-      if (ly > 0) {
-        if (lx > 0 && par[c - 65] >= 0) lds_unite(par, c, c - 65);
-        if (par[c - 64] >= 0) lds_unite(par, c, c - 64);
-        if (lx < 63 && par[c - 63] >= 0) lds_unite(par, c, c - 63);
+    if (tid < DM_TS) {  // enumerate runs of row tid
+      const int y = tid;
+      uint64_t st = s_start[y];
+      const uint64_t F = s_F[y];
+      int r = s_rbase[y];
+      while (st) {
+        const int s0 = __ffsll((unsigned long long)st) - 1;
+        const uint64_t rest = ~(F >> s0);
+        const int len = rest ? __ffsll((unsigned long long)rest) - 1 : 64 - s0;
+        r_s[r] = (uint8_t)s0;
+        r_e[r] = (uint8_t)(s0 + len - 1);
+        r_y[r] = (uint8_t)y;
+        r_par[r] = r;
+        ++r;
+        st &= st - 1;
       }
     }
-    __syncthreads();
-    for (int c = tid; c < DM_TS * DM_TS; c += kFT) {
-      if (par[c] >= 0) par[c] = lds_find(par, c);
-    }
-    __syncthreads();
-    for (int c = tid; c < DM_TS * DM_TS; c += kFT) {
-      if (par[c] == c) {
-        const int r = atomicAdd(&nroots, 1);
-        rid[c] = (int16_t)r;
-        rcell[r] = (int16_t)c;
-      }
-    }
+    if (tid == 0) nroots = 0;
     for (int r = tid; r < kMaxRoots; r += kFT) { ssz[r] = 0; ssx[r] = 0; ssy[r] = 0; }
     __syncthreads();
+    const int nruns = s_rbase[DM_TS];
+    // ---- 3. union with overlapping runs of the row above ---------------------
+    for (int r = tid; r < nruns; r += kFT) {
+      const int y = r_y[r];
+      if (y == 0) continue;
+      const int lo = r_s[r] > 0 ? r_s[r] - 1 : 0;
+      const int hi = r_e[r] < 63 ? r_e[r] + 1 : 63;
+      const uint64_t M = upto_mask(hi) & ~(lo > 0 ? upto_mask(lo - 1) : 0ull);
+      uint64_t P = s_F[y - 1] & M;
+      while (P) {
+        const int p = __ffsll((unsigned long long)P) - 1;
+        lds_unite(r_par, r, run_of(s_rbase, s_start, y - 1, p));
+        // skip the rest of that run inside M
+        const uint64_t rest = ~(s_F[y - 1] >> p);
+        const int len = rest ? __ffsll((unsigned long long)rest) - 1 : 64 - p;
+        P &= ~(upto_mask(p + len - 1));
+      }
+    }
+    __syncthreads();
+    for (int r = tid; r < nruns; r += kFT) r_par[r] = lds_find(r_par, r);
+    __syncthreads();
+    // ---- 4. components, sums, slots ------------------------------------------
+    for (int r = tid; r < nruns; r += kFT) {
+      if (r_par[r] == r) {
+        const int c = atomicAdd(&nroots, 1);
+        r_rid[r] = (int16_t)c;
+        c_run[c] = (int16_t)r;
+      }
+    }
+    __syncthreads();
     if (tid == 0) sbase = (long long)atomicAdd(&cnt[CNT_SLOTS], (unsigned long long)nroots);
-    for (int c = tid; c < DM_TS * DM_TS; c += kFT) {
-      const int32_t p = par[c];
-      if (p < 0) continue;
-      const int r = rid[p];
-      atomicAdd(&ssz[r], 1u);
-      atomicAdd(&ssx[r], (uint32_t)(c & 63));
-      atomicAdd(&ssy[r], (uint32_t)(c >> 6));
+    for (int r = tid; r < nruns; r += kFT) {
+      const int c = r_rid[r_par[r]];
+      const uint32_t s0 = r_s[r], e0 = r_e[r], len = e0 - s0 + 1;
+      atomicAdd(&ssz[c], len);
+      atomicAdd(&ssx[c], (s0 + e0) * len / 2);
+      atomicAdd(&ssy[c], (uint32_t)r_y[r] * len);
     }
     __syncthreads();
     const long long base = sbase;
     const int nr = nroots;
-    for (int r = tid; r < nr; r += kFT) {
-      const long long slot = base + r;
+    for (int c = tid; c < nr; c += kFT) {
+      const long long slot = base + c;
       if (slot >= g.slot_cap) { atomicOr(&cnt[CNT_OVERFLOW], 4ull); continue; }
-      const int c = rcell[r];
-      const long long gy = (long long)g.row0 + ty0 + (c >> 6);
-      const long long gx = (long long)tx0 + (c & 63);
-      const long long sz = ssz[r];
+      const int r = c_run[c];
+      const long long gy = (long long)g.row0 + ty0 + r_y[r];
+      const long long gx = (long long)tx0 + r_s[r];
+      const long long sz = ssz[c];
       slot_label[slot] = gy * g.W + gx;
       slot_parent[slot] = (int32_t)slot;
-      const long long sx = sz * tx0 + ssx[r];
-      const long long sy = sz * ((long long)g.row0 + ty0) + ssy[r];
+      const long long sx = sz * tx0 + ssx[c];
+      const long long sy = sz * ((long long)g.row0 + ty0) + ssy[c];
       slot_own[3 * slot + 0] = sz; slot_own[3 * slot + 1] = sx; slot_own[3 * slot + 2] = sy;
       slot_acc[3 * slot + 0] = sz; slot_acc[3 * slot + 1] = sx; slot_acc[3 * slot + 2] = sy;
     }
     // border slots: [0] first row, [1] last row, [2] first col, [3] last col
     {
       const int side = tid >> 6, pos = tid & 63;
-      const int c = side == 0 ? pos : side == 1 ? (63 * 64 + pos) : side == 2 ? (pos * 64) : (pos * 64 + 63);
-      const int32_t p = par[c];
-      long long s = p < 0 ? -1 : base + rid[p];
-      if (s >= g.slot_cap) s = -1;
-      border[j * 256 + tid] = (int32_t)s;
+      const int y = side == 0 ? 0 : side == 1 ? 63 : pos;
+      const int x = side == 0 || side == 1 ? pos : side == 2 ? 0 : 63;
+      long long sl = -1;
+      if ((s_F[y] >> x) & 1ull) {
+        sl = base + r_rid[r_par[run_of(s_rbase, s_start, y, x)]];
+        if (sl >= g.slot_cap) sl = -1;
+      }
+      border[j * 256 + tid] = (int32_t)sl;
     }
-    // band edge rows (for cross-band merging) and optional dense outputs
-    for (int c = tid; c < DM_TS * DM_TS; c += kFT) {
-      const int ly = c >> 6, lx = c & 63;
-      const int32_t y = ty0 + ly, x = tx0 + lx;
-      if (x >= g.W || y >= g.R) continue;
-      const int32_t p = par[c];
-      long long s = p < 0 ? -1 : base + rid[p];
-      if (s >= g.slot_cap) s = -1;
-      const int64_t gi = (int64_t)y * g.W + x;
-      if (g.want_mask) mask[gi] = p >= 0;
-      if (g.want_labels) cell_slot[gi] = (int32_t)s;
-      if (p >= 0) {
-        if (y == 0) edge_slot[x] = (int32_t)s;
-        if (y == g.R - 1) edge_slot[g.W + x] = (int32_t)s;
+    // band edge rows (cross-band merging) and optional dense outputs
+    const bool dense = g.want_mask || g.want_labels;
+    if (dense || ty0 == 0 || ty0 + DM_TS >= g.R) {
+      for (int c = tid; c < DM_TS * DM_TS; c += kFT) {
+        const int y = c >> 6, x = c & 63;
+        const int32_t gy = ty0 + y, gx = tx0 + x;
+        if (gx >= g.W || gy >= g.R) continue;
+        const bool edge = gy == 0 || gy == g.R - 1;
+        if (!dense && !edge) continue;
+        const bool f = (s_F[y] >> x) & 1ull;
+        long long sl = -1;
+        if (f) {
+          sl = base + r_rid[r_par[run_of(s_rbase, s_start, y, x)]];
+          if (sl >= g.slot_cap) sl = -1;
+        }
+        const int64_t gi = (int64_t)gy * g.W + gx;
+        if (g.want_mask) mask[gi] = f;
+        if (g.want_labels) cell_slot[gi] = (int32_t)sl;
+        if (f) {
+          if (gy == 0) edge_slot[gx] = (int32_t)sl;
+          if (gy == g.R - 1) edge_slot[g.W + gx] = (int32_t)sl;
+        }
       }
     }
     __syncthreads();

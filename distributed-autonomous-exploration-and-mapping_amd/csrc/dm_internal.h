@@ -39,7 +39,9 @@ enum {
   CNT_SLOTS = 5,    // tile-local frontier components
   CNT_CLUSTERS = 6, // output clusters
   CNT_OVERFLOW = 7, // capacity overflow flags
-  CNT_N = 8
+  CNT_ITEMS = 8,    // apply work items
+  CNT_HEAVY = 9,    // tiles split over several work items
+  CNT_N = 10
 };
 
 struct KernelTimer {
@@ -69,6 +71,12 @@ struct dm_grid {
   Seg* segs = nullptr; int64_t segs_cap = 0;
   int32_t* act_tiles = nullptr; int32_t* act_off = nullptr; int32_t* act_cur = nullptr;
   int64_t act_cap = 0;
+  int32_t* act_heavy = nullptr;  // active tile -> heavy ordinal or -1
+  int32_t* heavy_list = nullptr; // heavy ordinal -> active tile
+  int64_t heavy_cap = 0;
+  int2* items = nullptr;         // (active tile, chunk) work items
+  int64_t item_cap = 0;
+  uint32_t* slabs = nullptr;     // [heavy][2][64*64] merged counts
   double* trig = nullptr; int32_t trig_n = -1; float trig_amin = 0, trig_inc = 0;
   int64_t trig_cap = 0;
   double* pose4 = nullptr; int64_t pose_cap = 0;

@@ -21,7 +21,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _ffi
-from ._ffi import CLUSTER_DTYPE, DmCluster, DmError, DmParams, check, load_library
+from ._ffi import CLUSTER_DTYPE, DmError, DmParams, check, load_library
 
 
 def default_params(width: int, height: int, **overrides) -> DmParams:
@@ -80,6 +80,7 @@ class OccupancyMapper:
         self.width = int(out.width)
         self.rows = int(out.band_rows)
         self.row0 = int(out.band_row0)
+        self._cbuf = np.empty(1 << 14, dtype=np.dtype(CLUSTER_DTYPE))
 
     # -- lifetime ---------------------------------------------------------
     def close(self):
@@ -181,23 +182,26 @@ class OccupancyMapper:
         return out
 
     # -- frontiers --------------------------------------------------------
-    def frontiers(self, want_mask=False, want_labels=False, cap=1 << 16) -> Frontiers:
+    def frontiers(self, want_mask=False, want_labels=False, cap=None) -> Frontiers:
+        """Frontier mask / labels (optional dense copies) and the cluster
+        list sorted by label.  The cluster buffer is reused across calls and
+        grown when the library reports more clusters than it holds."""
         mask = np.empty((self.rows, self.width), np.uint8) if want_mask else None
         labels = np.empty((self.rows, self.width), np.int64) if want_labels else None
         n = ctypes.c_int64(0)
         with self._lock:
+            if cap is not None and (self._cbuf is None or self._cbuf.shape[0] < cap):
+                self._cbuf = np.empty(max(1, int(cap)), dtype=np.dtype(CLUSTER_DTYPE))
             while True:
-                buf = (DmCluster * max(1, cap))()
-                rc = self._lib.dm_frontiers(self._handle(), _vp(mask), _vp(labels),
-                                            ctypes.cast(buf, ctypes.c_void_p), cap, ctypes.byref(n))
-                if rc == _ffi.DM_ERR_CAPACITY and n.value > cap:
-                    cap = int(n.value)
+                buf = self._cbuf
+                rc = self._lib.dm_frontiers(self._handle(), _vp(mask), _vp(labels), _vp(buf),
+                                            buf.shape[0], ctypes.byref(n))
+                if rc == _ffi.DM_ERR_CAPACITY and n.value > buf.shape[0]:
+                    self._cbuf = np.empty(int(n.value) * 2, dtype=np.dtype(CLUSTER_DTYPE))
                     continue
                 check(rc)
                 break
-        k = int(n.value)
-        clusters = np.frombuffer(bytes(buf)[: k * ctypes.sizeof(DmCluster)],
-                                 dtype=np.dtype(CLUSTER_DTYPE)).copy()
+            clusters = buf[: int(n.value)].copy()
         return Frontiers(clusters=clusters, mask=mask, labels=labels)
 
     # -- sharding support -------------------------------------------------

@@ -130,7 +130,7 @@ def test_frontiers_on_states(oracle_lib, kind, R, W, seed):
 def test_frontier_band_with_halo(oracle_lib):
     W, H = 300, 640
     full = cases.blob_state(8, H, W, n_blobs=30)
-    for r0, rows in [(0, 192), (192, 256), (448, 192)]:
+    for r0, rows in [(0, 192), (192, 256), (448, 192), (128, 100), (64, 37)]:
         p = cases.make_params(W, H, band_row0=r0, band_rows=rows)
         om = oracle_lib.OracleMap(p)
         om.state[...] = full[r0:r0 + rows]
@@ -249,5 +249,5 @@ def test_profiling_counters():
         m.integrate(poses, ranges, amin, inc)
         m.frontiers()
         st = m.profile_read()
-    assert st["tile_apply"][0] == 1 and st["tile_apply"][1] > 0
+    assert st["tile_accum"][0] == 1 and st["tile_accum"][1] > 0
     assert "frontier_tile" in st
