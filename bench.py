@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="budget for the CPU-oracle baseline sample (0 disables)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1")
+    ap.add_argument("--device-override", type=int, default=None,
+                    help="put every rank on this GPU (rehearsal with --backend gloo)")
     return ap.parse_args()
 
 
@@ -58,9 +61,14 @@ def main():
     if world_size != args.gpus:
         if world_size == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    if args.device_override is not None:
+        local_rank = args.device_override
     torch.cuda.set_device(local_rank)
     if world_size > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(args.backend)
 
     import dm
     from dm import synth
@@ -99,10 +107,12 @@ def main():
 
     # per-batch U and T are properties of the batch (not of the map state):
     # measure them once, untimed
-    counts = []
+    counts, stats = [], []
     for k in range(len(dpool)):
         integrate(k)
-        counts.append(band.last_counts())
+        st = band.last_stats()
+        stats.append(st)
+        counts.append((st["updates"], st["touched"]))
     band.reset()
 
     def step(k):
@@ -126,14 +136,15 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    cdev = dev if args.backend == "nccl" else torch.device("cpu")
     if world_size > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     U_rank = sum(counts[(args.warmup + k) % len(counts)][0] for k in range(args.steps))
     U_all = U_rank
     if world_size > 1:
-        t = torch.tensor([U_rank], dtype=torch.int64, device=dev)
+        t = torch.tensor([U_rank], dtype=torch.int64, device=cdev)
         dist.all_reduce(t)
         U_all = int(t.item())
 
@@ -166,9 +177,15 @@ def main():
     band.profile(False)
     avg = {name: tot / max(1, n) for name, (n, tot) in kstats.items()}
     dominant = max(kstats, key=lambda n: kstats[n][1]) if kstats else None
-    t_apply_ms = avg.get("tile_apply", float("nan"))
-    bytes_apply = TILE_APPLY_BYTES_PER_UPDATE * U_mean + TILE_APPLY_BYTES_PER_TOUCHED * T_mean
-    achieved = bytes_apply / (t_apply_ms * 1e-3) / 1e9 if t_apply_ms > 0 else None
+    # roofline of the dominant integrate kernel, k_tile_accum: it performs
+    # every update (8 B each) and applies the touched cells of light tiles
+    # (25 B each); k_heavy_apply applies the rest
+    TH_mean = float(np.mean([st["touched_heavy"] for st in stats]))
+    t_accum_ms = avg.get("tile_accum", float("nan"))
+    bytes_accum = (TILE_APPLY_BYTES_PER_UPDATE * U_mean
+                   + TILE_APPLY_BYTES_PER_TOUCHED * (T_mean - TH_mean))
+    achieved = bytes_accum / (t_accum_ms * 1e-3) / 1e9 if t_accum_ms > 0 else None
+    traffic, traffic_src = pmc_traffic("k_tile_accum")
 
     result = None
     if rank == 0:
@@ -207,17 +224,20 @@ def main():
             "clusters": fr_clusters,
             "kernel_avg_ms": avg,
             "roofline": {
-                "kernel": "tile_apply",
+                "kernel": "tile_accum",
                 "dominant_kernel": dominant,
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
-                "traffic": None,
-                "algorithmic_bytes_per_launch": bytes_apply,
-                "bytes_model": "8*U + 25*T per integrate call (SURVEY.md §8(d))",
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "avg_launch_ms": t_accum_ms,
+                "algorithmic_bytes_per_launch": bytes_accum,
+                "bytes_model": "8*U + 25*(T - T_heavy) per call (SURVEY.md §8(d) per-unit figures)",
             },
+            "stage_stats": {k: float(np.mean([st[k] for st in stats])) for k in stats[0]},
             "cpu_baseline": cpu,
             "gen_seconds": t_gen,
         }
@@ -226,6 +246,22 @@ def main():
     if world_size > 1:
         dist.destroy_process_group()
     return result
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (tools/pmc_passes.sh + tools/pmc_summary.py), only if it was measured on
+    the same libdm sources; otherwise None."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    try:
+        from src_hash import src_hash
+        summ = json.load(open(os.path.join(REPO, "profiles", "pmc_latest.json")))
+    except (OSError, ValueError, ImportError):
+        return None, None
+    if summ.get("src_hash") != src_hash():
+        return None, "profiles/pmc_latest.json is from other sources"
+    k = summ.get("kernels", {}).get(kernel, {})
+    return k.get("traffic_bytes"), "profiles/pmc_latest.json (2*FETCH_SIZE + WRITE_SIZE, KiB->B)"
 
 
 def cpu_baseline(params, pool, amin, inc, budget_s):

@@ -414,6 +414,21 @@ int dm_last_counts(dm_grid* g, uint64_t* updates, uint64_t* touched) {
   return finish_counts(g, updates, touched);
 }
 
+int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (cap > 0 && !out) return dm_set_error(DM_ERR_INVALID_ARG, "out is NULL");
+  DM_HIP(hipMemcpyAsync(g->h_cnt, g->cnt, sizeof(unsigned long long) * CNT_N,
+                        hipMemcpyDeviceToHost, g->stream));
+  DM_HIP(hipStreamSynchronize(g->stream));
+  const uint64_t v[7] = {g->h_cnt[CNT_U],   g->h_cnt[CNT_T],     g->h_cnt[CNT_TH],
+                         g->h_cnt[CNT_SEGS], g->h_cnt[CNT_ACTIVE], g->h_cnt[CNT_ITEMS],
+                         g->h_cnt[CNT_HEAVY]};
+  for (int32_t i = 0; i < cap && i < 7; ++i) out[i] = v[i];
+  if (n_out) *n_out = 7;
+  return DM_OK;
+}
+
 int dm_get_state(dm_grid* g, int8_t* out) {
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;

@@ -128,6 +128,7 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
 // into kChunk-piece items on different CUs that merge their counts in a
 // per-tile slab, applied by k_heavy_apply.
 constexpr int kChunk = 256;
+static_assert(kChunk < 65536, "packed 16-bit LDS counts");
 
 __device__ inline void block_scan3(int64_t v[3], int64_t excl[3], int64_t tot[3], int64_t (*ws)[3]) {
   const int tid = threadIdx.x, lane = __lane_id(), wid = tid >> 6;
@@ -364,8 +365,10 @@ __global__ __launch_bounds__(kApplyThreads) void k_tile_accum(
     const Seg* __restrict__ segs, const Beam* __restrict__ beams, int32_t* tile_count,
     int32_t* tile_free, uint32_t* __restrict__ slabs, float* __restrict__ L,
     int8_t* __restrict__ state, unsigned long long* cnt, int vec_ok) {
-  __shared__ uint32_t hit[DM_TS * kLdsPitch];
-  __shared__ uint32_t miss[DM_TS * kLdsPitch];
+  // per-cell counts of this item, packed: hits << 16 | misses.  An item has
+  // at most kChunk = 256 pieces and a piece visits a cell at most once, so
+  // neither half can exceed 256: no carry between the halves.
+  __shared__ uint32_t cnt16[DM_TS * kLdsPitch];
   __shared__ Seg s_seg[kChunk];
   __shared__ Beam s_beam[kChunk];
   __shared__ int32_t sh_free, sh_T;
@@ -381,7 +384,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_tile_accum(
     const int32_t heavy = act_heavy[j];
     const int32_t c0 = act_off[j] + item.y * kChunk;
     const int32_t nseg = min(kChunk, act_off[j] + count - c0);
-    for (int e = tid; e < DM_TS * kLdsPitch; e += kApplyThreads) { hit[e] = 0u; miss[e] = 0u; }
+    for (int e = tid; e < DM_TS * kLdsPitch; e += kApplyThreads) cnt16[e] = 0u;
     if (tid == 0) { sh_free = 0; sh_T = 0; sh_U = 0u; }
     if (tid < nseg) {
       const Seg sg = segs[c0 + tid];
@@ -408,7 +411,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_tile_accum(
         const int32_t lx = x - tx0, ly = yl - ty0;
         if (x >= 0 && x < g.r.W && yl >= 0 && yl < g.r.R && (uint32_t)lx < DM_TS && (uint32_t)ly < DM_TS) {
           const bool is_hit = (k == bm.n) && (bm.flags & 2);
-          atomicAdd(is_hit ? &hit[ly * kLdsPitch + lx] : &miss[ly * kLdsPitch + lx], 1u);
+          atomicAdd(&cnt16[ly * kLdsPitch + lx], is_hit ? 0x10000u : 1u);
           ++myU;
         }
       }
@@ -419,8 +422,9 @@ __global__ __launch_bounds__(kApplyThreads) void k_tile_accum(
       apply_tile(g, p, tx0, ty0, L, state, vec_ok,
                  [&](int ly, int cx, uint32_t* h4, uint32_t* m4) {
                    for (int e = 0; e < 4; ++e) {
-                     h4[e] = hit[ly * kLdsPitch + cx + e];
-                     m4[e] = miss[ly * kLdsPitch + cx + e];
+                     const uint32_t v = cnt16[ly * kLdsPitch + cx + e];
+                     h4[e] = v >> 16;
+                     m4[e] = v & 0xFFFFu;
                    }
                  },
                  &sh_T, &sh_free);
@@ -428,7 +432,8 @@ __global__ __launch_bounds__(kApplyThreads) void k_tile_accum(
       uint32_t* sh = slabs + (int64_t)heavy * (2 * DM_TS * DM_TS);
       for (int e = tid; e < DM_TS * DM_TS; e += kApplyThreads) {
         const int ly = e >> 6, lx = e & 63;
-        const uint32_t h = hit[ly * kLdsPitch + lx], m = miss[ly * kLdsPitch + lx];
+        const uint32_t v = cnt16[ly * kLdsPitch + lx];
+        const uint32_t h = v >> 16, m = v & 0xFFFFu;
         if (h) atomicAdd(&sh[e], h);
         if (m) atomicAdd(&sh[DM_TS * DM_TS + e], m);
       }
@@ -475,7 +480,10 @@ __global__ __launch_bounds__(kApplyThreads) void k_heavy_apply(
       *reinterpret_cast<uint4*>(sh + e) = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
     if (tid == 0) {
-      if (sh_T) atomicAdd(&cnt[CNT_T], (unsigned long long)sh_T);
+      if (sh_T) {
+        atomicAdd(&cnt[CNT_T], (unsigned long long)sh_T);
+        atomicAdd(&cnt[CNT_TH], (unsigned long long)sh_T);
+      }
       tile_free[tile] += sh_free;
       tile_count[tile] = 0;
     }

@@ -41,7 +41,8 @@ enum {
   CNT_OVERFLOW = 7, // capacity overflow flags
   CNT_ITEMS = 8,    // apply work items
   CNT_HEAVY = 9,    // tiles split over several work items
-  CNT_N = 10
+  CNT_TH = 10,      // touched cells applied by k_heavy_apply
+  CNT_N = 11
 };
 
 struct KernelTimer {

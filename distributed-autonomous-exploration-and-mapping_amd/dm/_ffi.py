@@ -114,6 +114,7 @@ SIGNATURES = {
     "dm_integrate": [_vp, _i32, _vp, _i32, _vp, _f32, _f32, _vp, _vp],
     "dm_integrate_device": [_vp, _i32, _vp, _i32, _vp, _f32, _f32],
     "dm_last_counts": [_vp, _vp, _vp],
+    "dm_last_stats": [_vp, _vp, _i32, ctypes.POINTER(_i32)],
     "dm_get_state": [_vp, _vp],
     "dm_get_logodds": [_vp, _vp],
     "dm_set_logodds": [_vp, _vp],

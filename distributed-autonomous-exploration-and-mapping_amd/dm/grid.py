@@ -146,6 +146,17 @@ class OccupancyMapper:
             check(self._lib.dm_last_counts(self._handle(), ctypes.byref(U), ctypes.byref(T)))
         return int(U.value), int(T.value)
 
+    STAT_NAMES = ("updates", "touched", "touched_heavy", "pieces", "active_tiles", "work_items",
+                  "heavy_tiles")
+
+    def last_stats(self) -> dict:
+        """Diagnostics of the most recent integrate call (dm_last_stats)."""
+        out = (ctypes.c_uint64 * 7)()
+        n = ctypes.c_int32(0)
+        with self._lock:
+            check(self._lib.dm_last_stats(self._handle(), out, 7, ctypes.byref(n)))
+        return {k: int(out[i]) for i, k in enumerate(self.STAT_NAMES)}
+
     # -- map access -------------------------------------------------------
     def state(self) -> np.ndarray:
         out = np.empty((self.rows, self.width), np.int8)

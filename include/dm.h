@@ -128,6 +128,11 @@ int dm_integrate_device(dm_grid* g, int32_t S, const double* d_pose4,
 /* U and T of the most recent integrate call (synchronises the stream). */
 int dm_last_counts(dm_grid* g, uint64_t* updates, uint64_t* touched);
 
+/* Diagnostics of the most recent integrate call (synchronises the stream):
+ * out[0..6] = U, T, T applied by the heavy-tile pass, pieces (ray pieces
+ * binned by tile), active tiles, apply work items, heavy tiles. */
+int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out);
+
 /* OccupancyGrid.data for the band: int8[band_rows*width] (-1 / 0 / 100). */
 int dm_get_state(dm_grid* g, int8_t* out);
 /* Log-odds for the band: float[band_rows*width]. */

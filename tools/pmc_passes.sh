@@ -1,0 +1,16 @@
+#!/bin/bash
+# PMC passes over a short bench run (one rocprofv3 --pmc run per counter group).
+# Usage (on the GPU box, from the repo root): bash tools_pmc.sh OUTDIR
+set -o pipefail
+R=$PWD
+OUT=${1:-gpurun_out/pmc}
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+i=0
+for group in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU" \
+             "FETCH_SIZE GRBM_GUI_ACTIVE" "WRITE_SIZE GRBM_COUNT"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $group --kernel-trace --output-format csv -d $R/$OUT/p$i -o run \
+    -- python3 $R/bench.py --steps 5 --warmup 2 --cpu-seconds 0 --profile-steps 0 --pool 3 > $R/$OUT/p$i.log 2>&1 || { echo "pmc pass $i failed rc=$?"; exit 1; }
+  echo "pmc pass $i ok"
+done
