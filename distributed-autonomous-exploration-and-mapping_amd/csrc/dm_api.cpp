@@ -584,6 +584,58 @@ int dm_get_edge_labels(dm_grid* g, int64_t* first_row, int64_t* last_row) {
   return DM_OK;
 }
 
+static int check_ld06_args(int32_t S, int32_t N, const void* pts, const void* off, const void* out) {
+  if (S < 0) return dm_set_error(DM_ERR_SHAPE, "S must be >= 0");
+  if (N < 2 || N > 8192) return dm_set_error(DM_ERR_SHAPE, "N must be in [2, 8192] (got %d)", N);
+  if (S > 0 && (!pts || !off || !out)) return dm_set_error(DM_ERR_INVALID_ARG, "NULL buffer");
+  return DM_OK;
+}
+
+int dm_ld06_to_scans_device(dm_grid* g, int32_t S, const dm_ld06_point* d_points,
+                            const int64_t* d_offsets, int32_t N, int laser_scan_dir,
+                            float* d_ranges_out, float* d_intensities_out) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if ((rc = check_ld06_args(S, N, d_points, d_offsets, d_ranges_out))) return rc;
+  return dm_launch_ld06(g, S, d_points, d_offsets, N, laser_scan_dir ? 1 : 0, d_ranges_out,
+                        d_intensities_out);
+}
+
+int dm_ld06_to_scans(dm_grid* g, int32_t S, const dm_ld06_point* points, const int64_t* offsets,
+                     int32_t N, int laser_scan_dir, float* ranges_out, float* intensities_out) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if ((rc = check_ld06_args(S, N, points, offsets, ranges_out))) return rc;
+  if (S == 0) return DM_OK;
+  const int64_t np = offsets[S];
+  if (np < 0 || offsets[0] != 0) return dm_set_error(DM_ERR_SHAPE, "offsets must start at 0");
+  for (int32_t s = 0; s < S; ++s)
+    if (offsets[s + 1] < offsets[s]) return dm_set_error(DM_ERR_SHAPE, "offsets must be non-decreasing");
+  dm_ld06_point* dp = nullptr;
+  int64_t* doff = nullptr;
+  float* dr = nullptr;
+  float* di = nullptr;
+  auto cleanup = [&]() { dev_free(dp); dev_free(doff); dev_free(dr); dev_free(di); };
+  if ((rc = dev_alloc(&dp, np, "ld06 points")) || (rc = dev_alloc(&doff, S + 1, "ld06 offsets")) ||
+      (rc = dev_alloc(&dr, (int64_t)S * N, "ld06 ranges")) ||
+      (intensities_out && (rc = dev_alloc(&di, (int64_t)S * N, "ld06 intensities")))) {
+    cleanup();
+    return rc;
+  }
+  hipError_t e = hipMemcpyAsync(dp, points, sizeof(dm_ld06_point) * (size_t)np, hipMemcpyHostToDevice, g->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(doff, offsets, sizeof(int64_t) * (size_t)(S + 1), hipMemcpyHostToDevice, g->stream);
+  if (e == hipSuccess) rc = dm_launch_ld06(g, S, dp, doff, N, laser_scan_dir ? 1 : 0, dr, di);
+  if (e == hipSuccess && !rc)
+    e = hipMemcpyAsync(ranges_out, dr, sizeof(float) * (size_t)S * N, hipMemcpyDeviceToHost, g->stream);
+  if (e == hipSuccess && !rc && intensities_out)
+    e = hipMemcpyAsync(intensities_out, di, sizeof(float) * (size_t)S * N, hipMemcpyDeviceToHost, g->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(g->stream);
+  cleanup();
+  if (e != hipSuccess) return dm_hip_check(e, "dm_ld06_to_scans");
+  return rc;
+}
+
 static const char kMagic[8] = {'D', 'M', 'A', 'P', '0', '0', '0', '1'};
 
 int dm_save(dm_grid* g, const char* path) {

@@ -120,6 +120,8 @@ int dm_launch_state_from_logodds(dm_grid* g);
 int dm_launch_map_image(dm_grid* g, uint8_t* d_img);
 int dm_launch_set_state(dm_grid* g, const int8_t* d_state_in);
 int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters);
+int dm_launch_ld06(dm_grid* g, int32_t S, const dm_ld06_point* d_pts, const int64_t* d_offsets,
+                   int32_t N, int dir, float* d_ranges, float* d_intensities);
 
 // error plumbing (dm_api.cpp)
 int dm_set_error(int code, const char* fmt, ...);

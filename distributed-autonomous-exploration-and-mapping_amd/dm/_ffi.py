@@ -82,6 +82,20 @@ class DmCluster(ctypes.Structure):
     ]
 
 
+class DmLd06Point(ctypes.Structure):
+    """Mirror of ``dm_ld06_point`` (include/dm.h)."""
+
+    _fields_ = [
+        ("angle_deg", ctypes.c_float),
+        ("distance_mm", ctypes.c_uint16),
+        ("intensity", ctypes.c_uint8),
+        ("pad", ctypes.c_uint8),
+    ]
+
+
+LD06_POINT_DTYPE = [("angle_deg", "<f4"), ("distance_mm", "<u2"), ("intensity", "u1"), ("pad", "u1")]
+
+
 class DmKernelStat(ctypes.Structure):
     _fields_ = [
         ("name", ctypes.c_char * 32),
@@ -133,6 +147,8 @@ SIGNATURES = {
     "dm_profile_read": [_vp, ctypes.POINTER(DmKernelStat), _i32, ctypes.POINTER(_i32)],
     "dm_profile_reset": [_vp],
     "dm_map_image": [_vp, _vp],
+    "dm_ld06_to_scans": [_vp, _i32, _vp, _vp, _i32, ctypes.c_int, _vp, _vp],
+    "dm_ld06_to_scans_device": [_vp, _i32, _vp, _vp, _i32, ctypes.c_int, _vp, _vp],
 }
 # functions returning const char*
 STRING_FUNCS = ("dm_last_error", "dm_version")

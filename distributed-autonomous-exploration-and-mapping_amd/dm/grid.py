@@ -157,6 +157,22 @@ class OccupancyMapper:
             check(self._lib.dm_last_stats(self._handle(), out, 7, ctypes.byref(n)))
         return {k: int(out[i]) for i, k in enumerate(self.STAT_NAMES)}
 
+    def ld06_to_scans(self, points, offsets, n_beams: int, laser_scan_dir: bool = True,
+                      want_intensities: bool = False):
+        """LD06 PointData -> LaserScan ranges on the GPU, as the driver's
+        ToLaserscanMessagePublish (dm_ld06_to_scans).  points: structured
+        array of LD06_POINT_DTYPE; offsets: int64 [S+1].  Returns ranges
+        float32 [S, N] (and intensities)."""
+        pts = np.ascontiguousarray(points, dtype=np.dtype(_ffi.LD06_POINT_DTYPE))
+        off = np.ascontiguousarray(offsets, dtype=np.int64)
+        S = off.shape[0] - 1
+        ranges = np.empty((S, n_beams), np.float32)
+        inten = np.empty((S, n_beams), np.float32) if want_intensities else None
+        with self._lock:
+            check(self._lib.dm_ld06_to_scans(self._handle(), S, _vp(pts), _vp(off), int(n_beams),
+                                             1 if laser_scan_dir else 0, _vp(ranges), _vp(inten)))
+        return (ranges, inten) if want_intensities else ranges
+
     # -- map access -------------------------------------------------------
     def state(self) -> np.ndarray:
         out = np.empty((self.rows, self.width), np.int8)

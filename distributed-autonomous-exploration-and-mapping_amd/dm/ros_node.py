@@ -248,3 +248,7 @@ def main(args=None):  # pragma: no cover - needs ROS 2
         mn.destroy_node()
         node.destroy_node()
         rclpy.shutdown()
+
+
+if __name__ == "__main__":  # pragma: no cover
+    main()

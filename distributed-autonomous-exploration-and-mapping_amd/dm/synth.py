@@ -220,3 +220,21 @@ def pose4(poses: np.ndarray) -> np.ndarray:
     for i, (x, y, yaw) in enumerate(poses):
         out[i] = (x, y, math.cos(yaw), math.sin(yaw))
     return out
+
+
+def ld06_points(world: World, x: float, y: float, yaw: float, rng: np.random.Generator,
+                n_points: int = 450, dropout: float = 0.02) -> np.ndarray:
+    """One revolution of raw LD06 PointData (angle in degrees, distance in mm,
+    intensity), as LiPkg hands them to ToLaserscanMessagePublish: ~4500 Hz /
+    10 Hz = 450 points with slightly jittered angles, no return = (0 mm, 0)."""
+    from ._ffi import LD06_POINT_DTYPE
+
+    ang = (np.arange(n_points) + rng.uniform(-0.3, 0.3, n_points)) * (360.0 / n_points)
+    ang = np.mod(ang, 360.0).astype(np.float32)
+    d = ray_distances(world, x, y, yaw + np.deg2rad(ang.astype(np.float64)))
+    pts = np.zeros(n_points, dtype=np.dtype(LD06_POINT_DTYPE))
+    pts["angle_deg"] = ang
+    ok = np.isfinite(d) & (d * 1000.0 < 65535) & (rng.random(n_points) >= dropout)
+    pts["distance_mm"] = np.where(ok, np.round(d * 1000.0), 0).astype(np.uint16)
+    pts["intensity"] = np.where(ok, rng.integers(100, 255, n_points), 0).astype(np.uint8)
+    return pts

@@ -164,6 +164,28 @@ int dm_get_edge_rows_device(dm_grid* g, int8_t* d_first_row, int8_t* d_last_row)
 /* After dm_frontiers: band-local labels of the first/last rows (int64[W]). */
 int dm_get_edge_labels(dm_grid* g, int64_t* first_row, int64_t* last_row);
 
+/* LD06 driver point (ldlidar::PointData fields the LaserScan conversion uses). */
+typedef struct dm_ld06_point {
+  float angle_deg;      /* 0..360 */
+  uint16_t distance_mm;
+  uint8_t intensity;
+  uint8_t pad;
+} dm_ld06_point;
+
+/* LD06 PointData -> LaserScan.ranges/intensities for S revolutions, exactly
+ * as the driver's ToLaserscanMessagePublish (ldlidar_stl_ros2_node @0x7f853;
+ * SURVEY.md §8 a1): scan s holds points[offsets[s] .. offsets[s+1]), N beams,
+ * angle_min 0, angle_increment 6.2831855f/(N-1), NaN = no return, keep the
+ * nearest return per beam; laser_scan_dir mirrors the index
+ * (pi_hardware.launch.py:20).  ranges_out: float[S][N]; intensities_out may
+ * be NULL.  N must be in [2, 8192]. */
+int dm_ld06_to_scans(dm_grid* g, int32_t S, const dm_ld06_point* points,
+                     const int64_t* offsets, int32_t N, int laser_scan_dir,
+                     float* ranges_out, float* intensities_out);
+int dm_ld06_to_scans_device(dm_grid* g, int32_t S, const dm_ld06_point* d_points,
+                            const int64_t* d_offsets, int32_t N, int laser_scan_dir,
+                            float* d_ranges_out, float* d_intensities_out);
+
 /* Checkpoint: raw little-endian {magic, params, float L[band]} . */
 int dm_save(dm_grid* g, const char* path);
 int dm_load(dm_grid* g, const char* path);

@@ -315,3 +315,39 @@ void or_map_image(const int8_t* state, int64_t R, int64_t W, uint8_t* img) {
       img[(R - 1 - y) * W + x] = px;
     }
 }
+
+/* ------------------------------------------------------------------ a1 --- */
+/* LD06 PointData -> LaserScan.ranges/intensities, restating the driver's
+ * ToLaserscanMessagePublish (ldlidar_stl_ros2_node @0x7f853, x86-64 build in
+ * the reference; read from the disassembly, never executed):
+ *   range = (float)distance / 1000.0f                         @0x7fc54-0x7fc60
+ *   distance == 0 && intensity == 0 -> range = intensity = NaN @0x7fc96-0x7fcc5
+ *   angle_rad = (float)((double)deg * 3141.59 / 180000.0)      @0x7fd38-0x7fd58
+ *   idx = (int)ceilf((angle_rad - angle_min) / angle_increment) @0x7fd64-0x7fd89
+ *   idx >= N (or < 0) -> dropped                                @0x7fd93-0x7fdac
+ *   laser_scan_dir -> idx = N - idx - 1                         @0x7fff2-0x8000d
+ *   slot NaN -> range; else slot > range -> range (keep-min)    @0x80037-0x800e2
+ *   intensities[idx] = intensity (every point, in order)        @0x800e6-0x8011c
+ * with angle_min = 0.0f, angle_increment = (6.2831855f - 0.0f) / (float)(N - 1).
+ * Slots start NaN. */
+typedef struct { float angle_deg; uint16_t distance_mm; uint8_t intensity; uint8_t pad; } or_ld06_point;
+
+void or_ld06_to_scan(const or_ld06_point* pts, int64_t n, int32_t N, int laser_scan_dir,
+                     float* ranges, float* intensities) {
+  const float angle_min = 0.0f, angle_max = 6.2831855f;
+  const float inc = (angle_max - angle_min) / (float)(N - 1);
+  for (int32_t i = 0; i < N; ++i) { ranges[i] = NAN; if (intensities) intensities[i] = NAN; }
+  for (int64_t k = 0; k < n; ++k) {
+    float range = (float)pts[k].distance_mm / 1000.0f;
+    float inten = (float)pts[k].intensity;
+    if (pts[k].distance_mm == 0 && pts[k].intensity == 0) { range = NAN; inten = NAN; }
+    const float angle_rad = (float)((double)pts[k].angle_deg * 3141.59 / 180000.0);
+    const float q = (angle_rad - angle_min) / inc;
+    const int idx0 = (int)ceilf(q);
+    if (idx0 >= N || idx0 < 0) continue;
+    const int idx = laser_scan_dir ? N - idx0 - 1 : idx0;
+    if (isnan(ranges[idx])) ranges[idx] = range;
+    else if (ranges[idx] > range) ranges[idx] = range;
+    if (intensities) intensities[idx] = inten;
+  }
+}

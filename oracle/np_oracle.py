@@ -165,3 +165,30 @@ def map_image(state):
     img[state == 0] = 255
     img[state == 100] = 0
     return np.flipud(img)
+
+
+def ld06_to_scan(points, n_beams, laser_scan_dir=True):
+    """The LD06 driver's PointData -> LaserScan, float32
+    arithmetic step by step in NumPy, points in order."""
+    f32 = np.float32
+    inc = (f32(6.2831855) - f32(0.0)) / f32(n_beams - 1)
+    ranges = np.full(n_beams, np.nan, np.float32)
+    inten = np.full(n_beams, np.nan, np.float32)
+    for pt in points:
+        d, it = int(pt["distance_mm"]), int(pt["intensity"])
+        r = f32(d) / f32(1000.0)
+        iv = f32(it)
+        if d == 0 and it == 0:
+            r, iv = f32(np.nan), f32(np.nan)
+        ang = f32(float(np.float64(pt["angle_deg"])) * 3141.59 / 180000.0)
+        q = (ang - f32(0.0)) / inc
+        c = np.ceil(q)
+        if not (c >= 0 and c < n_beams):
+            continue
+        idx = int(c)
+        if laser_scan_dir:
+            idx = n_beams - idx - 1
+        if np.isnan(ranges[idx]) or ranges[idx] > r:
+            ranges[idx] = r
+        inten[idx] = iv
+    return ranges, inten

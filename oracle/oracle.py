@@ -51,6 +51,7 @@ def lib() -> ctypes.CDLL:
         L.or_line_length.restype = ctypes.c_int64
         L.or_state_from_logodds.argtypes = [P, vp, vp, ctypes.c_int64]
         L.or_map_image.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, vp]
+        L.or_ld06_to_scan.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int, vp, vp]
         _lib = L
     return _lib
 
@@ -136,3 +137,21 @@ class OracleMap:
         img = np.zeros((R, W), np.uint8)
         lib().or_map_image(_ptr(self.state), R, W, _ptr(img))
         return img
+
+
+def ld06_to_scans(points, offsets, n_beams, laser_scan_dir=True):
+    """LD06 PointData -> (ranges, intensities) [S, N] per the driver (a1)."""
+    from dm._ffi import LD06_POINT_DTYPE
+    pts = np.ascontiguousarray(points, dtype=np.dtype(LD06_POINT_DTYPE))
+    off = np.asarray(offsets, np.int64)
+    S = off.shape[0] - 1
+    ranges = np.empty((S, n_beams), np.float32)
+    inten = np.empty((S, n_beams), np.float32)
+    for s in range(S):
+        seg = np.ascontiguousarray(pts[off[s]:off[s + 1]])
+        r = np.empty(n_beams, np.float32)
+        i = np.empty(n_beams, np.float32)
+        lib().or_ld06_to_scan(_ptr(seg), seg.shape[0], n_beams, 1 if laser_scan_dir else 0,
+                              _ptr(r), _ptr(i))
+        ranges[s], inten[s] = r, i
+    return ranges, inten

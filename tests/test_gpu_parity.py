@@ -251,3 +251,53 @@ def test_profiling_counters():
         st = m.profile_read()
     assert st["tile_accum"][0] == 1 and st["tile_accum"][1] > 0
     assert "frontier_tile" in st
+
+
+def _window_world(seed, p, n_robots, n_beams, x0, y0, x1, y1, n_batches):
+    from dm import synth
+    world = synth.make_world(seed, x0 - 15, y0 - 15, x1 + 15, y1 + 15)
+    stream = synth.ScanStream(world, n_robots, n_beams, seed + 1, region=(x0, y0, x1, y1))
+    return [stream.next_batch() for _ in range(n_batches)]
+
+
+def test_c5_geometry_band_near_top(oracle_lib):
+    """C5 geometry (65536^2 @ 1 cm, rays of 1200 cells): a 2048-row band near
+    the top of the map, so global linear indices exceed 2^31 (int64 labels)."""
+    from dm import synth
+    W = H = 65536
+    res = 0.01
+    r0, rows = 62464, 2048
+    p = cases.make_params(W, H, resolution=res, band_row0=r0, band_rows=rows)
+    y0 = p.origin_y + (r0 + 300) * res
+    y1 = p.origin_y + (r0 + rows - 300) * res
+    batches = _window_world(51, p, 6, 4096, -3.0, y0, 3.0, y1, 2)
+    amin, inc = 0.0, float(synth.ld06_angle_increment(4096))
+    om = oracle_lib.OracleMap(p)
+    with dm.OccupancyMapper(p) as m:
+        for poses, ranges in batches:
+            assert m.integrate(poses, ranges, amin, inc) == om.integrate(poses, ranges, amin, inc)
+        assert_map_equal(m, om)
+        fr = m.frontiers(want_mask=True, want_labels=True)
+        mask, labels, clusters = om.frontiers()
+        assert_frontiers_equal(fr, mask, labels, clusters)
+        assert len(clusters) and clusters["label"].max() > 2 ** 31  # beyond int32
+
+
+@pytest.mark.parametrize("N", [12, 48, 192, 768, 4096])
+def test_c5_beam_density_sweep(oracle_lib, N):
+    """C5 scan-density sweep (12 .. 4096 beams per scan) on a 1 cm band."""
+    from dm import synth
+    W, H, res = 65536, 65536, 0.01
+    r0, rows = 30720, 2560
+    p = cases.make_params(W, H, resolution=res, band_row0=r0, band_rows=rows)
+    y0 = p.origin_y + (r0 + 100) * res
+    y1 = p.origin_y + (r0 + rows - 100) * res
+    batches = _window_world(60 + N, p, 8, N, -10.0, y0, 10.0, y1, 2)
+    amin, inc = 0.0, float(synth.ld06_angle_increment(N))
+    om = oracle_lib.OracleMap(p)
+    with dm.OccupancyMapper(p) as m:
+        for poses, ranges in batches:
+            assert m.integrate(poses, ranges, amin, inc) == om.integrate(poses, ranges, amin, inc)
+        assert_map_equal(m, om)
+        assert_frontiers_equal(m.frontiers(), None, None, om.frontiers(want_mask=False,
+                                                                         want_labels=False)[2])
