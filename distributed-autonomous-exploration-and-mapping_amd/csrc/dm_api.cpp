@@ -17,6 +17,11 @@
 
 #include "dm_internal.h"
 
+hipError_t dm_copy_shards(dm_grid* g) {
+  return hipMemcpyAsync(g->h_sh, g->ish, sizeof(unsigned long long) * 2 * kShards * kShardWords,
+                        hipMemcpyDeviceToHost, g->stream);
+}
+
 namespace {
 thread_local std::string t_err;
 
@@ -95,6 +100,7 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   if (act < 1) act = 1;
   if (act > g->act_cap) {
     int rc = dev_alloc(&g->act_tiles, act, "active tiles");
+    if (!rc) rc = dev_alloc(&g->act_raw, act * kShards, "first-touch lists");
     if (!rc) rc = dev_alloc(&g->act_off, act, "active offsets");
     if (!rc) rc = dev_alloc(&g->act_cur, act, "active cursors");
     if (rc) return rc;
@@ -146,14 +152,28 @@ int ensure_trig(dm_grid* g, int32_t N, float amin, float inc) {
 int grow_slots(dm_grid* g, int64_t need) {
   int64_t cap = std::max<int64_t>(need, 2 * g->slot_cap);
   if (cap < (1 << 16)) cap = 1 << 16;
+  cap = ceil_div(cap, kShards) * kShards;  // kShards equal regions (k_frontier_tile)
   int rc = dev_alloc(&g->slot_label, cap, "slot labels");
   if (!rc) rc = dev_alloc(&g->slot_parent, cap, "slot parents");
   if (!rc) rc = dev_alloc(&g->slot_root, cap, "slot roots");
   if (!rc) rc = dev_alloc(&g->slot_own, 3 * cap, "slot sums");
   if (!rc) rc = dev_alloc(&g->slot_acc, 3 * cap, "slot totals");
   if (!rc) rc = dev_alloc(&g->clusters, 4 * cap, "clusters");
+  if (!rc) rc = dev_alloc(&g->out_clu, cap, "sorted clusters");
   if (rc) return rc;
   g->slot_cap = cap;
+  return DM_OK;
+}
+
+int grow_host_out(dm_grid* g, int64_t need) {
+  if (need <= g->h_out_cap) return DM_OK;
+  int64_t cap = std::max<int64_t>(need, 2 * g->h_out_cap);
+  if (g->stream) DM_HIP(hipStreamSynchronize(g->stream));
+  if (g->h_out) (void)hipHostFree(g->h_out);
+  g->h_out = nullptr;
+  g->h_out_cap = 0;
+  DM_HIP(hipHostMalloc((void**)&g->h_out, sizeof(dm_cluster) * (size_t)cap, hipHostMallocDefault));
+  g->h_out_cap = cap;
   return DM_OK;
 }
 
@@ -179,6 +199,7 @@ int check_integrate_args(int32_t S, int32_t N, const void* poses, const void* ra
 int finish_counts(dm_grid* g, uint64_t* U, uint64_t* T) {
   DM_HIP(hipMemcpyAsync(g->h_cnt, g->cnt, sizeof(unsigned long long) * CNT_N,
                         hipMemcpyDeviceToHost, g->stream));
+  DM_HIP(dm_copy_shards(g));
   DM_HIP(hipStreamSynchronize(g->stream));
   if (g->h_cnt[CNT_OVERFLOW] & 11ull) {
     // cannot happen with the bounds in grow_integrate; keep the map consistent anyway
@@ -186,8 +207,8 @@ int finish_counts(dm_grid* g, uint64_t* U, uint64_t* T) {
     return dm_set_error(DM_ERR_CAPACITY, "integrate workspace overflow (flags %llu)",
                         (unsigned long long)g->h_cnt[CNT_OVERFLOW]);
   }
-  if (U) *U = g->h_cnt[CNT_U];
-  if (T) *T = g->h_cnt[CNT_T];
+  if (U) *U = dm_shard_sum(g->h_sh, SH_U);
+  if (T) *T = dm_shard_sum(g->h_sh, SH_T);
   return DM_OK;
 }
 
@@ -289,6 +310,8 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if ((rc = dev_alloc(&g->tile_slot, g->NT, "tile slots"))) return fail(rc);
   if ((rc = dev_alloc(&g->tile_free, g->NT, "tile free counts"))) return fail(rc);
   if ((rc = dev_alloc(&g->cnt, CNT_N, "counters"))) return fail(rc);
+  if ((rc = dev_alloc(&g->ish, 2 * kShards * kShardWords, "shard counters"))) return fail(rc);
+  g->fsh = g->ish + kShards * kShardWords;
   if ((rc = dev_alloc(&g->ftiles, g->NT, "frontier tiles"))) return fail(rc);
   if ((rc = dev_alloc(&g->fmap, g->NT, "frontier tile map"))) return fail(rc);
   if ((rc = dev_alloc(&g->border, g->NT * 256, "frontier borders"))) return fail(rc);
@@ -296,8 +319,12 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if ((rc = dev_alloc(&g->edge_label, 2 * g->W, "edge labels"))) return fail(rc);
   if ((rc = dev_alloc(&g->halo, 2 * g->W, "halo rows"))) return fail(rc);
   if ((rc = grow_slots(g, 1 << 16))) return fail(rc);
+  if ((rc = grow_host_out(g, 1 << 14))) return fail(rc);
   e = hipHostMalloc((void**)&g->h_cnt, sizeof(unsigned long long) * CNT_N, hipHostMallocDefault);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipHostMalloc(counters)"));
+  e = hipHostMalloc((void**)&g->h_sh, sizeof(unsigned long long) * 2 * kShards * kShardWords,
+                    hipHostMallocDefault);
+  if (e != hipSuccess) return fail(dm_hip_check(e, "hipHostMalloc(shard counters)"));
   e = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate"));
   g->own_stream = true;
@@ -319,8 +346,10 @@ int dm_destroy(dm_grid* g) {
   dev_free(g->border); dev_free(g->slot_label); dev_free(g->slot_parent); dev_free(g->slot_root);
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
   dev_free(g->edge_slot); dev_free(g->edge_label); dev_free(g->mask); dev_free(g->labels);
-  dev_free(g->halo);
+  dev_free(g->halo); dev_free(g->out_clu); dev_free(g->ish); dev_free(g->act_raw);
   if (g->h_cnt) (void)hipHostFree(g->h_cnt);
+  if (g->h_sh) (void)hipHostFree(g->h_sh);
+  if (g->h_out) (void)hipHostFree(g->h_out);
   if (g->h_pose4) (void)hipHostFree(g->h_pose4);
   if (g->stream && g->own_stream) (void)hipStreamDestroy(g->stream);
   delete g;
@@ -420,12 +449,16 @@ int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out) {
   if (cap > 0 && !out) return dm_set_error(DM_ERR_INVALID_ARG, "out is NULL");
   DM_HIP(hipMemcpyAsync(g->h_cnt, g->cnt, sizeof(unsigned long long) * CNT_N,
                         hipMemcpyDeviceToHost, g->stream));
+  DM_HIP(dm_copy_shards(g));
   DM_HIP(hipStreamSynchronize(g->stream));
-  const uint64_t v[7] = {g->h_cnt[CNT_U],   g->h_cnt[CNT_T],     g->h_cnt[CNT_TH],
-                         g->h_cnt[CNT_SEGS], g->h_cnt[CNT_ACTIVE], g->h_cnt[CNT_ITEMS],
-                         g->h_cnt[CNT_HEAVY]};
-  for (int32_t i = 0; i < cap && i < 7; ++i) out[i] = v[i];
-  if (n_out) *n_out = 7;
+  const unsigned long long* fs = g->h_sh + kShards * kShardWords;
+  const uint64_t v[10] = {dm_shard_sum(g->h_sh, SH_U),  dm_shard_sum(g->h_sh, SH_T),
+                          dm_shard_sum(g->h_sh, SH_TH), g->h_cnt[CNT_SEGS],
+                          g->h_cnt[CNT_ACTIVE],         g->h_cnt[CNT_ITEMS],
+                          g->h_cnt[CNT_HEAVY],          g->h_cnt[CNT_FTILES],
+                          dm_shard_sum(fs, SH_SLOT),    g->h_cnt[CNT_CLUSTERS]};
+  for (int32_t i = 0; i < cap && i < 10; ++i) out[i] = v[i];
+  if (n_out) *n_out = 10;
   return DM_OK;
 }
 
@@ -490,32 +523,44 @@ int dm_frontiers(dm_grid* g, uint8_t* mask, int64_t* labels, dm_cluster* out, in
     if ((rc = dev_alloc(&g->cell_slot, cells, "dense cell slots"))) return rc;
     if ((rc = dev_alloc(&g->labels, cells, "dense labels"))) return rc;
   }
-  int64_t n = 0;
+  int64_t n = 0, copied = 0;
   for (int attempt = 0; attempt < 8; ++attempt) {
-    rc = dm_launch_frontiers(g, mask != nullptr, labels != nullptr, &n);
+    rc = dm_launch_frontiers(g, mask != nullptr, labels != nullptr, &n, &copied);
     if (rc != DM_ERR_CAPACITY) break;
     if ((rc = grow_slots(g, n + n / 2 + 1024))) return rc;
     rc = DM_ERR_CAPACITY;
   }
   if (rc) return rc == DM_ERR_CAPACITY ? dm_set_error(rc, "frontier slot arrays kept overflowing") : rc;
   g->frontier_valid = true;
-  std::vector<HostCluster> hc((size_t)n);
-  if (n > 0)
-    DM_HIP(hipMemcpy(hc.data(), g->clusters, sizeof(HostCluster) * (size_t)n, hipMemcpyDeviceToHost));
-  std::sort(hc.begin(), hc.end(),
-            [](const HostCluster& a, const HostCluster& b) { return a.label < b.label; });
   const int64_t nw = std::min<int64_t>(n, cap);
-  for (int64_t i = 0; i < nw; ++i) {
-    dm_cluster& c = out[i];
-    c.label = hc[i].label;
-    c.size = hc[i].size;
-    c.sum_x = hc[i].sum_x;
-    c.sum_y = hc[i].sum_y;
-    const double mx = (double)c.sum_x / (double)c.size;
-    const double my = (double)c.sum_y / (double)c.size;
-    c.cx_m = g->p.origin_x + (mx + 0.5) * g->p.resolution;
-    c.cy_m = g->p.origin_y + (my + 0.5) * g->p.resolution;
+  if (g->h_cnt[CNT_SORTED]) {
+    // sorted records with centroids, computed on the device; the first
+    // clu_hint of them arrived together with the counters
+    const int64_t have = std::min<int64_t>(copied, nw);
+    if (have > 0) memcpy(out, g->h_out, sizeof(dm_cluster) * (size_t)have);
+    if (nw > have)
+      DM_HIP(hipMemcpy(out + have, g->out_clu + have, sizeof(dm_cluster) * (size_t)(nw - have),
+                       hipMemcpyDeviceToHost));
+  } else {  // too many clusters / labels >= 2^32: sort the raw records here
+    std::vector<HostCluster> hc((size_t)n);
+    if (n > 0)
+      DM_HIP(hipMemcpy(hc.data(), g->clusters, sizeof(HostCluster) * (size_t)n, hipMemcpyDeviceToHost));
+    std::sort(hc.begin(), hc.end(),
+              [](const HostCluster& a, const HostCluster& b) { return a.label < b.label; });
+    for (int64_t i = 0; i < nw; ++i) {
+      dm_cluster& c = out[i];
+      c.label = hc[i].label;
+      c.size = hc[i].size;
+      c.sum_x = hc[i].sum_x;
+      c.sum_y = hc[i].sum_y;
+      const double mx = (double)c.sum_x / (double)c.size;
+      const double my = (double)c.sum_y / (double)c.size;
+      c.cx_m = g->p.origin_x + (mx + 0.5) * g->p.resolution;
+      c.cy_m = g->p.origin_y + (my + 0.5) * g->p.resolution;
+    }
   }
+  g->clu_hint = std::max<int64_t>(1024, n + n / 4 + 64);
+  if (g->clu_hint > g->h_out_cap && (rc = grow_host_out(g, g->clu_hint))) return rc;
   if (mask) DM_HIP(hipMemcpy(mask, g->mask, (size_t)cells, hipMemcpyDeviceToHost));
   if (labels) DM_HIP(hipMemcpy(labels, g->labels, sizeof(int64_t) * (size_t)cells, hipMemcpyDeviceToHost));
   if (n_out) *n_out = n;

@@ -22,10 +22,11 @@
 //   k_frontier_resolve / k_frontier_compact  roots, int64 sums, cluster list
 #include "dm_internal.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr int kFT = 256;              // threads per frontier workgroup
-constexpr int kHP = DM_TS + 2;        // halo tile pitch (66)
 constexpr int kMaxRoots = 1024;       // 8-connected components in a 64x64 tile
 
 struct FGeom {
@@ -34,6 +35,7 @@ struct FGeom {
   int32_t want_mask, want_labels;
   int64_t H;
   int64_t slot_cap;
+  int64_t slot_per;  // slot_cap / kShards: slots of one shard region
   int64_t clu_cap;
   int64_t min_size;
 };
@@ -117,7 +119,7 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
     long long* __restrict__ slot_label, int32_t* __restrict__ slot_parent,
     long long* __restrict__ slot_own, long long* __restrict__ slot_acc,
     uint8_t* __restrict__ mask, int32_t* __restrict__ cell_slot, int32_t* __restrict__ edge_slot,
-    unsigned long long* cnt) {
+    unsigned long long* cnt, unsigned long long* fsh) {
   __shared__ uint64_t s_unk[DM_TS + 2];    // row y at index y+1, bit c = column c
   __shared__ uint8_t s_unkL[DM_TS + 2];    // column -1
   __shared__ uint8_t s_unkR[DM_TS + 2];    // column 64
@@ -273,7 +275,10 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
       }
     }
     __syncthreads();
-    if (tid == 0) sbase = (long long)atomicAdd(&cnt[CNT_SLOTS], (unsigned long long)nroots);
+    // slots come from this workgroup's shard region [shard*slot_per, +slot_per)
+    if (tid == 0)
+      sbase = (long long)atomicAdd(&fsh[(blockIdx.x % kShards) * kShardWords + SH_SLOT],
+                                   (unsigned long long)nroots);
     for (int r = tid; r < nruns; r += kFT) {
       const int c = r_rid[r_par[r]];
       const uint32_t s0 = r_s[r], e0 = r_e[r], len = e0 - s0 + 1;
@@ -283,10 +288,11 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
     }
     __syncthreads();
     const long long base = sbase;
+    const long long sh0 = (long long)(blockIdx.x % kShards) * g.slot_per;
     const int nr = nroots;
     for (int c = tid; c < nr; c += kFT) {
-      const long long slot = base + c;
-      if (slot >= g.slot_cap) { atomicOr(&cnt[CNT_OVERFLOW], 4ull); continue; }
+      if (base + c >= g.slot_per) { atomicOr(&cnt[CNT_OVERFLOW], 4ull); continue; }
+      const long long slot = sh0 + base + c;
       const int r = c_run[c];
       const long long gy = (long long)g.row0 + ty0 + r_y[r];
       const long long gx = (long long)tx0 + r_s[r];
@@ -306,7 +312,7 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
       long long sl = -1;
       if ((s_F[y] >> x) & 1ull) {
         sl = base + r_rid[r_par[run_of(s_rbase, s_start, y, x)]];
-        if (sl >= g.slot_cap) sl = -1;
+        sl = sl < g.slot_per ? sh0 + sl : -1;
       }
       border[j * 256 + tid] = (int32_t)sl;
     }
@@ -323,7 +329,7 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
         long long sl = -1;
         if (f) {
           sl = base + r_rid[r_par[run_of(s_rbase, s_start, y, x)]];
-          if (sl >= g.slot_cap) sl = -1;
+          sl = sl < g.slot_per ? sh0 + sl : -1;
         }
         const int64_t gi = (int64_t)gy * g.W + gx;
         if (g.want_mask) mask[gi] = f;
@@ -362,77 +368,90 @@ __device__ inline void g_unite(int32_t* par, const long long* label, int32_t a, 
   }
 }
 
+// Unions across tile borders.  Consecutive border cells of a frontier that
+// crosses the border usually join the same two slots; a lane skips every pair
+// its predecessor lane (the previous border cell) already issued, so repeated
+// unions do not queue same-address atomics behind each other.
 __global__ __launch_bounds__(256) void k_frontier_merge(FGeom g, const int32_t* __restrict__ ftiles,
                                                         const int32_t* __restrict__ fmap,
                                                         const int32_t* __restrict__ border,
                                                         const long long* __restrict__ slot_label,
                                                         int32_t* slot_parent,
                                                         const unsigned long long* cnt) {
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = __lane_id();
   const int64_t nft = (int64_t)cnt[CNT_FTILES];
   for (int64_t j = blockIdx.x; j < nft; j += gridDim.x) {
     const int32_t tile = ftiles[j];
     const int32_t tx = tile % g.TX, ty = tile / g.TX;
     const int32_t* bA = border + j * 256;
-    if (tid < 64) {  // right neighbour: our last column vs its first column
-      const int32_t sa = bA[3 * 64 + tid];
-      if (sa >= 0 && tx + 1 < g.TX) {
-        const int32_t fb = fmap[ty * g.TX + tx + 1];
-        if (fb >= 0) {
-          const int32_t* bB = border + (int64_t)fb * 256;
-          for (int d = -1; d <= 1; ++d) {
-            const int y2 = tid + d;
-            if (y2 < 0 || y2 > 63) continue;
-            const int32_t sb = bB[2 * 64 + y2];
-            if (sb >= 0) g_unite(slot_parent, slot_label, sa, sb);
-          }
-        }
+    // candidate pairs of this lane: (sa, sb[0..2]); -1 = none
+    int32_t sa = -1, sb[3] = {-1, -1, -1};
+    if (tid < 64) {  // our last column vs the right neighbour's first column
+      sa = bA[3 * 64 + tid];
+      int32_t nb;
+      if (sa >= 0 && tx + 1 < g.TX && (nb = fmap[ty * g.TX + tx + 1]) >= 0) {
+        const int32_t* bB = border + (int64_t)nb * 256 + 2 * 64;
+        for (int d = -1; d <= 1; ++d)
+          if (tid + d >= 0 && tid + d < 64) sb[d + 1] = bB[tid + d];
       }
-    } else if (tid < 128) {  // next tile row: our last row vs its first row
+    } else if (tid < 128) {  // our last row vs the next tile row's first row
       const int x = tid - 64;
-      const int32_t sa = bA[1 * 64 + x];
-      if (sa >= 0 && ty + 1 < g.TY) {
-        const int32_t fc = fmap[(ty + 1) * g.TX + tx];
-        if (fc >= 0) {
-          const int32_t* bC = border + (int64_t)fc * 256;
-          for (int d = -1; d <= 1; ++d) {
-            const int x2 = x + d;
-            if (x2 < 0 || x2 > 63) continue;
-            const int32_t sb = bC[x2];
-            if (sb >= 0) g_unite(slot_parent, slot_label, sa, sb);
-          }
-        }
+      sa = bA[1 * 64 + x];
+      int32_t nb;
+      if (sa >= 0 && ty + 1 < g.TY && (nb = fmap[(ty + 1) * g.TX + tx]) >= 0) {
+        const int32_t* bC = border + (int64_t)nb * 256;
+        for (int d = -1; d <= 1; ++d)
+          if (x + d >= 0 && x + d < 64) sb[d + 1] = bC[x + d];
       }
-    } else if (tid == 128) {  // diagonal: our (63,63) vs (tx+1,ty+1)'s (0,0)
-      const int32_t sa = bA[1 * 64 + 63];
-      if (sa >= 0 && tx + 1 < g.TX && ty + 1 < g.TY) {
-        const int32_t fd = fmap[(ty + 1) * g.TX + tx + 1];
-        if (fd >= 0) {
-          const int32_t sb = border[(int64_t)fd * 256 + 0];
-          if (sb >= 0) g_unite(slot_parent, slot_label, sa, sb);
-        }
-      }
-    } else if (tid == 129) {  // anti-diagonal: our (0,63) vs (tx-1,ty+1)'s (63,0)
-      const int32_t sa = bA[1 * 64 + 0];
-      if (sa >= 0 && tx > 0 && ty + 1 < g.TY) {
-        const int32_t fe = fmap[(ty + 1) * g.TX + tx - 1];
-        if (fe >= 0) {
-          const int32_t sb = border[(int64_t)fe * 256 + 63];
-          if (sb >= 0) g_unite(slot_parent, slot_label, sa, sb);
-        }
-      }
+    } else if (tid == 128) {  // our (63,63) vs (tx+1,ty+1)'s (0,0)
+      sa = bA[1 * 64 + 63];
+      int32_t nb;
+      if (sa >= 0 && tx + 1 < g.TX && ty + 1 < g.TY && (nb = fmap[(ty + 1) * g.TX + tx + 1]) >= 0)
+        sb[1] = border[(int64_t)nb * 256 + 0];
+    } else if (tid == 129) {  // our (0,63) vs (tx-1,ty+1)'s (63,0)
+      sa = bA[1 * 64 + 0];
+      int32_t nb;
+      if (sa >= 0 && tx > 0 && ty + 1 < g.TY && (nb = fmap[(ty + 1) * g.TX + tx - 1]) >= 0)
+        sb[1] = border[(int64_t)nb * 256 + 63];
+    }
+    // predecessor lane's pairs (lanes 0 of waves 0/1 start an edge: none)
+    const int32_t psa = __shfl_up(sa, 1);
+    int32_t psb[3];
+    for (int q = 0; q < 3; ++q) psb[q] = __shfl_up(sb[q], 1);
+    const bool has_prev = lane > 0 && tid < 128;
+    for (int q = 0; q < 3; ++q) {
+      const int32_t b = sb[q];
+      if (sa < 0 || b < 0) continue;
+      bool dup = false;
+      for (int r = 0; r < q; ++r) dup |= sb[r] == b;
+      if (has_prev && psa == sa) dup |= (psb[0] == b) | (psb[1] == b) | (psb[2] == b);
+      if (!dup) g_unite(slot_parent, slot_label, sa, b);
     }
   }
+}
+
+// Slot s is in use iff its offset inside its shard region is below that
+// shard's allocation count.
+__device__ inline void load_shard_counts(const FGeom& g, const unsigned long long* fsh, int64_t* s_n) {
+  if (threadIdx.x < kShards)
+    s_n[threadIdx.x] = min((int64_t)fsh[threadIdx.x * kShardWords + SH_SLOT], g.slot_per);
+  __syncthreads();
+}
+
+__device__ inline bool slot_used(const FGeom& g, const int64_t* s_n, int64_t s) {
+  return s < g.slot_cap && (s % g.slot_per) < s_n[s / g.slot_per];
 }
 
 __global__ __launch_bounds__(256) void k_frontier_resolve(FGeom g, const int32_t* __restrict__ slot_parent,
                                                           int32_t* __restrict__ slot_root,
                                                           const long long* __restrict__ slot_own,
                                                           long long* slot_acc,
-                                                          const unsigned long long* cnt) {
-  const int64_t ns = min((int64_t)cnt[CNT_SLOTS], g.slot_cap);
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ns;
+                                                          const unsigned long long* fsh) {
+  __shared__ int64_t s_n[kShards];
+  load_shard_counts(g, fsh, s_n);
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < g.slot_cap;
        s += (int64_t)gridDim.x * blockDim.x) {
+    if (!slot_used(g, s_n, s)) continue;
     int32_t r = (int32_t)s;
     for (int it = 0; it < (1 << 22); ++it) {
       const int32_t p = slot_parent[r];
@@ -448,18 +467,30 @@ __global__ __launch_bounds__(256) void k_frontier_resolve(FGeom g, const int32_t
   }
 }
 
+// Roots of size >= min_size become cluster records; one counter atomic per
+// wave (ballot + popcount) instead of one per cluster.
 __global__ __launch_bounds__(256) void k_frontier_compact(FGeom g, const int32_t* __restrict__ slot_root,
                                                           const long long* __restrict__ slot_label,
                                                           const long long* __restrict__ slot_acc,
                                                           long long* __restrict__ clusters,
-                                                          unsigned long long* cnt) {
-  const int64_t ns = min((int64_t)cnt[CNT_SLOTS], g.slot_cap);
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ns;
-       s += (int64_t)gridDim.x * blockDim.x) {
-    if (slot_root[s] != (int32_t)s) continue;
-    const long long sz = slot_acc[3 * s];
-    if (sz < g.min_size) continue;
-    const unsigned long long k = atomicAdd(&cnt[CNT_CLUSTERS], 1ull);
+                                                          unsigned long long* cnt,
+                                                          const unsigned long long* fsh) {
+  __shared__ int64_t s_n[kShards];
+  load_shard_counts(g, fsh, s_n);
+  const int lane = __lane_id();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); s0 < g.slot_cap; s0 += stride) {
+    const int64_t s = s0 + lane;
+    bool keep = slot_used(g, s_n, s) && slot_root[s] == (int32_t)s;
+    const long long sz = keep ? slot_acc[3 * s] : 0;
+    keep = keep && sz >= g.min_size;
+    const unsigned long long bal = __ballot(keep);
+    if (!bal) continue;
+    unsigned long long k0 = 0;
+    if (lane == __ffsll(bal) - 1) k0 = atomicAdd(&cnt[CNT_CLUSTERS], (unsigned long long)__popcll(bal));
+    k0 = __shfl(k0, __ffsll(bal) - 1);
+    if (!keep) continue;
+    const unsigned long long k = k0 + __popcll(bal & ((1ull << lane) - 1));
     if ((int64_t)k >= g.clu_cap) continue;
     clusters[4 * k + 0] = slot_label[s];
     clusters[4 * k + 1] = sz;
@@ -468,6 +499,61 @@ __global__ __launch_bounds__(256) void k_frontier_compact(FGeom g, const int32_t
   }
 }
 
+// Cluster list sorted by label, with centroids (SPEC a10), in one workgroup:
+// bitonic sort of (label << 32 | record) keys in LDS, then dm_cluster records
+// with cx_m = ox + ((double)sum_x / (double)size + 0.5) * res (double, IEEE
+// division on both host and device).  Requires labels < 2^32 (W*H <= 2^32)
+// and at most kSortCap clusters; otherwise CNT_SORTED stays 0 and the host
+// sorts the raw records.
+constexpr int kSortCap = 16384;  // 128 KiB of keys
+constexpr int kSortThreads = 1024;
+
+__global__ __launch_bounds__(kSortThreads) void k_sort_clusters(double ox, double oy, double res,
+                                                                int labels_fit,
+                                                                const long long* __restrict__ clusters,
+                                                                dm_cluster* __restrict__ out,
+                                                                unsigned long long* cnt) {
+  __shared__ unsigned long long keys[kSortCap];
+  const int tid = threadIdx.x;
+  const int64_t K = (int64_t)cnt[CNT_CLUSTERS];
+  if (!labels_fit || K > kSortCap) {
+    if (tid == 0) cnt[CNT_SORTED] = 0;
+    return;
+  }
+  int P = 1;
+  while (P < K) P <<= 1;
+  for (int i = tid; i < P; i += kSortThreads)
+    keys[i] = i < K ? (((unsigned long long)clusters[4 * i] << 32) | (uint32_t)i) : ~0ull;
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int jj = k >> 1; jj > 0; jj >>= 1) {
+      for (int i = tid; i < P; i += kSortThreads) {
+        const int l = i ^ jj;
+        if (l > i) {
+          const unsigned long long a = keys[i], b = keys[l];
+          if ((a > b) == ((i & k) == 0)) { keys[i] = b; keys[l] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < K; i += kSortThreads) {
+    const int64_t r = (int64_t)(keys[i] & 0xFFFFFFFFull);
+    dm_cluster c;
+    c.label = clusters[4 * r + 0];
+    c.size = clusters[4 * r + 1];
+    c.sum_x = clusters[4 * r + 2];
+    c.sum_y = clusters[4 * r + 3];
+    const double mx = (double)c.sum_x / (double)c.size;
+    const double my = (double)c.sum_y / (double)c.size;
+    c.cx_m = ox + (mx + 0.5) * res;
+    c.cy_m = oy + (my + 0.5) * res;
+    out[i] = c;
+  }
+  if (tid == 0) cnt[CNT_SORTED] = 1;
+}
+
+// Cell slot -> final label (the root of a set is its min-label slot).
 __global__ __launch_bounds__(256) void k_slot_labels(int64_t n, const int32_t* __restrict__ cslot,
                                                      const int32_t* __restrict__ slot_root,
                                                      const long long* __restrict__ slot_label,
@@ -488,10 +574,7 @@ int grid_for(int64_t n, int threads, int64_t cap) {
 
 }  // namespace
 
-// Runs the frontier pipeline.  Returns DM_ERR_CAPACITY (with *n_clusters set
-// to the number of slots needed) when the slot arrays overflowed; the caller
-// grows them and reruns.
-int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters) {
+static FGeom make_fgeom(const dm_grid* g, bool want_mask, bool want_labels) {
   FGeom fg;
   fg.W = (int32_t)g->W;
   fg.R = (int32_t)g->R;
@@ -504,11 +587,21 @@ int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n
   fg.want_labels = want_labels ? 1 : 0;
   fg.H = g->H;
   fg.slot_cap = g->slot_cap;
+  fg.slot_per = g->slot_cap / kShards;
   fg.clu_cap = g->slot_cap;
   fg.min_size = g->p.min_frontier_size;
-  const int64_t cells = g->R * g->W;
+  return fg;
+}
 
+// Runs the frontier pipeline and copies the counters plus a speculative first
+// chunk of the sorted cluster records into g->h_out with ONE synchronisation.  Returns DM_ERR_CAPACITY (with *n_clusters = slots needed)
+// when the slot arrays overflowed; the caller grows them and reruns.
+int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters,
+                        int64_t* copied) {
+  const FGeom fg = make_fgeom(g, want_mask, want_labels);
+  const int64_t cells = g->R * g->W;
   DM_HIP(hipMemsetAsync(g->cnt + CNT_FTILES, 0, sizeof(unsigned long long) * 4, g->stream));
+  DM_HIP(hipMemsetAsync(g->fsh, 0, sizeof(unsigned long long) * kShards * kShardWords, g->stream));
   DM_HIP(hipMemsetAsync(g->edge_slot, 0xFF, sizeof(int32_t) * 2 * g->W, g->stream));
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));
@@ -523,7 +616,7 @@ int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n
   dm_timer_begin(g, "frontier_tile", &t);
   hipLaunchKernelGGL(k_frontier_tile, dim3(nft_grid), dim3(kFT), 0, g->stream, fg, g->state,
                      g->halo, g->ftiles, g->border, g->slot_label, g->slot_parent, g->slot_own,
-                     g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt);
+                     g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "frontier_merge", &t);
@@ -534,12 +627,12 @@ int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n
   const int sgrid = grid_for(g->slot_cap, 256, 1024);
   dm_timer_begin(g, "frontier_resolve", &t);
   hipLaunchKernelGGL(k_frontier_resolve, dim3(sgrid), dim3(256), 0, g->stream, fg,
-                     g->slot_parent, g->slot_root, g->slot_own, g->slot_acc, g->cnt);
+                     g->slot_parent, g->slot_root, g->slot_own, g->slot_acc, g->fsh);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "frontier_compact", &t);
   hipLaunchKernelGGL(k_frontier_compact, dim3(sgrid), dim3(256), 0, g->stream, fg,
-                     g->slot_root, g->slot_label, g->slot_acc, g->clusters, g->cnt);
+                     g->slot_root, g->slot_label, g->slot_acc, g->clusters, g->cnt, g->fsh);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_slot_labels, dim3(grid_for(2 * g->W, 256, 1024)), dim3(256), 0, g->stream,
@@ -550,12 +643,26 @@ int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n
                        cells, g->cell_slot, g->slot_root, g->slot_label, g->labels);
     DM_HIP(hipGetLastError());
   }
+  const int labels_fit = (double)g->W * (double)(g->row0 + g->R) <= 4294967296.0 ? 1 : 0;
+  dm_timer_begin(g, "sort_clusters", &t);
+  hipLaunchKernelGGL(k_sort_clusters, dim3(1), dim3(kSortThreads), 0, g->stream, g->p.origin_x,
+                     g->p.origin_y, g->p.resolution, labels_fit, g->clusters, g->out_clu, g->cnt);
+  dm_timer_end(g, &t);
+  DM_HIP(hipGetLastError());
+  const int64_t hint = std::min<int64_t>(std::min<int64_t>(g->clu_hint, g->h_out_cap), g->slot_cap);
   DM_HIP(hipMemcpyAsync(g->h_cnt, g->cnt, sizeof(unsigned long long) * CNT_N, hipMemcpyDeviceToHost,
                         g->stream));
+  if (hint > 0)
+    DM_HIP(hipMemcpyAsync(g->h_out, g->out_clu, sizeof(dm_cluster) * (size_t)hint,
+                          hipMemcpyDeviceToHost, g->stream));
+  DM_HIP(dm_copy_shards(g));
   DM_HIP(hipStreamSynchronize(g->stream));
-  const unsigned long long slots = g->h_cnt[CNT_SLOTS];
-  if ((int64_t)slots > g->slot_cap || (g->h_cnt[CNT_OVERFLOW] & 4ull)) {
-    *n_clusters = (int64_t)slots;
+  *copied = hint;
+  unsigned long long most = 0;
+  const unsigned long long* fs = g->h_sh + kShards * kShardWords;
+  for (int i = 0; i < kShards; ++i) most = std::max(most, fs[i * kShardWords + SH_SLOT]);
+  if ((int64_t)most > g->slot_cap / kShards || (g->h_cnt[CNT_OVERFLOW] & 4ull)) {
+    *n_clusters = (int64_t)most * kShards;  // slot capacity that fits the fullest shard
     return DM_ERR_CAPACITY;
   }
   *n_clusters = (int64_t)g->h_cnt[CNT_CLUSTERS];

@@ -70,24 +70,53 @@ __device__ inline int hash_find(const int32_t* hkey, int32_t tile) {
   return -1;
 }
 
-__device__ inline void first_touch(const Geom& g, int32_t tile, int32_t old, int32_t* tile_slot,
-                                   int32_t* act_tiles, unsigned long long* cnt) {
+// Loop-free wave aggregation of the pieces emitted by the active lanes right
+// now: a run is a maximal group of consecutive active lanes with the same
+// tile (lane i+1 holds the next beam of the scan, so most pieces of a wave
+// fall in a few runs).  Only the head lane of a run touches the hash table /
+// global counters, with the run's length; the others take a rank in the run.
+struct LaneRun {
+  bool head;
+  int head_lane;
+  int len;   // valid in the head lane
+  int rank;  // active lanes of the run before this lane
+};
+
+__device__ inline LaneRun lane_run(int32_t tile) {
+  const int lane = lane_id();
+  const unsigned long long act = __ballot(1);
+  const int32_t prev = __shfl_up(tile, 1);
+  const bool prev_act = lane > 0 && ((act >> (lane - 1)) & 1ull);
+  const bool head = !(prev_act && prev == tile);
+  const unsigned long long heads = __ballot(head);
+  const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= lane
+  LaneRun r;
+  r.head = head;
+  r.head_lane = 63 - __clzll(heads & le);
+  const unsigned long long after = heads & ~le;
+  const unsigned long long before_end = after ? ((1ull << (__ffsll(after) - 1)) - 1ull) : ~0ull;
+  const unsigned long long from_head = ~((1ull << r.head_lane) - 1ull);
+  r.len = __popcll(act & from_head & before_end);
+  r.rank = __popcll(act & from_head & ((1ull << lane) - 1ull));
+  return r;
+}
+
+// First touch of a tile in this call: append it to this workgroup's shard of
+// the active list (k_plan compacts the shards and assigns tile slots).
+__device__ inline void first_touch(const Geom& g, int32_t tile, int32_t old, int32_t* act_raw,
+                                   unsigned long long* ish, unsigned long long* cnt) {
   if (old != 0) return;
-  const unsigned long long slot = atomicAdd(&cnt[CNT_ACTIVE], 1ull);
-  if (slot < (unsigned long long)g.act_cap) {
-    act_tiles[slot] = tile;
-    tile_slot[tile] = (int32_t)slot;
-  } else {
-    tile_slot[tile] = -1;
-    atomicOr(&cnt[CNT_OVERFLOW], 1ull);
-  }
+  const int sh = blockIdx.x % kShards;
+  const unsigned long long l = atomicAdd(&ish[sh * kShardWords + SH_ACT], 1ull);
+  if (l < (unsigned long long)g.act_cap) act_raw[(int64_t)sh * g.act_cap + (int64_t)l] = tile;
+  else atomicOr(&cnt[CNT_OVERFLOW], 1ull);
 }
 
 __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const double* __restrict__ pose4,
                                                    const float* __restrict__ ranges,
                                                    const double* __restrict__ trig,
                                                    Beam* __restrict__ beams, int32_t* tile_count,
-                                                   int32_t* tile_slot, int32_t* act_tiles,
+                                                   int32_t* act_raw, unsigned long long* ish,
                                                    unsigned long long* cnt) {
   __shared__ int32_t hkey[kHash];
   __shared__ int32_t hcnt[kHash];
@@ -102,12 +131,15 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
     beams[b] = bm;
     if (bm.flags & 1) {
       dm_for_each_piece(bm, g.r, [&](int32_t tile, int32_t, int32_t) {
-        const int h = hash_insert(hkey, tile);
-        if (h >= 0) {
-          atomicAdd(&hcnt[h], 1);
-        } else {
-          const int32_t old = atomicAdd(&tile_count[tile], 1);
-          first_touch(g, tile, old, tile_slot, act_tiles, cnt);
+        const LaneRun run = lane_run(tile);
+        if (run.head) {
+          const int h = hash_insert(hkey, tile);
+          if (h >= 0) {
+            atomicAdd(&hcnt[h], run.len);
+          } else {
+            const int32_t old = atomicAdd(&tile_count[tile], run.len);
+            first_touch(g, tile, old, act_raw, ish, cnt);
+          }
         }
       });
     }
@@ -117,7 +149,7 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
     const int32_t tile = hkey[e];
     if (tile < 0) continue;
     const int32_t old = atomicAdd(&tile_count[tile], hcnt[e]);
-    first_touch(g, tile, old, tile_slot, act_tiles, cnt);
+    first_touch(g, tile, old, act_raw, ish, cnt);
   }
 }
 
@@ -154,20 +186,41 @@ __device__ inline void block_scan3(int64_t v[3], int64_t excl[3], int64_t tot[3]
   }
 }
 
-__global__ __launch_bounds__(1024) void k_plan(Geom g, const int32_t* __restrict__ act_tiles,
+__global__ __launch_bounds__(1024) void k_plan(Geom g, const int32_t* __restrict__ act_raw,
+                                               const unsigned long long* __restrict__ ish,
+                                               int32_t* __restrict__ act_tiles, int32_t* __restrict__ tile_slot,
                                                const int32_t* __restrict__ tile_count,
                                                int32_t* __restrict__ act_off, int32_t* __restrict__ act_cur,
                                                int32_t* __restrict__ act_heavy,
                                                int32_t* __restrict__ heavy_list,
                                                int2* __restrict__ items, unsigned long long* cnt) {
   __shared__ int64_t ws[17][3];
+  __shared__ int32_t soff[kShards + 1];
   const int tid = threadIdx.x;
-  const int64_t n = min((int64_t)cnt[CNT_ACTIVE], (int64_t)g.act_cap);
+  if (tid == 0) {
+    int32_t run = 0;
+    for (int s = 0; s < kShards; ++s) {
+      soff[s] = run;
+      run += (int32_t)min((unsigned long long)g.act_cap, ish[s * kShardWords + SH_ACT]);
+    }
+    soff[kShards] = run;
+  }
+  __syncthreads();
+  const int64_t n = min((int64_t)soff[kShards], (int64_t)g.act_cap);
   const int64_t per = (n + 1023) / 1024;
   const int64_t lo = min((int64_t)tid * per, n), hi = min(lo + per, n);
+  // compact the per-shard first-touch lists: active tile j -> tile
+  auto tile_of = [&](int64_t j) {
+    int s = 0;
+    while (s + 1 < kShards && soff[s + 1] <= j) ++s;
+    return act_raw[(int64_t)s * g.act_cap + (j - soff[s])];
+  };
   int64_t v[3] = {0, 0, 0};
   for (int64_t j = lo; j < hi; ++j) {
-    const int64_t c = tile_count[act_tiles[j]];
+    const int32_t t = tile_of(j);
+    act_tiles[j] = t;
+    tile_slot[t] = (int32_t)j;
+    const int64_t c = tile_count[t];
     v[0] += c;
     v[1] += (c + kChunk - 1) / kChunk;
     v[2] += c > kChunk;
@@ -175,13 +228,14 @@ __global__ __launch_bounds__(1024) void k_plan(Geom g, const int32_t* __restrict
   int64_t ex[3], tot[3];
   block_scan3(v, ex, tot, ws);
   if (tid == 0) {
+    cnt[CNT_ACTIVE] = (unsigned long long)n;
     cnt[CNT_SEGS] = (unsigned long long)tot[0];
     cnt[CNT_ITEMS] = (unsigned long long)min(tot[1], g.item_cap);
     cnt[CNT_HEAVY] = (unsigned long long)min(tot[2], g.heavy_cap);
     if (tot[1] > g.item_cap || tot[2] > g.heavy_cap) atomicOr(&cnt[CNT_OVERFLOW], 8ull);
   }
   for (int64_t j = lo; j < hi; ++j) {
-    const int64_t c = tile_count[act_tiles[j]];
+    const int64_t c = tile_count[tile_of(j)];
     act_off[j] = (int32_t)ex[0];
     act_cur[j] = (int32_t)ex[0];
     const int64_t ni = (c + kChunk - 1) / kChunk;
@@ -229,14 +283,21 @@ __global__ __launch_bounds__(256) void k_scatter(RayArgs a, Geom g, const Beam* 
   const bool valid = (b < nb) && (bm.flags & 1);
   if (valid) {
     dm_for_each_piece(bm, g.r, [&](int32_t tile, int32_t k0, int32_t k1) {
-      const int h = hash_insert(hkey, tile);
-      if (h >= 0) {
-        atomicAdd(&hcnt[h], 1);
-      } else {
-        const int32_t slot = tile_slot[tile];
-        const int64_t idx = (slot >= 0 && slot < g.act_cap) ? (int64_t)atomicAdd(&act_cur[slot], 1) : -1;
-        put_seg(g, segs, idx, b, k0, k1, cnt);
+      const LaneRun run = lane_run(tile);
+      int h = -1;
+      int32_t base = -1;
+      if (run.head) {
+        h = hash_insert(hkey, tile);
+        if (h >= 0) {
+          atomicAdd(&hcnt[h], run.len);
+        } else {  // table full: place the run's pieces straight from the global cursor
+          const int32_t slot = tile_slot[tile];
+          base = (slot >= 0 && slot < g.act_cap) ? atomicAdd(&act_cur[slot], run.len) : -1;
+        }
       }
+      h = __shfl(h, run.head_lane);
+      base = __shfl(base, run.head_lane);
+      if (h < 0) put_seg(g, segs, base >= 0 ? (int64_t)base + run.rank : -1, b, k0, k1, cnt);
     });
   }
   __syncthreads();
@@ -250,11 +311,17 @@ __global__ __launch_bounds__(256) void k_scatter(RayArgs a, Geom g, const Beam* 
   __syncthreads();
   if (valid) {
     dm_for_each_piece(bm, g.r, [&](int32_t tile, int32_t k0, int32_t k1) {
-      const int h = hash_find(hkey, tile);
+      const LaneRun run = lane_run(tile);
+      int h = -1;
+      int32_t pos = -1;
+      if (run.head) {
+        h = hash_find(hkey, tile);
+        if (h >= 0 && hbase[h] >= 0) pos = hbase[h] + atomicAdd(&hcnt[h], run.len);
+      }
+      h = __shfl(h, run.head_lane);
+      pos = __shfl(pos, run.head_lane);
       if (h < 0) return;  // placed by the global path above
-      const int32_t base = hbase[h];
-      const int64_t idx = base >= 0 ? (int64_t)base + atomicAdd(&hcnt[h], 1) : -1;
-      put_seg(g, segs, idx, b, k0, k1, cnt);
+      put_seg(g, segs, pos >= 0 ? (int64_t)pos + run.rank : -1, b, k0, k1, cnt);
     });
   }
 }
@@ -287,10 +354,11 @@ __device__ inline float apply_one(const ApplyArgs& p, float L, uint32_t h, uint3
 template <class Counts>
 __device__ inline void apply_tile(const Geom& g, const ApplyArgs& p, int32_t tx0, int32_t ty0,
                                   float* __restrict__ L, int8_t* __restrict__ state, int vec_ok,
-                                  Counts&& counts, int32_t* sh_T, int32_t* sh_free) {
+                                  Counts&& counts, int32_t* sh_T, int32_t* sh_free, uint32_t* sh_U) {
   constexpr int kRows = DM_TS / 16;
   const int tid = threadIdx.x;
   int32_t dT = 0, dFree = 0;
+  uint32_t dU = 0;
   const int cx = (tid & 15) * 4;
   uint32_t h4[kRows][4], m4[kRows][4];
   bool any[kRows];
@@ -323,6 +391,7 @@ __device__ inline void apply_tile(const Geom& g, const ApplyArgs& p, int32_t tx0
       int8_t sv[4] = {(int8_t)s4[rr].x, (int8_t)s4[rr].y, (int8_t)s4[rr].z, (int8_t)s4[rr].w};
       for (int e = 0; e < 4; ++e) {
         if ((h4[rr][e] | m4[rr][e]) == 0u) continue;
+        dU += h4[rr][e] + m4[rr][e];
         const int8_t old = sv[e];
         lv[e] = apply_one(p, lv[e], h4[rr][e], m4[rr][e]);
         sv[e] = state_of(p, lv[e]);
@@ -338,6 +407,7 @@ __device__ inline void apply_tile(const Geom& g, const ApplyArgs& p, int32_t tx0
       for (int e = 0; e < 4; ++e) {
         if ((h4[rr][e] | m4[rr][e]) == 0u) continue;
         if (tx0 + cx + e >= g.r.W) continue;
+        dU += h4[rr][e] + m4[rr][e];
         const int64_t i = base[rr] + e;
         const int8_t old = state[i];
         const float nl = apply_one(p, L[i], h4[rr][e], m4[rr][e]);
@@ -351,26 +421,32 @@ __device__ inline void apply_tile(const Geom& g, const ApplyArgs& p, int32_t tx0
   }
   if (dT) atomicAdd(sh_T, dT);
   if (dFree) atomicAdd(sh_free, dFree);
+  if (dU) atomicAdd(sh_U, dU);
 }
 
-// One work item = up to kChunk pieces of one tile.  Pieces (and their beams)
-// are staged in LDS by all 256 lanes at once; each wave then walks pieces with
-// its lanes along the piece's major axis (up to 64 cells per wave-instruction,
-// distinct cells, LDS atomics).  A light tile (one item) applies its counts
-// right away; a heavy tile's item adds its non-zero counts to the tile's slab
-// with row-contiguous global atomics (256 B per wave-instruction).
+// One work item = up to kChunk (= 256) pieces of one tile.  Each piece is
+// turned into tile-local LDS addresses once (dm_tile_piece: one division per
+// piece) and then walked without divisions or bounds checks (every cell of a
+// piece lies in its tile).  Counts go to a packed LDS tile (hits << 16 |
+// misses): every cell adds 1, the hit cell of a beam then adds 0xFFFF, which
+// turns that miss into a hit (an item's 256 pieces visit a cell at most 256
+// times, so the miss half never carries on its own).  U is counted by the
+// apply step over in-grid cells.
+//  * light tile (one item): one piece per lane, incremental PieceCursor walk;
+//    the counts are applied to L / state right away;
+//  * heavy tile (around a sensor, > kChunk pieces): the pieces converge on
+//    the same cells, so each wave takes one piece at a time with one lane per
+//    cell (distinct cells: conflict-free LDS atomics) and the item's counts
+//    are added to the tile's slab with row-contiguous global atomics.
 __global__ __launch_bounds__(kApplyThreads) void k_tile_accum(
     Geom g, ApplyArgs p, const int2* __restrict__ items, const int32_t* __restrict__ act_tiles,
     const int32_t* __restrict__ act_off, const int32_t* __restrict__ act_heavy,
     const Seg* __restrict__ segs, const Beam* __restrict__ beams, int32_t* tile_count,
     int32_t* tile_free, uint32_t* __restrict__ slabs, float* __restrict__ L,
-    int8_t* __restrict__ state, unsigned long long* cnt, int vec_ok) {
-  // per-cell counts of this item, packed: hits << 16 | misses.  An item has
-  // at most kChunk = 256 pieces and a piece visits a cell at most once, so
-  // neither half can exceed 256: no carry between the halves.
+    int8_t* __restrict__ state, unsigned long long* cnt, unsigned long long* ish, int vec_ok) {
   __shared__ uint32_t cnt16[DM_TS * kLdsPitch];
-  __shared__ Seg s_seg[kChunk];
-  __shared__ Beam s_beam[kChunk];
+  __shared__ TilePiece s_tp[kChunk];
+  __shared__ float s_rcp[kChunk];
   __shared__ int32_t sh_free, sh_T;
   __shared__ uint32_t sh_U;
   const int tid = threadIdx.x, lane = lane_id();
@@ -384,51 +460,35 @@ __global__ __launch_bounds__(kApplyThreads) void k_tile_accum(
     const int32_t heavy = act_heavy[j];
     const int32_t c0 = act_off[j] + item.y * kChunk;
     const int32_t nseg = min(kChunk, act_off[j] + count - c0);
-    for (int e = tid; e < DM_TS * kLdsPitch; e += kApplyThreads) cnt16[e] = 0u;
-    if (tid == 0) { sh_free = 0; sh_T = 0; sh_U = 0u; }
-    if (tid < nseg) {
-      const Seg sg = segs[c0 + tid];
-      s_seg[tid] = sg;
-      if ((int64_t)sg.beam < g.nb) {
-        s_beam[tid] = beams[sg.beam];
-      } else {  // cannot happen; keeps a logic error in-bounds
-        Beam z;
-        z.flags = 0;
-        s_beam[tid] = z;
-      }
-    }
-    __syncthreads();
     const int32_t tx0 = (tile % g.r.TX) * DM_TS;
     const int32_t ty0 = (tile / g.r.TX) * DM_TS;  // band-local
-    uint32_t myU = 0;
-    for (int si = wid; si < nseg; si += kApplyThreads / 64) {
-      const Seg sg = s_seg[si];
-      const Beam bm = s_beam[si];
-      const int32_t k = (int32_t)sg.k0 + lane;
-      if (k <= (int32_t)sg.k1 && (bm.flags & 1)) {
-        int32_t x, yl;
-        dm_cell(bm, k, g.r.row0, &x, &yl);
-        const int32_t lx = x - tx0, ly = yl - ty0;
-        if (x >= 0 && x < g.r.W && yl >= 0 && yl < g.r.R && (uint32_t)lx < DM_TS && (uint32_t)ly < DM_TS) {
-          const bool is_hit = (k == bm.n) && (bm.flags & 2);
-          atomicAdd(&cnt16[ly * kLdsPitch + lx], is_hit ? 0x10000u : 1u);
-          ++myU;
-        }
+    for (int e = tid; e < DM_TS * kLdsPitch; e += kApplyThreads) cnt16[e] = 0u;
+    if (tid == 0) { sh_free = 0; sh_T = 0; sh_U = 0u; }
+    // this thread's piece
+    TilePiece tp;
+    tp.addr0 = 0; tp.addr_end = -1; tp.len = 0; tp.da = tp.db = 0;
+    tp.rem0 = 0; tp.two_adb = 0; tp.two_n = 1;
+    if (tid < nseg) {
+      const Seg sg = segs[c0 + tid];
+      if ((int64_t)sg.beam < g.nb) {
+        const Beam bm = beams[sg.beam];
+        if (bm.flags & 1) tp = dm_tile_piece(bm, sg.k0, sg.k1, g.r.row0, tx0, ty0, kLdsPitch);
       }
     }
-    if (myU) atomicAdd(&sh_U, myU);
-    __syncthreads();
-    if (heavy < 0) {
-      apply_tile(g, p, tx0, ty0, L, state, vec_ok,
-                 [&](int ly, int cx, uint32_t* h4, uint32_t* m4) {
-                   for (int e = 0; e < 4; ++e) {
-                     const uint32_t v = cnt16[ly * kLdsPitch + cx + e];
-                     h4[e] = v >> 16;
-                     m4[e] = v & 0xFFFFu;
-                   }
-                 },
-                 &sh_T, &sh_free);
-    } else {
+    if (heavy >= 0) {
+      if (tid < nseg) {
+        s_tp[tid] = tp;
+        s_rcp[tid] = __builtin_amdgcn_rcpf((float)tp.two_n);
+      }
+      __syncthreads();
+      for (int si = wid; si < nseg; si += kApplyThreads / 64) {
+        const TilePiece q = s_tp[si];
+        if (lane < q.len) {
+          const int32_t a = dm_piece_addr(q, lane, s_rcp[si]);
+          atomicAdd(&cnt16[a], (lane == q.len - 1 && q.addr_end >= 0) ? 0x10000u : 1u);
+        }
+      }
+      __syncthreads();
       uint32_t* sh = slabs + (int64_t)heavy * (2 * DM_TS * DM_TS);
       for (int e = tid; e < DM_TS * DM_TS; e += kApplyThreads) {
         const int ly = e >> 6, lx = e & 63;
@@ -437,15 +497,39 @@ __global__ __launch_bounds__(kApplyThreads) void k_tile_accum(
         if (h) atomicAdd(&sh[e], h);
         if (m) atomicAdd(&sh[DM_TS * DM_TS + e], m);
       }
+      __syncthreads();
+      continue;
     }
+    __syncthreads();  // cnt16 cleared
+    // light tile: wave-uniform trip count = the longest piece of the wave
+    int32_t wl = tp.len;
+    for (int o = 32; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o));
+    PieceCursor cur;
+    cur.init(tp);
+    for (int32_t st = 0; st < wl; ++st) {
+      if (st < tp.len) {
+        atomicAdd(&cnt16[cur.addr], 1u);
+        cur.step(tp);
+      }
+    }
+    if (tp.addr_end >= 0) atomicAdd(&cnt16[tp.addr_end], 0xFFFFu);
+    __syncthreads();
+    apply_tile(g, p, tx0, ty0, L, state, vec_ok,
+               [&](int ly, int cx, uint32_t* h4, uint32_t* m4) {
+                 for (int e = 0; e < 4; ++e) {
+                   const uint32_t v = cnt16[ly * kLdsPitch + cx + e];
+                   h4[e] = v >> 16;
+                   m4[e] = v & 0xFFFFu;
+                 }
+               },
+               &sh_T, &sh_free, &sh_U);
     __syncthreads();
     if (tid == 0) {
-      if (sh_T) atomicAdd(&cnt[CNT_T], (unsigned long long)sh_T);
-      if (sh_U) atomicAdd(&cnt[CNT_U], (unsigned long long)sh_U);
-      if (heavy < 0) {
-        tile_free[tile] += sh_free;
-        tile_count[tile] = 0;  // ready for the next call
-      }
+      unsigned long long* sh = ish + (blockIdx.x % kShards) * kShardWords;
+      if (sh_T) atomicAdd(&sh[SH_T], (unsigned long long)sh_T);
+      if (sh_U) atomicAdd(&sh[SH_U], (unsigned long long)sh_U);
+      tile_free[tile] += sh_free;
+      tile_count[tile] = 0;  // ready for the next call
     }
     __syncthreads();
   }
@@ -456,13 +540,14 @@ __global__ __launch_bounds__(kApplyThreads) void k_tile_accum(
 __global__ __launch_bounds__(kApplyThreads) void k_heavy_apply(
     Geom g, ApplyArgs p, const int32_t* __restrict__ heavy_list, const int32_t* __restrict__ act_tiles,
     int32_t* tile_count, int32_t* tile_free, uint32_t* __restrict__ slabs, float* __restrict__ L,
-    int8_t* __restrict__ state, unsigned long long* cnt, int vec_ok) {
+    int8_t* __restrict__ state, unsigned long long* cnt, unsigned long long* ish, int vec_ok) {
   __shared__ int32_t sh_free, sh_T;
+  __shared__ uint32_t sh_U;
   const int tid = threadIdx.x;
   const int64_t nh = (int64_t)cnt[CNT_HEAVY];
   for (int64_t h = blockIdx.x; h < nh; h += gridDim.x) {
     const int32_t tile = act_tiles[heavy_list[h]];
-    if (tid == 0) { sh_free = 0; sh_T = 0; }
+    if (tid == 0) { sh_free = 0; sh_T = 0; sh_U = 0u; }
     __syncthreads();
     uint32_t* sh = slabs + h * (2 * DM_TS * DM_TS);
     const int32_t tx0 = (tile % g.r.TX) * DM_TS;
@@ -474,16 +559,18 @@ __global__ __launch_bounds__(kApplyThreads) void k_heavy_apply(
                  h4[0] = a.x; h4[1] = a.y; h4[2] = a.z; h4[3] = a.w;
                  m4[0] = b.x; m4[1] = b.y; m4[2] = b.z; m4[3] = b.w;
                },
-               &sh_T, &sh_free);
+               &sh_T, &sh_free, &sh_U);
     // clear all 64 rows (apply_tile stops at the band's last row)
     for (int e = tid * 4; e < 2 * DM_TS * DM_TS; e += kApplyThreads * 4)
       *reinterpret_cast<uint4*>(sh + e) = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
     if (tid == 0) {
+      unsigned long long* shd = ish + (blockIdx.x % kShards) * kShardWords;
       if (sh_T) {
-        atomicAdd(&cnt[CNT_T], (unsigned long long)sh_T);
-        atomicAdd(&cnt[CNT_TH], (unsigned long long)sh_T);
+        atomicAdd(&shd[SH_T], (unsigned long long)sh_T);
+        atomicAdd(&shd[SH_TH], (unsigned long long)sh_T);
       }
+      if (sh_U) atomicAdd(&shd[SH_U], (unsigned long long)sh_U);
       tile_free[tile] += sh_free;
       tile_count[tile] = 0;
     }
@@ -580,6 +667,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                         const float* d_ranges, const double* d_trig) {
   const int64_t nb = (int64_t)S * N;
   DM_HIP(hipMemsetAsync(g->cnt, 0, sizeof(unsigned long long) * CNT_N, g->stream));
+  DM_HIP(hipMemsetAsync(g->ish, 0, sizeof(unsigned long long) * kShards * kShardWords, g->stream));
   if (nb == 0) return DM_OK;
   RayArgs a;
   a.S = S;
@@ -595,12 +683,13 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   KernelTimer t;
   dm_timer_begin(g, "beam_prep", &t);
   hipLaunchKernelGGL(k_beam_prep, dim3(nblk), dim3(256), 0, g->stream, a, ge, d_pose4, d_ranges,
-                     d_trig, g->beams, g->tile_count, g->tile_slot, g->act_tiles, g->cnt);
+                     d_trig, g->beams, g->tile_count, g->act_raw, g->ish, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "plan", &t);
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, g->stream, ge, g->act_tiles, g->tile_count,
-                     g->act_off, g->act_cur, g->act_heavy, g->heavy_list, g->items, g->cnt);
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, g->stream, ge, g->act_raw, g->ish, g->act_tiles,
+                     g->tile_slot, g->tile_count, g->act_off, g->act_cur, g->act_heavy,
+                     g->heavy_list, g->items, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "scatter", &t);
@@ -613,13 +702,13 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   hipLaunchKernelGGL(k_tile_accum, dim3(grid_for(g->item_cap, 1, 4096)), dim3(kApplyThreads), 0,
                      g->stream, ge, make_apply(g), g->items, g->act_tiles, g->act_off, g->act_heavy,
                      g->segs, g->beams, g->tile_count, g->tile_free, g->slabs, g->L, g->state,
-                     g->cnt, vec_ok);
+                     g->cnt, g->ish, vec_ok);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "heavy_apply", &t);
   hipLaunchKernelGGL(k_heavy_apply, dim3(grid_for(g->heavy_cap, 1, 2048)), dim3(kApplyThreads), 0,
                      g->stream, ge, make_apply(g), g->heavy_list, g->act_tiles, g->tile_count,
-                     g->tile_free, g->slabs, g->L, g->state, g->cnt, vec_ok);
+                     g->tile_free, g->slabs, g->L, g->state, g->cnt, g->ish, vec_ok);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   return DM_OK;

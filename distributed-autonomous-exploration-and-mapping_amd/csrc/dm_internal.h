@@ -42,8 +42,27 @@ enum {
   CNT_ITEMS = 8,    // apply work items
   CNT_HEAVY = 9,    // tiles split over several work items
   CNT_TH = 10,      // touched cells applied by k_heavy_apply
-  CNT_N = 11
+  CNT_SORTED = 11,  // 1: out_clu holds the clusters sorted by label
+  CNT_N = 12
 };
+
+// Sharded counters: same-address device atomics serialise at the memory side
+// (~12 ns each, MI355X_MICROARCH.md price list "fanin"), so per-workgroup
+// totals go to one of kShards counters, each on its own 128-B line
+// (shard = blockIdx.x % kShards); readers sum the shards.
+constexpr int kShards = 32;
+constexpr int kShardWords = 16;  // 128 B per shard
+enum { SH_U = 0, SH_T = 1, SH_TH = 2, SH_ACT = 3 };  // integrate shard fields
+enum { SH_SLOT = 0 };                                 // frontier shard fields
+
+struct dm_grid;
+// async D2H of both shard-counter blocks into g->h_sh (pinned)
+hipError_t dm_copy_shards(dm_grid* g);
+inline unsigned long long dm_shard_sum(const unsigned long long* sh, int field) {
+  unsigned long long s = 0;
+  for (int i = 0; i < kShards; ++i) s += sh[i * kShardWords + field];
+  return s;
+}
 
 struct KernelTimer {
   std::string name;
@@ -66,11 +85,15 @@ struct dm_grid {
   int32_t* tile_free = nullptr;
   unsigned long long* cnt = nullptr;  // CNT_N device counters
   unsigned long long* h_cnt = nullptr;  // pinned mirror
+  unsigned long long* ish = nullptr;    // [kShards][kShardWords] integrate shards
+  unsigned long long* fsh = nullptr;    // [kShards][kShardWords] frontier shards
+  unsigned long long* h_sh = nullptr;   // pinned mirror of ish then fsh
 
   // integrate workspace
   Beam* beams = nullptr; int64_t beams_cap = 0;
   Seg* segs = nullptr; int64_t segs_cap = 0;
   int32_t* act_tiles = nullptr; int32_t* act_off = nullptr; int32_t* act_cur = nullptr;
+  int32_t* act_raw = nullptr;    // [kShards][act_cap] first-touch lists per shard
   int64_t act_cap = 0;
   int32_t* act_heavy = nullptr;  // active tile -> heavy ordinal or -1
   int32_t* heavy_list = nullptr; // heavy ordinal -> active tile
@@ -96,7 +119,11 @@ struct dm_grid {
   int32_t* slot_root = nullptr;
   long long* slot_own = nullptr;  // [slot][3] size, sum_x, sum_y
   long long* slot_acc = nullptr;  // [slot][3]
-  long long* clusters = nullptr;  // [cap][4] label,size,sum_x,sum_y
+  long long* clusters = nullptr;  // [cap][4] label,size,sum_x,sum_y (unsorted)
+  dm_cluster* out_clu = nullptr;  // [slot_cap] sorted cluster records (k_sort_clusters)
+  dm_cluster* h_out = nullptr;    // pinned staging for sorted cluster records
+  int64_t h_out_cap = 0;
+  int64_t clu_hint = 1024;        // records copied speculatively with the counters
   int32_t* cell_slot = nullptr;   // dense [R][W] (only when labels requested)
   int32_t* edge_slot = nullptr;   // [2][W] slots of the band's first / last row
   long long* edge_label = nullptr;// [2][W]
@@ -119,7 +146,8 @@ int dm_launch_recount(dm_grid* g);
 int dm_launch_state_from_logodds(dm_grid* g);
 int dm_launch_map_image(dm_grid* g, uint8_t* d_img);
 int dm_launch_set_state(dm_grid* g, const int8_t* d_state_in);
-int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters);
+int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters,
+                        int64_t* copied);
 int dm_launch_ld06(dm_grid* g, int32_t S, const dm_ld06_point* d_pts, const int64_t* d_offsets,
                    int32_t N, int dir, float* d_ranges, float* d_intensities);
 

@@ -125,6 +125,12 @@ DM_HD inline void dm_for_each_piece(const Beam& b, const RayGeom& g, Emit&& emit
   const int32_t lim_a = b.xmajor ? g.TX : g.TY;
   const int32_t lim_b = b.xmajor ? g.TY : g.TX;
   const int32_t max_iter = 2 * (n / DM_TS) + 8;
+  // k at which the minor coordinate reaches step count Q:
+  //   ceil(n*(2Q-1) / (2*adb)); operands < 2^31 (n, adb <= 16386, Q <= adb+1),
+  //   so a double reciprocal (once per beam) + one exact correction replaces a
+  //   64-bit integer division per piece
+  const int32_t den_b = 2 * b.adb;
+  const double rden_b = b.adb > 0 ? 1.0 / (double)den_b : 0.0;
   int32_t k = 0;
   for (int32_t it = 0; k <= n && it < max_iter; ++it) {
     const int32_t q = dm_minor_steps(b, k);
@@ -140,10 +146,9 @@ DM_HD inline void dm_for_each_piece(const Beam& b, const RayGeom& g, Emit&& emit
     if (b.ib == 0) {
       kb = (int64_t)n + 1;
     } else {
-      const int64_t Q = (int64_t)q + (b.ib > 0 ? (DM_TS * (tb + 1) - mb) : (mb - DM_TS * tb) + 1);
-      const int64_t num = (int64_t)n * (2 * Q - 1);
-      const int64_t den = 2 * (int64_t)b.adb;
-      kb = (num + den - 1) / den;
+      const int32_t Q = q + (b.ib > 0 ? (DM_TS * (tb + 1) - mb) : (mb - DM_TS * tb) + 1);
+      const int32_t num = n * (2 * Q - 1);
+      kb = dm_udiv(num + den_b - 1, den_b, rden_b);
     }
     int64_t ke = ka < kb ? ka : kb;
     if (ke > (int64_t)n + 1) ke = (int64_t)n + 1;
@@ -166,3 +171,113 @@ DM_HD inline void dm_cell(const Beam& b, int32_t k, int32_t row0, int32_t* x, in
   *x = b.xmajor ? ma : mb;
   *yl = (b.xmajor ? mb : ma) - row0;
 }
+
+// Incremental walk along a piece (used by k_tile_accum and the host
+// emulation): the cell of step k0, then one step per k with the exact integer
+// carry of the minor coordinate, q(k) = floor((2k*adb + n) / (2n)):
+// rem = (2k*adb + n) mod 2n, rem += 2*adb per step, carry when rem >= 2n
+// (adb <= n, so at most one carry per step).  Equals dm_cell(b, k) for every k.
+struct PieceWalk {
+  int32_t x, yl;           // current cell (global x, band-local y)
+  int32_t rem, two_n, two_adb;
+  int32_t dxa, dya, dxb, dyb;  // per step / per carry
+
+  DM_HD void init(const Beam& b, int32_t k0, int32_t row0) {
+    two_n = 1;
+    two_adb = 0;
+    int32_t q = 0;
+    rem = 0;
+    if (b.n > 0) {
+      two_n = 2 * b.n;
+      two_adb = 2 * b.adb;
+      const int32_t num = k0 * two_adb + b.n;
+      q = dm_udiv(num, two_n, b.rden);
+      rem = num - q * two_n;
+    }
+    const int32_t ma = b.sa + k0 * b.ia, mb = b.sb + b.ib * q;
+    x = b.xmajor ? ma : mb;
+    yl = (b.xmajor ? mb : ma) - row0;
+    dxa = b.xmajor ? b.ia : 0;
+    dya = b.xmajor ? 0 : b.ia;
+    dxb = b.xmajor ? 0 : b.ib;
+    dyb = b.xmajor ? b.ib : 0;
+  }
+
+  DM_HD void step() {
+    x += dxa;
+    yl += dya;
+    rem += two_adb;
+    if (rem >= two_n) {
+      rem -= two_n;
+      x += dxb;
+      yl += dyb;
+    }
+  }
+};
+
+// floor(num / den) for 0 <= num < 2^22, 0 < den, from an approximate fp32
+// reciprocal of den (relative error < 2^-20): the estimate is within 1 of the
+// quotient, one integer correction each way makes it exact.
+DM_HD inline int32_t dm_udiv_small(int32_t num, int32_t den, float rden) {
+  int32_t q = (int32_t)((float)num * rden);
+  if ((q + 1) * den <= num) ++q;
+  else if (q * den > num) --q;
+  return q;
+}
+
+// A piece (beam steps k0..k1 inside one tile) in tile-local LDS word
+// addresses, row pitch `pitch`: cell k0 + j sits at
+//   addr0 + j*da + db * floor((rem0 + j*two_adb) / two_n)
+// (the minor carry of PieceWalk in closed form), so a kernel can walk it one
+// cell per step (dm_piece_walk below) or put one lane per cell.  addr_end is
+// the address of the beam's hit cell when this piece ends the beam with a hit
+// (SPEC a6: the endpoint counts as a hit), else -1.  Every cell of a piece is
+// inside the tile by construction (dm_for_each_piece), so the addresses are
+// in [0, 64*pitch); cells beyond the grid's last column / the band's last row
+// (edge tiles) land on LDS words the apply step ignores.
+struct TilePiece {
+  int32_t addr0, addr_end, len;
+  int32_t da, db;
+  int32_t rem0, two_adb, two_n;
+};
+
+// tx0 / ty0: the tile's first column / band-local first row.
+DM_HD inline TilePiece dm_tile_piece(const Beam& b, int32_t k0, int32_t k1, int32_t row0, int32_t tx0,
+                                     int32_t ty0, int32_t pitch) {
+  TilePiece tp;
+  PieceWalk w;
+  w.init(b, k0, row0);
+  tp.addr0 = (w.yl - ty0) * pitch + (w.x - tx0);
+  tp.len = k1 - k0 + 1;
+  tp.da = b.xmajor ? (int32_t)b.ia : (int32_t)b.ia * pitch;
+  tp.db = b.xmajor ? (int32_t)b.ib * pitch : (int32_t)b.ib;
+  tp.rem0 = w.rem;
+  tp.two_adb = w.two_adb;
+  tp.two_n = w.two_n;
+  tp.addr_end = -1;
+  if ((b.flags & 2) && k1 == b.n) {
+    // q(n) = adb: the endpoint cell
+    const int32_t ma = b.sa + b.n * b.ia, mb = b.sb + b.ib * b.adb;
+    const int32_t x = b.xmajor ? ma : mb, yl = (b.xmajor ? mb : ma) - row0;
+    tp.addr_end = (yl - ty0) * pitch + (x - tx0);
+  }
+  return tp;
+}
+
+// LDS address of cell k0 + j of a piece (one lane per cell; j < 64 keeps
+// num < 2^22).
+DM_HD inline int32_t dm_piece_addr(const TilePiece& tp, int32_t j, float rtwo_n) {
+  const int32_t dq = dm_udiv_small(tp.rem0 + j * tp.two_adb, tp.two_n, rtwo_n);
+  return tp.addr0 + j * tp.da + dq * tp.db;
+}
+
+// Incremental form: the address of the current cell, then one step per k.
+struct PieceCursor {
+  int32_t addr, rem;
+  DM_HD void init(const TilePiece& tp) { addr = tp.addr0; rem = tp.rem0; }
+  DM_HD void step(const TilePiece& tp) {
+    addr += tp.da;
+    rem += tp.two_adb;
+    if (rem >= tp.two_n) { rem -= tp.two_n; addr += tp.db; }
+  }
+};

@@ -147,14 +147,15 @@ class OccupancyMapper:
         return int(U.value), int(T.value)
 
     STAT_NAMES = ("updates", "touched", "touched_heavy", "pieces", "active_tiles", "work_items",
-                  "heavy_tiles")
+                  "heavy_tiles", "frontier_tiles", "frontier_slots", "frontier_clusters")
 
     def last_stats(self) -> dict:
         """Diagnostics of the most recent integrate call (dm_last_stats)."""
-        out = (ctypes.c_uint64 * 7)()
+        k = len(self.STAT_NAMES)
+        out = (ctypes.c_uint64 * k)()
         n = ctypes.c_int32(0)
         with self._lock:
-            check(self._lib.dm_last_stats(self._handle(), out, 7, ctypes.byref(n)))
+            check(self._lib.dm_last_stats(self._handle(), out, k, ctypes.byref(n)))
         return {k: int(out[i]) for i, k in enumerate(self.STAT_NAMES)}
 
     def ld06_to_scans(self, points, offsets, n_beams: int, laser_scan_dir: bool = True,

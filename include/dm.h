@@ -128,9 +128,10 @@ int dm_integrate_device(dm_grid* g, int32_t S, const double* d_pose4,
 /* U and T of the most recent integrate call (synchronises the stream). */
 int dm_last_counts(dm_grid* g, uint64_t* updates, uint64_t* touched);
 
-/* Diagnostics of the most recent integrate call (synchronises the stream):
- * out[0..6] = U, T, T applied by the heavy-tile pass, pieces (ray pieces
- * binned by tile), active tiles, apply work items, heavy tiles. */
+/* Diagnostics of the most recent calls (synchronises the stream):
+ * out[0..6] = integrate: U, T, T applied by the heavy-tile pass, pieces (ray
+ * pieces binned by tile), active tiles, apply work items, heavy tiles;
+ * out[7..9] = frontiers: tiles visited, tile-local components, clusters. */
 int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out);
 
 /* OccupancyGrid.data for the band: int8[band_rows*width] (-1 / 0 / 100). */

@@ -45,31 +45,42 @@ extern "C" int emu_integrate(int32_t W, int32_t R, int32_t row0, double ox, doub
     });
   }
   uint64_t U = 0, T = 0;
+  constexpr int32_t kPitch = DM_TS + 1;  // k_tile_accum's LDS row pitch
   std::vector<uint32_t> hit(DM_TS * DM_TS), miss(DM_TS * DM_TS);
-  for (size_t j = 0; j < act.size(); ++j) {  // k_tile_apply
+  for (size_t j = 0; j < act.size(); ++j) {  // k_tile_accum
     const int32_t t = act[j];
     const int32_t tx0 = (t % g.TX) * DM_TS, ty0 = (t / g.TX) * DM_TS;
     std::fill(hit.begin(), hit.end(), 0u);
     std::fill(miss.begin(), miss.end(), 0u);
     for (int64_t s = off[j]; s < off[j + 1]; ++s) {
       const Beam& bm = beams[segs[s].beam];
-      for (int lane = 0; lane < 64; ++lane) {
-        const int32_t k = segs[s].k0 + lane;
-        if (k > segs[s].k1) break;
+      const TilePiece tp = dm_tile_piece(bm, segs[s].k0, segs[s].k1, row0, tx0, ty0, kPitch);
+      const float rtwo_n = 1.0f / (float)tp.two_n;
+      PieceCursor cur;
+      cur.init(tp);
+      if (tp.len < 1 || tp.len > DM_TS) return -101;
+      for (int st = 0; st < tp.len; ++st, cur.step(tp)) {
+        const int32_t k = segs[s].k0 + st;
         int32_t x, yl;
         dm_cell(bm, k, row0, &x, &yl);
         const int32_t lx = x - tx0, ly = yl - ty0;
-        if (x >= 0 && x < W && yl >= 0 && yl < R && (uint32_t)lx < DM_TS && (uint32_t)ly < DM_TS) {
-          const bool is_hit = (k == bm.n) && (bm.flags & 2);
-          (is_hit ? hit : miss)[ly * DM_TS + lx] += 1;
-          ++U;
-        }
+        // both address forms must name the closed-form cell, inside the tile
+        if ((uint32_t)lx >= DM_TS || (uint32_t)ly >= DM_TS) return -102;
+        if (cur.addr != ly * kPitch + lx) return -100;
+        if (dm_piece_addr(tp, st, rtwo_n) != cur.addr) return -103;
+        const bool is_hit = (k == bm.n) && (bm.flags & 2);
+        if (is_hit != (tp.addr_end == cur.addr && st == tp.len - 1)) return -104;
+        // the kernel adds 1 per cell, then 0xFFFF at addr_end (a miss becomes a hit)
+        (is_hit ? hit : miss)[ly * DM_TS + lx] += 1;
       }
     }
+    for (int ly = 0; ly < DM_TS; ++ly)  // U: in-grid cells only, as apply_tile counts it
+      for (int lx = 0; lx < DM_TS; ++lx)
+        if (tx0 + lx < W && ty0 + ly < R) U += hit[ly * DM_TS + lx] + miss[ly * DM_TS + lx];
     for (int ly = 0; ly < DM_TS; ++ly)
       for (int lx = 0; lx < DM_TS; ++lx) {
         const uint32_t h = hit[ly * DM_TS + lx], m = miss[ly * DM_TS + lx];
-        if (!(h | m)) continue;
+        if (!(h | m) || tx0 + lx >= W || ty0 + ly >= R) continue;
         const int64_t i = (int64_t)(ty0 + ly) * W + tx0 + lx;
         float l = L[i];
         const float tt = (float)h * l_occ;

@@ -44,11 +44,12 @@ class EmuMap:
                          for i in range(N)], np.float64).reshape(N, 2)
         U, T, G = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
-        self.lib.emu_integrate(int(p.width), self.L.shape[0], int(p.band_row0), p.origin_x, p.origin_y,
+        rc = self.lib.emu_integrate(int(p.width), self.L.shape[0], int(p.band_row0), p.origin_x, p.origin_y,
                                p.resolution, p.range_min, p.range_max, p.l_occ, p.l_free, p.l_min,
                                p.l_max, p.occ_thresh, p.free_thresh, ptr(self.L), ptr(self.state), S,
                                ptr(pose4), N, ptr(ranges), ptr(trig), ctypes.byref(U),
                                ctypes.byref(T), ctypes.byref(G))
+        assert rc == 0, "incremental piece walk disagrees with the closed form"
         return int(U.value), int(T.value)
 
 

@@ -102,10 +102,13 @@ def test_c3_full_size_batch(oracle_lib):
         np.testing.assert_array_equal(fr.clusters, clusters)
 
 
-@pytest.mark.parametrize("kind,R,W,seed", [("random", 64, 64, 1), ("random", 200, 333, 2),
-                                           ("blob", 700, 650, 3), ("blob", 1, 300, 4),
-                                           ("blob", 300, 1, 5), ("checker", 128, 192, 6),
-                                           ("stripes", 256, 256, 7)])
+FRONTIER_STATE_CASES = [("random", 64, 64, 1), ("random", 200, 333, 2), ("blob", 700, 650, 3),
+                        ("blob", 1, 300, 4), ("blob", 300, 1, 5), ("checker", 128, 192, 6),
+                        ("stripes", 256, 256, 7), ("random", 1024, 1024, 8),
+                        ("sparse", 400, 330, 9), ("sparse", 2048, 2048, 10)]
+
+
+@pytest.mark.parametrize("kind,R,W,seed", FRONTIER_STATE_CASES)
 def test_frontiers_on_states(oracle_lib, kind, R, W, seed):
     if kind == "random":
         st = cases.random_state(seed, R, W)
@@ -114,6 +117,10 @@ def test_frontiers_on_states(oracle_lib, kind, R, W, seed):
     elif kind == "checker":
         yy, xx = np.mgrid[0:R, 0:W]
         st = np.where((yy + xx) % 2 == 0, 0, -1).astype(np.int8)
+    elif kind == "sparse":  # isolated free cells in unknown space: one cluster each
+        rng = np.random.Generator(np.random.PCG64(seed))
+        st = np.full((R, W), -1, np.int8)
+        st[::3, ::3] = np.where(rng.random(st[::3, ::3].shape) < 0.9, 0, -1)
     else:  # long diagonal frontier stripes crossing many tiles
         yy, xx = np.mgrid[0:R, 0:W]
         st = np.where(((xx + yy) // 3) % 4 == 0, -1, 0).astype(np.int8)
@@ -125,6 +132,7 @@ def test_frontiers_on_states(oracle_lib, kind, R, W, seed):
         np.testing.assert_array_equal(m.state(), st)
         fr = m.frontiers(want_mask=True, want_labels=True)
         assert_frontiers_equal(fr, *om.frontiers())
+        assert m.last_stats()["frontier_clusters"] == len(fr.clusters)
 
 
 def test_frontier_band_with_halo(oracle_lib):
