@@ -8,8 +8,10 @@ resident in HBM, dm_integrate_device) + full frontier extraction
 (mask + CCL + clusters, clusters copied to the host, dm_frontiers).
 
 N GPUs (weak scaling): rank r owns a 16384-row band of a 16384 x 16384*N map
-with its own 64 robots; frontiers are merged across bands with RCCL
-(halo rows, edge labels, cluster all-gather; dm/sharded.py).
+with its own 64 robots anywhere in the band (plus the neighbours' scans that
+reach across the band edge); frontiers are merged across bands on the device
+(RCCL all-gather of halo rows and export records, dm_merge_bands;
+dm/sharded.py).
 
 Prints ONE JSON line on rank 0.  See DESIGN.md §5 for every field.
 """
@@ -78,20 +80,41 @@ def main():
     H_total = G * world_size
     half_w = G * res / 2.0
     oy_global = -H_total * res / 2.0
-    # this rank's band of the world, in metres
-    y0 = oy_global + rank * G * res
-    y1 = y0 + G * res
-    world = synth.make_world(args.seed * 1000 + rank, -half_w, y0, half_w, y1)
-    margin = float(12.5) if world_size > 1 else 1.0  # scans stay inside the band
-    stream = synth.ScanStream(world, args.robots, args.beams, args.seed * 1000 + 500 + rank,
-                              region=(-half_w + 1.0, y0 + margin, half_w - 1.0, y1 - margin))
+    # one world over the whole map (every rank builds the same one)
+    world = synth.make_world(args.seed * 1000, -half_w, oy_global, half_w, -oy_global)
+
+    def band_stream(q):
+        """Rank q's robots: random-walking anywhere in q's band."""
+        y0 = oy_global + q * G * res
+        return synth.ScanStream(world, args.robots, args.beams, args.seed * 1000 + 500 + q,
+                                region=(-half_w + 1.0, y0 + 1.0, half_w - 1.0, y0 + G * res - 1.0))
+
+    # Scans near a band edge also reach the neighbouring band: each rank
+    # integrates its own robots' scans plus the neighbours' scans whose
+    # max-range disk reaches its band (host-side replication of the scan
+    # stream, SURVEY.md §8(e)); libdm clips every ray to the band, so each
+    # cell update is counted by exactly one rank.
+    reach = 12.0 + 2 * res
+    ylo = oy_global + rank * G * res - reach
+    yhi = oy_global + (rank + 1) * G * res + reach
+    streams = {q: band_stream(q) for q in (rank - 1, rank, rank + 1) if 0 <= q < world_size}
     t_gen = time.perf_counter()
-    pool = [stream.next_batch() for _ in range(args.pool)]
+    pool = []
+    for _ in range(args.pool):
+        poses, ranges = [], []
+        for q, st in streams.items():
+            p_, r_ = st.next_batch()
+            keep = np.ones(len(p_), bool) if q == rank else (p_[:, 1] >= ylo) & (p_[:, 1] <= yhi)
+            poses.append(p_[keep])
+            ranges.append(r_[keep])
+        pool.append((np.concatenate(poses), np.concatenate(ranges)))
     t_gen = time.perf_counter() - t_gen
     amin = float(synth.LD06_ANGLE_MIN)
     inc = float(synth.ld06_angle_increment(args.beams))
     dev = torch.device("cuda", local_rank)
-    dpool = [(torch.from_numpy(synth.pose4(p)).to(dev), torch.from_numpy(r).to(dev)) for p, r in pool]
+    dpool = [(torch.from_numpy(synth.pose4(p)).to(dev), torch.from_numpy(np.ascontiguousarray(r)).to(dev))
+             for p, r in pool]
+    torch.cuda.synchronize()
 
     params = dm.default_params(G, H_total, resolution=res)
     params.origin_x = -half_w
@@ -103,7 +126,7 @@ def main():
 
     def integrate(k):
         pose4, rng = dpool[k % len(dpool)]
-        band.integrate_device(pose4.data_ptr(), S, rng.data_ptr(), N, amin, inc)
+        band.integrate_device(pose4.data_ptr(), pose4.shape[0], rng.data_ptr(), N, amin, inc)
 
     # per-batch U and T are properties of the batch (not of the map state):
     # measure them once, untimed
@@ -238,6 +261,10 @@ def main():
                 "bytes_model": "8*U + 25*(T - T_heavy) per call (SURVEY.md §8(d) per-unit figures)",
             },
             "stage_stats": {k: float(np.mean([st[k] for st in stats])) for k in stats[0]},
+            "scans_per_rank_batch": float(np.mean([p.shape[0] for p, _ in pool])),
+            "exchange": ("device: RCCL all-gather of halo rows + export records, dm_merge_bands"
+                         if world_size > 1 else None),
+            "exchange_fallbacks": getattr(mapper, "fallbacks", 0),
             "cpu_baseline": cpu,
             "gen_seconds": t_gen,
         }

@@ -160,6 +160,8 @@ int grow_slots(dm_grid* g, int64_t need) {
   if (!rc) rc = dev_alloc(&g->slot_acc, 3 * cap, "slot totals");
   if (!rc) rc = dev_alloc(&g->clusters, 4 * cap, "clusters");
   if (!rc) rc = dev_alloc(&g->out_clu, cap, "sorted clusters");
+  if (!rc) rc = dev_alloc(&g->slot_k, cap, "slot cluster index");
+  if (!rc) rc = dev_alloc(&g->rank_of, cap, "cluster sorted position");
   if (rc) return rc;
   g->slot_cap = cap;
   return DM_OK;
@@ -174,6 +176,49 @@ int grow_host_out(dm_grid* g, int64_t need) {
   g->h_out_cap = 0;
   DM_HIP(hipHostMalloc((void**)&g->h_out, sizeof(dm_cluster) * (size_t)cap, hipHostMallocDefault));
   g->h_out_cap = cap;
+  return DM_OK;
+}
+
+// Copy nw sorted cluster records to `out`: the first `have` are already in
+// g->h_out (arrived with the counters); the rest come from d_sorted.  When
+// the device could not sort (too many records), sort the n raw records of
+// d_raw ([n][4] int64) here and compute the centroids with the same formula.
+int copy_clusters(dm_grid* g, bool sorted, int64_t n, int64_t nw, int64_t have,
+                  const dm_cluster* d_sorted, const long long* d_raw, dm_cluster* out) {
+  if (sorted) {
+    have = std::min<int64_t>(have, nw);
+    if (have > 0) memcpy(out, g->h_out, sizeof(dm_cluster) * (size_t)have);
+    if (nw > have)
+      DM_HIP(hipMemcpy(out + have, d_sorted + have, sizeof(dm_cluster) * (size_t)(nw - have),
+                       hipMemcpyDeviceToHost));
+    return DM_OK;
+  }
+  std::vector<HostCluster> hc((size_t)n);
+  if (n > 0) DM_HIP(hipMemcpy(hc.data(), d_raw, sizeof(HostCluster) * (size_t)n, hipMemcpyDeviceToHost));
+  std::sort(hc.begin(), hc.end(), [](const HostCluster& a, const HostCluster& b) { return a.label < b.label; });
+  for (int64_t i = 0; i < nw; ++i) {
+    dm_cluster& c = out[i];
+    c.label = hc[i].label;
+    c.size = hc[i].size;
+    c.sum_x = hc[i].sum_x;
+    c.sum_y = hc[i].sum_y;
+    const double mx = (double)c.sum_x / (double)c.size;
+    const double my = (double)c.sum_y / (double)c.size;
+    c.cx_m = g->p.origin_x + (mx + 0.5) * g->p.resolution;
+    c.cy_m = g->p.origin_y + (my + 0.5) * g->p.resolution;
+  }
+  return DM_OK;
+}
+
+int grow_merge(dm_grid* g, int64_t n) {
+  if (n <= g->m_cap) return DM_OK;
+  int rc = dev_alloc(&g->m_parent, n, "merge parents");
+  if (!rc) rc = dev_alloc(&g->m_label, n, "merge labels");
+  if (!rc) rc = dev_alloc(&g->m_acc, 3 * n, "merge sums");
+  if (!rc) rc = dev_alloc(&g->m_clu, 4 * n, "merged clusters");
+  if (!rc) rc = dev_alloc(&g->m_out, n, "merged clusters (sorted)");
+  if (rc) { g->m_cap = 0; return rc; }
+  g->m_cap = n;
   return DM_OK;
 }
 
@@ -325,6 +370,9 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   e = hipHostMalloc((void**)&g->h_sh, sizeof(unsigned long long) * 2 * kShards * kShardWords,
                     hipHostMallocDefault);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipHostMalloc(shard counters)"));
+  if ((rc = dev_alloc(&g->m_cnt, 4, "merge counters"))) return fail(rc);
+  e = hipHostMalloc((void**)&g->h_mcnt, sizeof(unsigned long long) * 4, hipHostMallocDefault);
+  if (e != hipSuccess) return fail(dm_hip_check(e, "hipHostMalloc(merge counters)"));
   e = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate"));
   g->own_stream = true;
@@ -347,6 +395,9 @@ int dm_destroy(dm_grid* g) {
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
   dev_free(g->edge_slot); dev_free(g->edge_label); dev_free(g->mask); dev_free(g->labels);
   dev_free(g->halo); dev_free(g->out_clu); dev_free(g->ish); dev_free(g->act_raw);
+  dev_free(g->slot_k); dev_free(g->rank_of); dev_free(g->m_parent); dev_free(g->m_label);
+  dev_free(g->m_acc); dev_free(g->m_clu); dev_free(g->m_out); dev_free(g->m_cnt);
+  if (g->h_mcnt) (void)hipHostFree(g->h_mcnt);
   if (g->h_cnt) (void)hipHostFree(g->h_cnt);
   if (g->h_sh) (void)hipHostFree(g->h_sh);
   if (g->h_out) (void)hipHostFree(g->h_out);
@@ -533,38 +584,72 @@ int dm_frontiers(dm_grid* g, uint8_t* mask, int64_t* labels, dm_cluster* out, in
   if (rc) return rc == DM_ERR_CAPACITY ? dm_set_error(rc, "frontier slot arrays kept overflowing") : rc;
   g->frontier_valid = true;
   const int64_t nw = std::min<int64_t>(n, cap);
-  if (g->h_cnt[CNT_SORTED]) {
-    // sorted records with centroids, computed on the device; the first
-    // clu_hint of them arrived together with the counters
-    const int64_t have = std::min<int64_t>(copied, nw);
-    if (have > 0) memcpy(out, g->h_out, sizeof(dm_cluster) * (size_t)have);
-    if (nw > have)
-      DM_HIP(hipMemcpy(out + have, g->out_clu + have, sizeof(dm_cluster) * (size_t)(nw - have),
-                       hipMemcpyDeviceToHost));
-  } else {  // too many clusters / labels >= 2^32: sort the raw records here
-    std::vector<HostCluster> hc((size_t)n);
-    if (n > 0)
-      DM_HIP(hipMemcpy(hc.data(), g->clusters, sizeof(HostCluster) * (size_t)n, hipMemcpyDeviceToHost));
-    std::sort(hc.begin(), hc.end(),
-              [](const HostCluster& a, const HostCluster& b) { return a.label < b.label; });
-    for (int64_t i = 0; i < nw; ++i) {
-      dm_cluster& c = out[i];
-      c.label = hc[i].label;
-      c.size = hc[i].size;
-      c.sum_x = hc[i].sum_x;
-      c.sum_y = hc[i].sum_y;
-      const double mx = (double)c.sum_x / (double)c.size;
-      const double my = (double)c.sum_y / (double)c.size;
-      c.cx_m = g->p.origin_x + (mx + 0.5) * g->p.resolution;
-      c.cy_m = g->p.origin_y + (my + 0.5) * g->p.resolution;
-    }
-  }
+  if ((rc = copy_clusters(g, g->h_cnt[CNT_SORTED] != 0, n, nw, copied, g->out_clu, g->clusters, out)))
+    return rc;
   g->clu_hint = std::max<int64_t>(1024, n + n / 4 + 64);
   if (g->clu_hint > g->h_out_cap && (rc = grow_host_out(g, g->clu_hint))) return rc;
   if (mask) DM_HIP(hipMemcpy(mask, g->mask, (size_t)cells, hipMemcpyDeviceToHost));
   if (labels) DM_HIP(hipMemcpy(labels, g->labels, sizeof(int64_t) * (size_t)cells, hipMemcpyDeviceToHost));
   if (n_out) *n_out = n;
   if (n > cap) return dm_set_error(DM_ERR_CAPACITY, "%lld clusters, capacity %lld", (long long)n,
+                                   (long long)cap);
+  return DM_OK;
+}
+
+int dm_export_bytes(const dm_grid* g, int64_t rec_cap, int64_t* bytes) {
+  int rc = check_grid(g);
+  if (rc) return rc;
+  if (!bytes || rec_cap < 0) return dm_set_error(DM_ERR_INVALID_ARG, "bytes is NULL or rec_cap < 0");
+  *bytes = dm_export_nbytes(g->W, rec_cap);
+  return DM_OK;
+}
+
+int dm_frontiers_export_device(dm_grid* g, void* d_export, int64_t rec_cap) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (!d_export || rec_cap < 0) return dm_set_error(DM_ERR_INVALID_ARG, "d_export is NULL or rec_cap < 0");
+  if (g->p.min_frontier_size > 1)
+    return dm_set_error(DM_ERR_INVALID_ARG,
+                        "export needs a band handle with min_frontier_size <= 1 (the size filter "
+                        "applies to merged clusters)");
+  if ((rc = dm_enqueue_frontiers(g, false, false))) return rc;
+  if ((rc = dm_launch_export(g, d_export, rec_cap))) return rc;
+  g->frontier_valid = true;
+  return DM_OK;
+}
+
+int dm_merge_bands(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap, int64_t min_size,
+                   dm_cluster* out, int64_t cap, int64_t* n_out) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (!d_gathered || nranks < 1 || rec_cap < 1)
+    return dm_set_error(DM_ERR_INVALID_ARG, "need d_gathered, nranks >= 1, rec_cap >= 1");
+  if (cap < 0 || (cap > 0 && !out)) return dm_set_error(DM_ERR_INVALID_ARG, "bad cluster buffer");
+  const int64_t n = (int64_t)nranks * rec_cap;
+  if (n >= (1ll << 31)) return dm_set_error(DM_ERR_SHAPE, "nranks * rec_cap must be < 2^31");
+  if ((rc = grow_merge(g, n))) return rc;
+  if ((rc = dm_launch_merge(g, d_gathered, nranks, rec_cap, min_size))) return rc;
+  const int64_t hint = std::min<int64_t>(std::min<int64_t>(g->m_hint, g->h_out_cap), n);
+  DM_HIP(hipMemcpyAsync(g->h_mcnt, g->m_cnt, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost,
+                        g->stream));
+  if (hint > 0)
+    DM_HIP(hipMemcpyAsync(g->h_out, g->m_out, sizeof(dm_cluster) * (size_t)hint, hipMemcpyDeviceToHost,
+                          g->stream));
+  DM_HIP(hipStreamSynchronize(g->stream));
+  if (g->h_mcnt[1]) {
+    if (n_out) *n_out = (int64_t)g->h_mcnt[3];
+    return dm_set_error(DM_ERR_INCOMPLETE,
+                        "a band export is incomplete (flags %llu: 1 slot overflow, 2 K > rec_cap, "
+                        "4 unsorted, 8 width mismatch, 16 bands not contiguous); largest band K %llu",
+                        (unsigned long long)g->h_mcnt[1], (unsigned long long)g->h_mcnt[3]);
+  }
+  const int64_t K = (int64_t)g->h_mcnt[0];
+  const int64_t nw = std::min<int64_t>(K, cap);
+  if ((rc = copy_clusters(g, g->h_mcnt[2] != 0, K, nw, hint, g->m_out, g->m_clu, out))) return rc;
+  g->m_hint = std::max<int64_t>(1024, K + K / 4 + 64);
+  if (g->m_hint > g->h_out_cap && (rc = grow_host_out(g, g->m_hint))) return rc;
+  if (n_out) *n_out = K;
+  if (K > cap) return dm_set_error(DM_ERR_CAPACITY, "%lld clusters, capacity %lld", (long long)K,
                                    (long long)cap);
   return DM_OK;
 }

@@ -21,6 +21,7 @@
 //                   lock-free CAS union-find keyed by label
 //   k_frontier_resolve / k_frontier_compact  roots, int64 sums, cluster list
 #include "dm_internal.h"
+#include "dm_uf.h"
 
 #include <algorithm>
 
@@ -39,6 +40,15 @@ struct FGeom {
   int64_t clu_cap;
   int64_t min_size;
 };
+
+// Per-call reset in one launch: frontier counters, slot shards, edge slots.
+__global__ __launch_bounds__(256) void k_frontier_reset(int64_t n_edge, unsigned long long* cnt,
+                                                        unsigned long long* fsh, int32_t* edge_slot) {
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i0 < 4) cnt[CNT_FTILES + i0] = 0ull;
+  if (i0 < kShards * kShardWords) fsh[i0] = 0ull;
+  for (int64_t i = i0; i < n_edge; i += (int64_t)gridDim.x * blockDim.x) edge_slot[i] = -1;
+}
 
 __global__ __launch_bounds__(256) void k_ftile_list(FGeom g, int64_t NT, const int32_t* __restrict__ tile_free,
                                                     int32_t* __restrict__ ftiles,
@@ -344,30 +354,6 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
   }
 }
 
-__device__ inline int32_t g_load(int32_t* p) { return atomicOr(p, 0); }
-
-__device__ inline int32_t g_find(int32_t* par, int32_t x) {
-  for (int it = 0; it < (1 << 22); ++it) {
-    const int32_t p = g_load(par + x);
-    if (p == x) return x;
-    x = p;
-  }
-  return x;
-}
-
-// Lock-free union: hook the root with the larger label under the other.
-// Every access to parent[] is an atomic RMW, performed at the device-coherent
-// point (per-XCD L2s are not coherent; MI355X_MICROARCH.md §Workgroup dispatch).
-__device__ inline void g_unite(int32_t* par, const long long* label, int32_t a, int32_t b) {
-  for (int it = 0; it < (1 << 20); ++it) {
-    a = g_find(par, a);
-    b = g_find(par, b);
-    if (a == b) return;
-    if (label[a] < label[b]) { const int32_t t = a; a = b; b = t; }
-    if (atomicCAS(&par[a], a, b) == a) return;
-  }
-}
-
 // Unions across tile borders.  Consecutive border cells of a frontier that
 // crosses the border usually join the same two slots; a lane skips every pair
 // its predecessor lane (the previous border cell) already issued, so repeated
@@ -425,7 +411,7 @@ __global__ __launch_bounds__(256) void k_frontier_merge(FGeom g, const int32_t* 
       bool dup = false;
       for (int r = 0; r < q; ++r) dup |= sb[r] == b;
       if (has_prev && psa == sa) dup |= (psb[0] == b) | (psb[1] == b) | (psb[2] == b);
-      if (!dup) g_unite(slot_parent, slot_label, sa, b);
+      if (!dup) dm_uf_unite(slot_parent, slot_label, sa, b);
     }
   }
 }
@@ -452,12 +438,7 @@ __global__ __launch_bounds__(256) void k_frontier_resolve(FGeom g, const int32_t
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < g.slot_cap;
        s += (int64_t)gridDim.x * blockDim.x) {
     if (!slot_used(g, s_n, s)) continue;
-    int32_t r = (int32_t)s;
-    for (int it = 0; it < (1 << 22); ++it) {
-      const int32_t p = slot_parent[r];
-      if (p == r) break;
-      r = p;
-    }
+    const int32_t r = dm_uf_root(slot_parent, (int32_t)s);
     slot_root[s] = r;
     if (r != (int32_t)s) {
       atomicAdd((unsigned long long*)&slot_acc[3 * (int64_t)r + 0], (unsigned long long)slot_own[3 * s + 0]);
@@ -473,6 +454,7 @@ __global__ __launch_bounds__(256) void k_frontier_compact(FGeom g, const int32_t
                                                           const long long* __restrict__ slot_label,
                                                           const long long* __restrict__ slot_acc,
                                                           long long* __restrict__ clusters,
+                                                          int32_t* __restrict__ slot_k,
                                                           unsigned long long* cnt,
                                                           const unsigned long long* fsh) {
   __shared__ int64_t s_n[kShards];
@@ -492,6 +474,7 @@ __global__ __launch_bounds__(256) void k_frontier_compact(FGeom g, const int32_t
     if (!keep) continue;
     const unsigned long long k = k0 + __popcll(bal & ((1ull << lane) - 1));
     if ((int64_t)k >= g.clu_cap) continue;
+    slot_k[s] = (int32_t)k;
     clusters[4 * k + 0] = slot_label[s];
     clusters[4 * k + 1] = sz;
     clusters[4 * k + 2] = slot_acc[3 * s + 1];
@@ -499,58 +482,65 @@ __global__ __launch_bounds__(256) void k_frontier_compact(FGeom g, const int32_t
   }
 }
 
-// Cluster list sorted by label, with centroids (SPEC a10), in one workgroup:
-// bitonic sort of (label << 32 | record) keys in LDS, then dm_cluster records
-// with cx_m = ox + ((double)sum_x / (double)size + 0.5) * res (double, IEEE
-// division on both host and device).  Requires labels < 2^32 (W*H <= 2^32)
-// and at most kSortCap clusters; otherwise CNT_SORTED stays 0 and the host
-// sorts the raw records.
-constexpr int kSortCap = 16384;  // 128 KiB of keys
-constexpr int kSortThreads = 1024;
+// Cluster list sorted by label, with centroids (SPEC a10).  Labels are
+// unique (one per component), so a record's position is the number of
+// records with a smaller label: every workgroup stages the labels through
+// LDS in 4096-key chunks and each lane counts for its own record (the LDS
+// reads are wave-uniform broadcasts).  O(K^2) compares spread over the whole
+// chip: ~2.5M at C3's ~1.6k clusters, a few microseconds, and no serial
+// single-workgroup bitonic network.  Records become dm_cluster with
+// cx_m = ox + ((double)sum_x / (double)size + 0.5) * res (IEEE division in
+// double on host and device).  rank_of (may be NULL) receives each input
+// record's sorted position.  More than kRankSortCap records: *sorted = 0
+// and the host sorts the raw records.
+constexpr int kSortChunk = 4096;
+constexpr int kSortThreads = 256;
+constexpr int64_t kRankSortCap = 1 << 16;  // ~100 us worst case; more: host sort
 
-__global__ __launch_bounds__(kSortThreads) void k_sort_clusters(double ox, double oy, double res,
-                                                                int labels_fit,
-                                                                const long long* __restrict__ clusters,
-                                                                dm_cluster* __restrict__ out,
-                                                                unsigned long long* cnt) {
-  __shared__ unsigned long long keys[kSortCap];
+__global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy, double res,
+                                                            const long long* __restrict__ clusters,
+                                                            const unsigned long long* __restrict__ count,
+                                                            int64_t cap, dm_cluster* __restrict__ out,
+                                                            int32_t* __restrict__ rank_of,
+                                                            unsigned long long* sorted) {
+  __shared__ long long keys[kSortChunk];
   const int tid = threadIdx.x;
-  const int64_t K = (int64_t)cnt[CNT_CLUSTERS];
-  if (!labels_fit || K > kSortCap) {
-    if (tid == 0) cnt[CNT_SORTED] = 0;
+  const int64_t K = (int64_t)*count;
+  if (K > cap) {
+    if (blockIdx.x == 0 && tid == 0) *sorted = 0;
     return;
   }
-  int P = 1;
-  while (P < K) P <<= 1;
-  for (int i = tid; i < P; i += kSortThreads)
-    keys[i] = i < K ? (((unsigned long long)clusters[4 * i] << 32) | (uint32_t)i) : ~0ull;
-  __syncthreads();
-  for (int k = 2; k <= P; k <<= 1) {
-    for (int jj = k >> 1; jj > 0; jj >>= 1) {
-      for (int i = tid; i < P; i += kSortThreads) {
-        const int l = i ^ jj;
-        if (l > i) {
-          const unsigned long long a = keys[i], b = keys[l];
-          if ((a > b) == ((i & k) == 0)) { keys[i] = b; keys[l] = a; }
-        }
-      }
+  for (int64_t i0 = (int64_t)blockIdx.x * kSortThreads; i0 < K; i0 += (int64_t)gridDim.x * kSortThreads) {
+    const int64_t i = i0 + tid;
+    const long long key = i < K ? clusters[4 * i] : 0;
+    int64_t rank = 0;
+    for (int64_t c0 = 0; c0 < K; c0 += kSortChunk) {
+      const int n = (int)min((int64_t)kSortChunk, K - c0);
       __syncthreads();
+      for (int e = tid; e < n; e += kSortThreads) keys[e] = clusters[4 * (c0 + e)];
+      __syncthreads();
+      int r = 0;
+      int e = 0;
+      for (; e + 4 <= n; e += 4)
+        r += (keys[e] < key) + (keys[e + 1] < key) + (keys[e + 2] < key) + (keys[e + 3] < key);
+      for (; e < n; ++e) r += keys[e] < key;
+      rank += r;
+    }
+    if (i < K) {
+      dm_cluster c;
+      c.label = key;
+      c.size = clusters[4 * i + 1];
+      c.sum_x = clusters[4 * i + 2];
+      c.sum_y = clusters[4 * i + 3];
+      const double mx = (double)c.sum_x / (double)c.size;
+      const double my = (double)c.sum_y / (double)c.size;
+      c.cx_m = ox + (mx + 0.5) * res;
+      c.cy_m = oy + (my + 0.5) * res;
+      out[rank] = c;
+      if (rank_of) rank_of[i] = (int32_t)rank;
     }
   }
-  for (int i = tid; i < K; i += kSortThreads) {
-    const int64_t r = (int64_t)(keys[i] & 0xFFFFFFFFull);
-    dm_cluster c;
-    c.label = clusters[4 * r + 0];
-    c.size = clusters[4 * r + 1];
-    c.sum_x = clusters[4 * r + 2];
-    c.sum_y = clusters[4 * r + 3];
-    const double mx = (double)c.sum_x / (double)c.size;
-    const double my = (double)c.sum_y / (double)c.size;
-    c.cx_m = ox + (mx + 0.5) * res;
-    c.cy_m = oy + (my + 0.5) * res;
-    out[i] = c;
-  }
-  if (tid == 0) cnt[CNT_SORTED] = 1;
+  if (blockIdx.x == 0 && tid == 0) *sorted = 1;
 }
 
 // Cell slot -> final label (the root of a set is its min-label slot).
@@ -593,16 +583,25 @@ static FGeom make_fgeom(const dm_grid* g, bool want_mask, bool want_labels) {
   return fg;
 }
 
-// Runs the frontier pipeline and copies the counters plus a speculative first
-// chunk of the sorted cluster records into g->h_out with ONE synchronisation.  Returns DM_ERR_CAPACITY (with *n_clusters = slots needed)
-// when the slot arrays overflowed; the caller grows them and reruns.
-int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters,
-                        int64_t* copied) {
+int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const unsigned long long* d_count,
+                        int64_t max_records, double ox, double oy, double res, dm_cluster* out,
+                        int32_t* rank_of, unsigned long long* d_sorted) {
+  const int64_t cap = std::min<int64_t>(max_records, kRankSortCap);
+  hipLaunchKernelGGL(k_rank_sort, dim3(grid_for(cap, kSortThreads, 1024)), dim3(kSortThreads), 0, stream,
+                     ox, oy, res, clusters, d_count, cap, out, rank_of, d_sorted);
+  DM_HIP(hipGetLastError());
+  return DM_OK;
+}
+
+// Enqueues the band pipeline (no synchronisation): tile list, tile CCL,
+// border merge, roots, compaction, sort.  Shared by dm_launch_frontiers and
+// the cross-band export (dm_merge.hip).
+int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   const FGeom fg = make_fgeom(g, want_mask, want_labels);
   const int64_t cells = g->R * g->W;
-  DM_HIP(hipMemsetAsync(g->cnt + CNT_FTILES, 0, sizeof(unsigned long long) * 4, g->stream));
-  DM_HIP(hipMemsetAsync(g->fsh, 0, sizeof(unsigned long long) * kShards * kShardWords, g->stream));
-  DM_HIP(hipMemsetAsync(g->edge_slot, 0xFF, sizeof(int32_t) * 2 * g->W, g->stream));
+  hipLaunchKernelGGL(k_frontier_reset, dim3(grid_for(std::max<int64_t>(2 * g->W, kShards * kShardWords), 256, 256)), dim3(256), 0, g->stream,
+                     2 * g->W, g->cnt, g->fsh, g->edge_slot);
+  DM_HIP(hipGetLastError());
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));
 
@@ -632,7 +631,7 @@ int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "frontier_compact", &t);
   hipLaunchKernelGGL(k_frontier_compact, dim3(sgrid), dim3(256), 0, g->stream, fg,
-                     g->slot_root, g->slot_label, g->slot_acc, g->clusters, g->cnt, g->fsh);
+                     g->slot_root, g->slot_label, g->slot_acc, g->clusters, g->slot_k, g->cnt, g->fsh);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_slot_labels, dim3(grid_for(2 * g->W, 256, 1024)), dim3(256), 0, g->stream,
@@ -643,12 +642,22 @@ int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n
                        cells, g->cell_slot, g->slot_root, g->slot_label, g->labels);
     DM_HIP(hipGetLastError());
   }
-  const int labels_fit = (double)g->W * (double)(g->row0 + g->R) <= 4294967296.0 ? 1 : 0;
   dm_timer_begin(g, "sort_clusters", &t);
-  hipLaunchKernelGGL(k_sort_clusters, dim3(1), dim3(kSortThreads), 0, g->stream, g->p.origin_x,
-                     g->p.origin_y, g->p.resolution, labels_fit, g->clusters, g->out_clu, g->cnt);
+  const int rc = dm_launch_rank_sort(g->stream, g->clusters, g->cnt + CNT_CLUSTERS, g->slot_cap, g->p.origin_x,
+                           g->p.origin_y, g->p.resolution, g->out_clu, g->rank_of, g->cnt + CNT_SORTED);
   dm_timer_end(g, &t);
-  DM_HIP(hipGetLastError());
+  if (rc) return rc;
+  return DM_OK;
+}
+
+// Runs the frontier pipeline and copies the counters plus a speculative first
+// chunk of the sorted cluster records into g->h_out with ONE synchronisation.
+// Returns DM_ERR_CAPACITY (with *n_clusters = slots needed) when the slot
+// arrays overflowed; the caller grows them and reruns.
+int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters,
+                        int64_t* copied) {
+  int rc = dm_enqueue_frontiers(g, want_mask, want_labels);
+  if (rc) return rc;
   const int64_t hint = std::min<int64_t>(std::min<int64_t>(g->clu_hint, g->h_out_cap), g->slot_cap);
   DM_HIP(hipMemcpyAsync(g->h_cnt, g->cnt, sizeof(unsigned long long) * CNT_N, hipMemcpyDeviceToHost,
                         g->stream));

@@ -580,6 +580,13 @@ __global__ __launch_bounds__(kApplyThreads) void k_heavy_apply(
 
 // ---- maintenance kernels ----------------------------------------------------
 
+// Per-call reset of the device counters and integrate shards in one launch.
+__global__ __launch_bounds__(256) void k_integrate_reset(unsigned long long* cnt, unsigned long long* ish) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < CNT_N) cnt[i] = 0ull;
+  if (i < kShards * kShardWords) ish[i] = 0ull;
+}
+
 __global__ __launch_bounds__(256) void k_recount(Geom g, const int8_t* __restrict__ state,
                                                  int32_t* __restrict__ tile_free) {
   const int64_t tile = blockIdx.x;
@@ -666,8 +673,8 @@ int grid_for(int64_t n, int threads, int64_t cap = 8192) {
 int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                         const float* d_ranges, const double* d_trig) {
   const int64_t nb = (int64_t)S * N;
-  DM_HIP(hipMemsetAsync(g->cnt, 0, sizeof(unsigned long long) * CNT_N, g->stream));
-  DM_HIP(hipMemsetAsync(g->ish, 0, sizeof(unsigned long long) * kShards * kShardWords, g->stream));
+  hipLaunchKernelGGL(k_integrate_reset, dim3(2), dim3(256), 0, g->stream, g->cnt, g->ish);
+  DM_HIP(hipGetLastError());
   if (nb == 0) return DM_OK;
   RayArgs a;
   a.S = S;

@@ -52,6 +52,7 @@ enum {
 // (shard = blockIdx.x % kShards); readers sum the shards.
 constexpr int kShards = 32;
 constexpr int kShardWords = 16;  // 128 B per shard
+static_assert(kShards * kShardWords == 512, "k_integrate_reset covers 512 shard words");
 enum { SH_U = 0, SH_T = 1, SH_TH = 2, SH_ACT = 3 };  // integrate shard fields
 enum { SH_SLOT = 0 };                                 // frontier shard fields
 
@@ -120,7 +121,9 @@ struct dm_grid {
   long long* slot_own = nullptr;  // [slot][3] size, sum_x, sum_y
   long long* slot_acc = nullptr;  // [slot][3]
   long long* clusters = nullptr;  // [cap][4] label,size,sum_x,sum_y (unsorted)
-  dm_cluster* out_clu = nullptr;  // [slot_cap] sorted cluster records (k_sort_clusters)
+  int32_t* slot_k = nullptr;      // [slot_cap] root slot -> compact cluster index
+  int32_t* rank_of = nullptr;     // [slot_cap] compact cluster index -> sorted position
+  dm_cluster* out_clu = nullptr;  // [slot_cap] sorted cluster records (k_rank_sort)
   dm_cluster* h_out = nullptr;    // pinned staging for sorted cluster records
   int64_t h_out_cap = 0;
   int64_t clu_hint = 1024;        // records copied speculatively with the counters
@@ -132,6 +135,17 @@ struct dm_grid {
   int8_t* halo = nullptr;         // [2][W]: row before band, row after band
   int has_halo[2] = {0, 0};
   bool frontier_valid = false;
+
+  // cross-band merge workspace (dm_merge.hip), sized nranks * rec_cap
+  int64_t m_cap = 0;
+  int64_t m_hint = 1024;          // merged records copied speculatively with the counters
+  int32_t* m_parent = nullptr;
+  long long* m_label = nullptr;
+  long long* m_acc = nullptr;     // [m_cap][3] size, sum_x, sum_y
+  long long* m_clu = nullptr;     // [m_cap][4] merged records (unsorted)
+  dm_cluster* m_out = nullptr;    // [m_cap] merged records, sorted
+  unsigned long long* m_cnt = nullptr;    // [4] device: K, flags, sorted, max band K
+  unsigned long long* h_mcnt = nullptr;   // pinned mirror
 
   // profiling
   bool profile = false;
@@ -146,8 +160,17 @@ int dm_launch_recount(dm_grid* g);
 int dm_launch_state_from_logodds(dm_grid* g);
 int dm_launch_map_image(dm_grid* g, uint8_t* d_img);
 int dm_launch_set_state(dm_grid* g, const int8_t* d_state_in);
+int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels);
 int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters,
                         int64_t* copied);
+int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const unsigned long long* d_count,
+                        int64_t max_records, double ox, double oy, double res, dm_cluster* out,
+                        int32_t* rank_of, unsigned long long* d_sorted);
+// cross-band exchange (dm_merge.hip)
+int64_t dm_export_nbytes(int64_t W, int64_t rec_cap);
+int dm_launch_export(dm_grid* g, void* d_export, int64_t rec_cap);
+int dm_launch_merge(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap,
+                    int64_t min_size);
 int dm_launch_ld06(dm_grid* g, int32_t S, const dm_ld06_point* d_pts, const int64_t* d_offsets,
                    int32_t N, int dir, float* d_ranges, float* d_intensities);
 

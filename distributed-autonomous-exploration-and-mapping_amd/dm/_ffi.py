@@ -22,6 +22,7 @@ DM_ERR_OOM = -4
 DM_ERR_CAPACITY = -5
 DM_ERR_IO = -6
 DM_ERR_STATE = -7
+DM_ERR_INCOMPLETE = -8
 DM_TILE = 64
 
 _ERR_NAMES = {
@@ -32,6 +33,7 @@ _ERR_NAMES = {
     DM_ERR_CAPACITY: "DM_ERR_CAPACITY",
     DM_ERR_IO: "DM_ERR_IO",
     DM_ERR_STATE: "DM_ERR_STATE",
+    DM_ERR_INCOMPLETE: "DM_ERR_INCOMPLETE",
 }
 
 
@@ -149,6 +151,9 @@ SIGNATURES = {
     "dm_map_image": [_vp, _vp],
     "dm_ld06_to_scans": [_vp, _i32, _vp, _vp, _i32, ctypes.c_int, _vp, _vp],
     "dm_ld06_to_scans_device": [_vp, _i32, _vp, _vp, _i32, ctypes.c_int, _vp, _vp],
+    "dm_export_bytes": [_vp, _i64, ctypes.POINTER(_i64)],
+    "dm_frontiers_export_device": [_vp, _vp, _i64],
+    "dm_merge_bands": [_vp, _vp, _i32, _i64, _i64, _vp, _i64, ctypes.POINTER(_i64)],
 }
 # functions returning const char*
 STRING_FUNCS = ("dm_last_error", "dm_version")

@@ -264,6 +264,40 @@ class OccupancyMapper:
             check(self._lib.dm_get_edge_labels(self._handle(), _vp(first), _vp(last)))
         return first, last
 
+    # -- cross-band exchange (device-resident; dm/sharded.py) --------------
+    def export_bytes(self, rec_cap: int) -> int:
+        n = ctypes.c_int64(0)
+        check(self._lib.dm_export_bytes(self._handle(), int(rec_cap), ctypes.byref(n)))
+        return int(n.value)
+
+    def frontiers_export_device(self, d_export_ptr: int, rec_cap: int):
+        """Band frontiers + export record into a device buffer of
+        export_bytes(rec_cap) bytes; asynchronous on the handle's stream."""
+        with self._lock:
+            check(self._lib.dm_frontiers_export_device(self._handle(), ctypes.c_void_p(d_export_ptr),
+                                                       int(rec_cap)))
+
+    def merge_bands(self, d_gathered_ptr: int, nranks: int, rec_cap: int, min_size: int):
+        """Merge all-gathered export records on the device.  Returns
+        (clusters, None) or (None, largest band K) when a band's record was
+        incomplete (DM_ERR_INCOMPLETE: rerun with more capacity)."""
+        n = ctypes.c_int64(0)
+        with self._lock:
+            while True:
+                buf = self._mbuf if getattr(self, "_mbuf", None) is not None else \
+                    np.empty(1 << 14, dtype=np.dtype(CLUSTER_DTYPE))
+                rc = self._lib.dm_merge_bands(self._handle(), ctypes.c_void_p(d_gathered_ptr), int(nranks),
+                                              int(rec_cap), int(min_size), _vp(buf), buf.shape[0],
+                                              ctypes.byref(n))
+                self._mbuf = buf
+                if rc == _ffi.DM_ERR_INCOMPLETE:
+                    return None, int(n.value)
+                if rc == _ffi.DM_ERR_CAPACITY and n.value > buf.shape[0]:
+                    self._mbuf = np.empty(int(n.value) * 2, dtype=np.dtype(CLUSTER_DTYPE))
+                    continue
+                check(rc)
+                return buf[: int(n.value)].copy(), None
+
     # -- checkpoint / streams / profiling ----------------------------------
     def save(self, path: str):
         with self._lock:

@@ -8,7 +8,15 @@ the global map, rows_r a multiple of 64 except for the last band.
   whose max-range disk reaches its band; libdm clips rays to the band, so
   cell writes are disjoint and the union of the bands equals a 1-GPU map
   bit for bit (tests/test_sharded.py).
-* Frontier extraction has the only real exchange steps:
+* Frontier extraction has the only real exchange steps.  On GPUs they are
+  device-resident (one host synchronisation per call, as on one GPU): edge
+  rows are gathered with RCCL straight into the neighbours' halos, every band
+  writes an export record (include/dm.h: its edge components as indices into
+  its sorted cluster list, and the clusters), the records are all-gathered
+  with RCCL and every rank merges them with libdm's merge kernels
+  (dm_merge_bands, csrc/dm_merge.hip).  The host path below is the
+  restatement the CPU tests run (and the fallback when a band's record
+  overflows its capacity):
   1. halo rows: each band's first/last state rows are all-gathered (W bytes
      per edge) and installed as the neighbours' halos, so the 8-neighbour
      frontier test sees across band edges;
@@ -149,6 +157,7 @@ class ShardedMapper:
         self.row0, self.rows = int(bp.band_row0), int(bp.band_rows or params.height)
         self.W = int(params.width)
         self._device = None
+        self._dev_path = False
         if world_size > 1:
             import torch.distributed as dist
 
@@ -158,6 +167,20 @@ class ShardedMapper:
                 import torch
 
                 self._device = torch.device("cuda", device)
+            # device-resident exchange when the band is a libdm handle
+            self._dev_path = hasattr(self.band, "frontiers_export_device")
+            if self._dev_path:
+                import torch
+
+                self._torch = torch
+                self._tdev = torch.device("cuda", device)
+                # one stream for the band's kernels and the collectives
+                # around them: RCCL orders itself against it
+                self.stream = torch.cuda.Stream(device=self._tdev)
+                self.band.set_stream(self.stream.cuda_stream)
+                self.rec_cap = 4096
+                self._bufs = {}
+                self.fallbacks = 0
 
     # -- integration ------------------------------------------------------
     def scan_mask(self, poses) -> np.ndarray:
@@ -200,9 +223,59 @@ class ShardedMapper:
         after = rows[self.rank + 1, 0] if self.rank + 1 < self.world_size else None
         self.band.set_halo(before, after)
 
+    # -- device-resident exchange (RCCL + dm_merge_bands) -------------------
+    def _buf(self, name, n, dtype):
+        t = self._bufs.get(name)
+        if t is None or t.numel() != n:
+            t = self._torch.empty(n, dtype=dtype, device=self._tdev)
+            self._bufs[name] = t
+        return t
+
+    def _gather_dev(self, t, out):
+        """all-gather a device tensor into out ([P * n], rank order)."""
+        if self._nccl:
+            self._dist.all_gather_into_tensor(out, t, group=self.group)
+        else:  # gloo rehearsal on GPUs: host-staged
+            o = self._torch.empty(out.numel(), dtype=t.dtype)
+            self._dist.all_gather_into_tensor(o, t.cpu(), group=self.group)
+            out.copy_(o)
+
+    def _frontiers_device(self):
+        torch = self._torch
+        W, P, r = self.W, self.world_size, self.rank
+        with torch.cuda.stream(self.stream):
+            rows = self._buf("rows", 2 * W, torch.int8)
+            grows = self._buf("grows", P * 2 * W, torch.int8)
+            self.band.edge_rows_device(rows.data_ptr(), rows.data_ptr() + W)
+            self._gather_dev(rows, grows)
+            g0 = grows.data_ptr()
+            self.band.set_halo_device(g0 + (r - 1) * 2 * W + W if r > 0 else None,
+                                      g0 + (r + 1) * 2 * W if r + 1 < P else None)
+            nb = self.band.export_bytes(self.rec_cap)
+            exp = self._buf("exp", nb, torch.uint8)
+            gexp = self._buf("gexp", P * nb, torch.uint8)
+            self.band.frontiers_export_device(exp.data_ptr(), self.rec_cap)
+            self._gather_dev(exp, gexp)
+            clusters, max_k = self.band.merge_bands(gexp.data_ptr(), P, self.rec_cap, self.min_size)
+        if clusters is not None:
+            return Frontiers(clusters=clusters)
+        # a band's record was incomplete; every rank merged the same gathered
+        # headers, so all ranks take this branch together
+        self.fallbacks += 1
+        while self.rec_cap < max_k:
+            self.rec_cap *= 2
+        return self._frontiers_host(False, False)
+
     def frontiers(self, want_mask=False, want_labels=False) -> Frontiers:
         if self.world_size == 1:
             return self.band.frontiers(want_mask=want_mask, want_labels=want_labels)
+        if self._dev_path and not (want_mask or want_labels):
+            return self._frontiers_device()
+        return self._frontiers_host(want_mask, want_labels)
+
+    def _frontiers_host(self, want_mask, want_labels) -> Frontiers:
+        if self._dev_path:
+            self._torch.cuda.synchronize(self._tdev)
         self.exchange_halos()
         local = self.band.frontiers(want_mask=want_mask, want_labels=want_labels)
         first, last = self.band.edge_labels()

@@ -46,6 +46,7 @@ extern "C" {
 #define DM_ERR_CAPACITY (-5)
 #define DM_ERR_IO (-6)
 #define DM_ERR_STATE (-7)
+#define DM_ERR_INCOMPLETE (-8) /* a band's export record was incomplete (dm_merge_bands) */
 
 /* Tile edge (cells) used by the kernels; band_row0 must be a multiple of it. */
 #define DM_TILE 64
@@ -164,6 +165,34 @@ int dm_get_edge_rows(dm_grid* g, int8_t* first_row, int8_t* last_row);
 int dm_get_edge_rows_device(dm_grid* g, int8_t* d_first_row, int8_t* d_last_row);
 /* After dm_frontiers: band-local labels of the first/last rows (int64[W]). */
 int dm_get_edge_labels(dm_grid* g, int64_t* first_row, int64_t* last_row);
+
+/* ---- Cross-band frontier exchange, device-resident
+ * Replaces the host-side label merge of a row-band sharded map: every band
+ * writes an export record into a caller-owned device buffer, the caller
+ * all-gathers the records with RCCL (rank order = band order, bands
+ * contiguous), and dm_merge_bands resolves labels across band edges and
+ * merges the clusters on the device.  Export record (little-endian,
+ * dm_export_bytes bytes):
+ *   int64 hdr[8]  K (band clusters), flags (0 = complete; bit0 slot overflow,
+ *                 bit1 K > rec_cap, bit2 too many clusters to sort on the
+ *                 device), band_row0, band_rows, width, 0, 0, 0
+ *   int32 edge[2][width]  component of each cell of the band's first / last
+ *                 row as an index into rec[], -1 off-frontier
+ *   int64 rec[rec_cap][4] (label, size, sum_x, sum_y), sorted by label;
+ *                 band-local min-index labels, global cell coordinates
+ * The band handle must have min_frontier_size <= 1 (the size filter applies
+ * to merged clusters: dm_merge_bands' min_size). */
+int dm_export_bytes(const dm_grid* g, int64_t rec_cap, int64_t* bytes);
+/* Band frontier extraction + export record, asynchronous on the handle's
+ * stream (no host synchronisation).  Halo rows must be set first. */
+int dm_frontiers_export_device(dm_grid* g, void* d_export, int64_t rec_cap);
+/* Merge nranks gathered export records (d_gathered = nranks consecutive
+ * records of dm_export_bytes(rec_cap) bytes) into global clusters sorted by
+ * label, keeping those with size >= min_size.  Synchronous.  Returns
+ * DM_ERR_INCOMPLETE (*n_out = largest band K) when a record is flagged
+ * incomplete, DM_ERR_CAPACITY (*n_out = clusters) when cap is too small. */
+int dm_merge_bands(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap,
+                   int64_t min_size, dm_cluster* out, int64_t cap, int64_t* n_out);
 
 /* LD06 driver point (ldlidar::PointData fields the LaserScan conversion uses). */
 typedef struct dm_ld06_point {
