@@ -358,7 +358,6 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if ((rc = dev_alloc(&g->ish, 2 * kShards * kShardWords, "shard counters"))) return fail(rc);
   g->fsh = g->ish + kShards * kShardWords;
   if ((rc = dev_alloc(&g->ftiles, g->NT, "frontier tiles"))) return fail(rc);
-  if ((rc = dev_alloc(&g->fmap, g->NT, "frontier tile map"))) return fail(rc);
   if ((rc = dev_alloc(&g->border, g->NT * 256, "frontier borders"))) return fail(rc);
   if ((rc = dev_alloc(&g->edge_slot, 2 * g->W, "edge slots"))) return fail(rc);
   if ((rc = dev_alloc(&g->edge_label, 2 * g->W, "edge labels"))) return fail(rc);
@@ -390,8 +389,8 @@ int dm_destroy(dm_grid* g) {
   dev_free(g->tile_free); dev_free(g->cnt); dev_free(g->beams); dev_free(g->segs);
   dev_free(g->act_tiles); dev_free(g->act_off); dev_free(g->act_cur); dev_free(g->trig);
   dev_free(g->act_heavy); dev_free(g->heavy_list); dev_free(g->items); dev_free(g->slabs);
-  dev_free(g->pose4); dev_free(g->ranges); dev_free(g->ftiles); dev_free(g->fmap);
-  dev_free(g->border); dev_free(g->slot_label); dev_free(g->slot_parent); dev_free(g->slot_root);
+  dev_free(g->pose4); dev_free(g->ranges); 
+  dev_free(g->border); dev_free(g->ftiles); dev_free(g->slot_label); dev_free(g->slot_parent); dev_free(g->slot_root);
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
   dev_free(g->edge_slot); dev_free(g->edge_label); dev_free(g->mask); dev_free(g->labels);
   dev_free(g->halo); dev_free(g->out_clu); dev_free(g->ish); dev_free(g->act_raw);
@@ -506,7 +505,7 @@ int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out) {
   const uint64_t v[10] = {dm_shard_sum(g->h_sh, SH_U),  dm_shard_sum(g->h_sh, SH_T),
                           dm_shard_sum(g->h_sh, SH_TH), g->h_cnt[CNT_SEGS],
                           g->h_cnt[CNT_ACTIVE],         g->h_cnt[CNT_ITEMS],
-                          g->h_cnt[CNT_HEAVY],          g->h_cnt[CNT_FTILES],
+                          g->h_cnt[CNT_HEAVY],          g->h_cnt[g->fparity ? CNT_FL1 : CNT_FL0],
                           dm_shard_sum(fs, SH_SLOT),    g->h_cnt[CNT_CLUSTERS]};
   for (int32_t i = 0; i < cap && i < 10; ++i) out[i] = v[i];
   if (n_out) *n_out = 10;

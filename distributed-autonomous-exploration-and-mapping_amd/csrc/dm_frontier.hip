@@ -33,6 +33,7 @@ constexpr int kMaxRoots = 1024;       // 8-connected components in a 64x64 tile
 struct FGeom {
   int32_t W, R, row0, TX, TY;
   int32_t has_before, has_after;
+  int64_t NT;
   int32_t want_mask, want_labels;
   int64_t H;
   int64_t slot_cap;
@@ -41,27 +42,35 @@ struct FGeom {
   int64_t min_size;
 };
 
-// Per-call reset in one launch: frontier counters, slot shards, edge slots.
-__global__ __launch_bounds__(256) void k_frontier_reset(int64_t n_edge, unsigned long long* cnt,
-                                                        unsigned long long* fsh, int32_t* edge_slot) {
+// Per-call preparation in one launch: reset the frontier counters, slot
+// shards and edge slots, and list the tiles holding >= 1 free cell (only
+// free cells can be frontier cells; tile_free is maintained by the
+// integrate kernels, so every other tile is skipped without reading it).
+// The list length goes to *list_n, which the previous call zeroed; this call
+// zeroes *other_n for the next one (the two alternate by call parity).
+__global__ __launch_bounds__(256) void k_frontier_prep(int64_t NT, const int32_t* __restrict__ tile_free,
+                                                       int32_t* __restrict__ ftiles,
+                                                       unsigned long long* list_n,
+                                                       unsigned long long* other_n, int64_t n_edge,
+                                                       unsigned long long* cnt, unsigned long long* fsh,
+                                                       int32_t* __restrict__ edge_slot) {
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i0 < 4) cnt[CNT_FTILES + i0] = 0ull;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int lane = __lane_id();
+  if (i0 < 3) cnt[CNT_SLOTS + i0] = 0ull;  // slots, clusters, overflow
+  if (i0 == 0) *other_n = 0ull;
   if (i0 < kShards * kShardWords) fsh[i0] = 0ull;
-  for (int64_t i = i0; i < n_edge; i += (int64_t)gridDim.x * blockDim.x) edge_slot[i] = -1;
-}
-
-__global__ __launch_bounds__(256) void k_ftile_list(FGeom g, int64_t NT, const int32_t* __restrict__ tile_free,
-                                                    int32_t* __restrict__ ftiles,
-                                                    int32_t* __restrict__ fmap,
-                                                    unsigned long long* cnt) {
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < NT;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    int32_t idx = -1;
-    if (tile_free[t] > 0) {
-      idx = (int32_t)atomicAdd(&cnt[CNT_FTILES], 1ull);
-      ftiles[idx] = (int32_t)t;
-    }
-    fmap[t] = idx;
+  for (int64_t i = i0; i < n_edge; i += stride) edge_slot[i] = -1;
+  for (int64_t t0 = i0 - lane; t0 < NT; t0 += stride) {  // whole waves: ballot compaction
+    const int64_t t = t0 + lane;
+    const bool f = t < NT && tile_free[t] > 0;
+    const unsigned long long bal = __ballot(f);
+    if (!bal) continue;
+    const int first = __ffsll(bal) - 1;
+    unsigned long long base = 0;
+    if (lane == first) base = atomicAdd(list_n, (unsigned long long)__popcll(bal));
+    base = __shfl(base, first);
+    if (f) ftiles[base + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)t;
   }
 }
 
@@ -125,7 +134,8 @@ __device__ inline uint32_t halo_unknown(const FGeom& g, const int8_t* state, con
 //     slot ids for k_frontier_merge.
 __global__ __launch_bounds__(kFT) void k_frontier_tile(
     FGeom g, const int8_t* __restrict__ state, const int8_t* __restrict__ halo,
-    const int32_t* __restrict__ ftiles, int32_t* __restrict__ border,
+    const int32_t* __restrict__ ftiles, const unsigned long long* __restrict__ list_n,
+    int32_t* __restrict__ border,
     long long* __restrict__ slot_label, int32_t* __restrict__ slot_parent,
     long long* __restrict__ slot_own, long long* __restrict__ slot_acc,
     uint8_t* __restrict__ mask, int32_t* __restrict__ cell_slot, int32_t* __restrict__ edge_slot,
@@ -145,9 +155,10 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
   __shared__ int32_t nroots;
   __shared__ long long sbase;
   const int tid = threadIdx.x, lane = __lane_id();
-  const int64_t nft = (int64_t)cnt[CNT_FTILES];
-  for (int64_t j = blockIdx.x; j < nft; j += gridDim.x) {
-    const int32_t tile = ftiles[j];
+  const int64_t nft = (int64_t)*list_n;
+  for (int64_t jj = blockIdx.x; jj < nft; jj += gridDim.x) {
+    const int32_t tile = ftiles[jj];
+    const int64_t j = tile;  // border records are indexed by tile
     const int32_t tx0 = (tile % g.TX) * DM_TS;
     const int32_t ty0 = (tile / g.TX) * DM_TS;  // band-local
     // ---- 1. bit rows ------------------------------------------------------
@@ -359,15 +370,17 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
 // its predecessor lane (the previous border cell) already issued, so repeated
 // unions do not queue same-address atomics behind each other.
 __global__ __launch_bounds__(256) void k_frontier_merge(FGeom g, const int32_t* __restrict__ ftiles,
-                                                        const int32_t* __restrict__ fmap,
+                                                        const unsigned long long* __restrict__ list_n,
+                                                        const int32_t* __restrict__ tile_free,
                                                         const int32_t* __restrict__ border,
                                                         const long long* __restrict__ slot_label,
                                                         int32_t* slot_parent,
                                                         const unsigned long long* cnt) {
   const int tid = threadIdx.x, lane = __lane_id();
-  const int64_t nft = (int64_t)cnt[CNT_FTILES];
-  for (int64_t j = blockIdx.x; j < nft; j += gridDim.x) {
-    const int32_t tile = ftiles[j];
+  const int64_t nft = (int64_t)*list_n;
+  for (int64_t jj = blockIdx.x; jj < nft; jj += gridDim.x) {
+    const int32_t tile = ftiles[jj];
+    const int64_t j = tile;
     const int32_t tx = tile % g.TX, ty = tile / g.TX;
     const int32_t* bA = border + j * 256;
     // candidate pairs of this lane: (sa, sb[0..2]); -1 = none
@@ -375,7 +388,7 @@ __global__ __launch_bounds__(256) void k_frontier_merge(FGeom g, const int32_t* 
     if (tid < 64) {  // our last column vs the right neighbour's first column
       sa = bA[3 * 64 + tid];
       int32_t nb;
-      if (sa >= 0 && tx + 1 < g.TX && (nb = fmap[ty * g.TX + tx + 1]) >= 0) {
+      if (sa >= 0 && tx + 1 < g.TX && tile_free[nb = ty * g.TX + tx + 1] > 0) {
         const int32_t* bB = border + (int64_t)nb * 256 + 2 * 64;
         for (int d = -1; d <= 1; ++d)
           if (tid + d >= 0 && tid + d < 64) sb[d + 1] = bB[tid + d];
@@ -384,7 +397,7 @@ __global__ __launch_bounds__(256) void k_frontier_merge(FGeom g, const int32_t* 
       const int x = tid - 64;
       sa = bA[1 * 64 + x];
       int32_t nb;
-      if (sa >= 0 && ty + 1 < g.TY && (nb = fmap[(ty + 1) * g.TX + tx]) >= 0) {
+      if (sa >= 0 && ty + 1 < g.TY && tile_free[nb = (ty + 1) * g.TX + tx] > 0) {
         const int32_t* bC = border + (int64_t)nb * 256;
         for (int d = -1; d <= 1; ++d)
           if (x + d >= 0 && x + d < 64) sb[d + 1] = bC[x + d];
@@ -392,12 +405,12 @@ __global__ __launch_bounds__(256) void k_frontier_merge(FGeom g, const int32_t* 
     } else if (tid == 128) {  // our (63,63) vs (tx+1,ty+1)'s (0,0)
       sa = bA[1 * 64 + 63];
       int32_t nb;
-      if (sa >= 0 && tx + 1 < g.TX && ty + 1 < g.TY && (nb = fmap[(ty + 1) * g.TX + tx + 1]) >= 0)
+      if (sa >= 0 && tx + 1 < g.TX && ty + 1 < g.TY && tile_free[nb = (ty + 1) * g.TX + tx + 1] > 0)
         sb[1] = border[(int64_t)nb * 256 + 0];
     } else if (tid == 129) {  // our (0,63) vs (tx-1,ty+1)'s (63,0)
       sa = bA[1 * 64 + 0];
       int32_t nb;
-      if (sa >= 0 && tx > 0 && ty + 1 < g.TY && (nb = fmap[(ty + 1) * g.TX + tx - 1]) >= 0)
+      if (sa >= 0 && tx > 0 && ty + 1 < g.TY && tile_free[nb = (ty + 1) * g.TX + tx - 1] > 0)
         sb[1] = border[(int64_t)nb * 256 + 63];
     }
     // predecessor lane's pairs (lanes 0 of waves 0/1 start an edge: none)
@@ -484,18 +497,21 @@ __global__ __launch_bounds__(256) void k_frontier_compact(FGeom g, const int32_t
 
 // Cluster list sorted by label, with centroids (SPEC a10).  Labels are
 // unique (one per component), so a record's position is the number of
-// records with a smaller label: every workgroup stages the labels through
-// LDS in 4096-key chunks and each lane counts for its own record (the LDS
-// reads are wave-uniform broadcasts).  O(K^2) compares spread over the whole
-// chip: ~2.5M at C3's ~1.6k clusters, a few microseconds, and no serial
-// single-workgroup bitonic network.  Records become dm_cluster with
+// records with a smaller label.  One workgroup per 64 records (lane = record),
+// its 16 waves split the keys: the labels are staged through LDS in
+// 4096-key chunks (every thread's loads in flight at once) and each wave
+// counts over its sixteenth of the chunk with wave-uniform LDS broadcasts;
+// the 16 partial counts are summed in LDS.  O(K^2) compares spread over
+// ceil(K/64) workgroups: no serial single-workgroup network, a few
+// microseconds at C3's ~1.6k clusters.  Records become dm_cluster with
 // cx_m = ox + ((double)sum_x / (double)size + 0.5) * res (IEEE division in
 // double on host and device).  rank_of (may be NULL) receives each input
 // record's sorted position.  More than kRankSortCap records: *sorted = 0
 // and the host sorts the raw records.
 constexpr int kSortChunk = 4096;
-constexpr int kSortThreads = 256;
-constexpr int64_t kRankSortCap = 1 << 16;  // ~100 us worst case; more: host sort
+constexpr int kSortThreads = 1024;
+constexpr int kSortWaves = kSortThreads / 64;
+constexpr int64_t kRankSortCap = 1 << 16;
 
 __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy, double res,
                                                             const long long* __restrict__ clusters,
@@ -504,54 +520,68 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
                                                             int32_t* __restrict__ rank_of,
                                                             unsigned long long* sorted) {
   __shared__ long long keys[kSortChunk];
-  const int tid = threadIdx.x;
+  __shared__ int32_t part[kSortWaves][64];
+  const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
   const int64_t K = (int64_t)*count;
-  if (K > cap) {
-    if (blockIdx.x == 0 && tid == 0) *sorted = 0;
-    return;
-  }
-  for (int64_t i0 = (int64_t)blockIdx.x * kSortThreads; i0 < K; i0 += (int64_t)gridDim.x * kSortThreads) {
-    const int64_t i = i0 + tid;
-    const long long key = i < K ? clusters[4 * i] : 0;
-    int64_t rank = 0;
-    for (int64_t c0 = 0; c0 < K; c0 += kSortChunk) {
-      const int n = (int)min((int64_t)kSortChunk, K - c0);
-      __syncthreads();
-      for (int e = tid; e < n; e += kSortThreads) keys[e] = clusters[4 * (c0 + e)];
-      __syncthreads();
-      int r = 0;
-      int e = 0;
-      for (; e + 4 <= n; e += 4)
-        r += (keys[e] < key) + (keys[e + 1] < key) + (keys[e + 2] < key) + (keys[e + 3] < key);
-      for (; e < n; ++e) r += keys[e] < key;
-      rank += r;
+  if (blockIdx.x == 0 && tid == 0) *sorted = K <= cap ? 1ull : 0ull;
+  if (K > cap) return;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  if ((int64_t)blockIdx.x * 64 >= K) return;  // whole workgroup: no barrier skipped
+  const long long key = i < K ? clusters[4 * i] : 0;
+  int32_t r = 0;
+  for (int64_t c0 = 0; c0 < K; c0 += kSortChunk) {
+    const int n = (int)min((int64_t)kSortChunk, K - c0);
+    __syncthreads();
+    {
+      long long v[kSortChunk / kSortThreads];
+#pragma unroll
+      for (int q = 0; q < kSortChunk / kSortThreads; ++q) {
+        const int e = tid + q * kSortThreads;
+        v[q] = e < n ? clusters[4 * (c0 + e)] : 0;
+      }
+#pragma unroll
+      for (int q = 0; q < kSortChunk / kSortThreads; ++q) {
+        const int e = tid + q * kSortThreads;
+        if (e < n) keys[e] = v[q];
+      }
     }
-    if (i < K) {
-      dm_cluster c;
-      c.label = key;
-      c.size = clusters[4 * i + 1];
-      c.sum_x = clusters[4 * i + 2];
-      c.sum_y = clusters[4 * i + 3];
-      const double mx = (double)c.sum_x / (double)c.size;
-      const double my = (double)c.sum_y / (double)c.size;
-      c.cx_m = ox + (mx + 0.5) * res;
-      c.cy_m = oy + (my + 0.5) * res;
-      out[rank] = c;
-      if (rank_of) rank_of[i] = (int32_t)rank;
-    }
+    __syncthreads();
+    const int per = (n + kSortWaves - 1) / kSortWaves;
+    const int lo = min(n, w * per), hi = min(n, lo + per);
+    int e = lo;
+    for (; e + 4 <= hi; e += 4)
+      r += (keys[e] < key) + (keys[e + 1] < key) + (keys[e + 2] < key) + (keys[e + 3] < key);
+    for (; e < hi; ++e) r += keys[e] < key;
   }
-  if (blockIdx.x == 0 && tid == 0) *sorted = 1;
+  part[w][lane] = r;
+  __syncthreads();
+  if (w == 0 && i < K) {
+    int32_t rank = 0;
+#pragma unroll
+    for (int q = 0; q < kSortWaves; ++q) rank += part[q][lane];
+    dm_cluster c;
+    c.label = key;
+    c.size = clusters[4 * i + 1];
+    c.sum_x = clusters[4 * i + 2];
+    c.sum_y = clusters[4 * i + 3];
+    const double mx = (double)c.sum_x / (double)c.size;
+    const double my = (double)c.sum_y / (double)c.size;
+    c.cx_m = ox + (mx + 0.5) * res;
+    c.cy_m = oy + (my + 0.5) * res;
+    out[rank] = c;
+    if (rank_of) rank_of[i] = rank;
+  }
 }
 
 // Cell slot -> final label (the root of a set is its min-label slot).
-__global__ __launch_bounds__(256) void k_slot_labels(int64_t n, const int32_t* __restrict__ cslot,
+__global__ __launch_bounds__(256) void k_slot_labels(int64_t n, int64_t slot_cap, const int32_t* __restrict__ cslot,
                                                      const int32_t* __restrict__ slot_root,
                                                      const long long* __restrict__ slot_label,
                                                      long long* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t s = cslot[i];
-    out[i] = s < 0 ? -1 : slot_label[slot_root[s]];
+    out[i] = (s < 0 || s >= slot_cap) ? -1 : slot_label[slot_root[s]];
   }
 }
 
@@ -571,6 +601,7 @@ static FGeom make_fgeom(const dm_grid* g, bool want_mask, bool want_labels) {
   fg.row0 = (int32_t)g->row0;
   fg.TX = (int32_t)g->TX;
   fg.TY = (int32_t)g->TY;
+  fg.NT = g->NT;
   fg.has_before = g->has_halo[0];
   fg.has_after = g->has_halo[1];
   fg.want_mask = want_mask ? 1 : 0;
@@ -587,7 +618,7 @@ int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const uns
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
                         int32_t* rank_of, unsigned long long* d_sorted) {
   const int64_t cap = std::min<int64_t>(max_records, kRankSortCap);
-  hipLaunchKernelGGL(k_rank_sort, dim3(grid_for(cap, kSortThreads, 1024)), dim3(kSortThreads), 0, stream,
+  hipLaunchKernelGGL(k_rank_sort, dim3(grid_for(cap, 64, 1 << 20)), dim3(kSortThreads), 0, stream,
                      ox, oy, res, clusters, d_count, cap, out, rank_of, d_sorted);
   DM_HIP(hipGetLastError());
   return DM_OK;
@@ -599,28 +630,26 @@ int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const uns
 int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   const FGeom fg = make_fgeom(g, want_mask, want_labels);
   const int64_t cells = g->R * g->W;
-  hipLaunchKernelGGL(k_frontier_reset, dim3(grid_for(std::max<int64_t>(2 * g->W, kShards * kShardWords), 256, 256)), dim3(256), 0, g->stream,
-                     2 * g->W, g->cnt, g->fsh, g->edge_slot);
+  g->fparity ^= 1;
+  unsigned long long* list_n = g->cnt + (g->fparity ? CNT_FL1 : CNT_FL0);
+  unsigned long long* other_n = g->cnt + (g->fparity ? CNT_FL0 : CNT_FL1);
+  hipLaunchKernelGGL(k_frontier_prep, dim3(grid_for(std::max<int64_t>(std::max<int64_t>(g->NT, 2 * g->W), kShards * kShardWords), 256, 1024)), dim3(256), 0,
+                     g->stream, g->NT, g->tile_free, g->ftiles, list_n, other_n, 2 * g->W, g->cnt, g->fsh,
+                     g->edge_slot);
   DM_HIP(hipGetLastError());
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));
-
   KernelTimer t;
-  dm_timer_begin(g, "ftile_list", &t);
-  hipLaunchKernelGGL(k_ftile_list, dim3(grid_for(g->NT, 256, 4096)), dim3(256), 0, g->stream, fg,
-                     g->NT, g->tile_free, g->ftiles, g->fmap, g->cnt);
-  dm_timer_end(g, &t);
-  DM_HIP(hipGetLastError());
   const int nft_grid = grid_for(g->NT, 1, 2048);
   dm_timer_begin(g, "frontier_tile", &t);
   hipLaunchKernelGGL(k_frontier_tile, dim3(nft_grid), dim3(kFT), 0, g->stream, fg, g->state,
-                     g->halo, g->ftiles, g->border, g->slot_label, g->slot_parent, g->slot_own,
+                     g->halo, g->ftiles, list_n, g->border, g->slot_label, g->slot_parent, g->slot_own,
                      g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "frontier_merge", &t);
-  hipLaunchKernelGGL(k_frontier_merge, dim3(nft_grid), dim3(256), 0, g->stream, fg, g->ftiles,
-                     g->fmap, g->border, g->slot_label, g->slot_parent, g->cnt);
+  hipLaunchKernelGGL(k_frontier_merge, dim3(nft_grid), dim3(256), 0, g->stream, fg, g->ftiles, list_n, g->tile_free,
+                     g->border, g->slot_label, g->slot_parent, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   const int sgrid = grid_for(g->slot_cap, 256, 1024);
@@ -635,11 +664,11 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_slot_labels, dim3(grid_for(2 * g->W, 256, 1024)), dim3(256), 0, g->stream,
-                     2 * g->W, g->edge_slot, g->slot_root, g->slot_label, g->edge_label);
+                     2 * g->W, g->slot_cap, g->edge_slot, g->slot_root, g->slot_label, g->edge_label);
   DM_HIP(hipGetLastError());
   if (want_labels) {
     hipLaunchKernelGGL(k_slot_labels, dim3(grid_for(cells, 256, 8192)), dim3(256), 0, g->stream,
-                       cells, g->cell_slot, g->slot_root, g->slot_label, g->labels);
+                       cells, g->slot_cap, g->cell_slot, g->slot_root, g->slot_label, g->labels);
     DM_HIP(hipGetLastError());
   }
   dm_timer_begin(g, "sort_clusters", &t);

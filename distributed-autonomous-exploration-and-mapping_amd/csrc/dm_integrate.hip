@@ -186,67 +186,83 @@ __device__ inline void block_scan3(int64_t v[3], int64_t excl[3], int64_t tot[3]
   }
 }
 
-__global__ __launch_bounds__(1024) void k_plan(Geom g, const int32_t* __restrict__ act_raw,
-                                               const unsigned long long* __restrict__ ish,
-                                               int32_t* __restrict__ act_tiles, int32_t* __restrict__ tile_slot,
-                                               const int32_t* __restrict__ tile_count,
-                                               int32_t* __restrict__ act_off, int32_t* __restrict__ act_cur,
-                                               int32_t* __restrict__ act_heavy,
-                                               int32_t* __restrict__ heavy_list,
-                                               int2* __restrict__ items, unsigned long long* cnt) {
+constexpr int kPlanThreads = 1024;
+constexpr int kPlanPer = 8;  // active tiles per thread per round, loads batched in registers
+
+__global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __restrict__ act_raw,
+                                                       const unsigned long long* __restrict__ ish,
+                                                       int32_t* __restrict__ act_tiles, int32_t* __restrict__ tile_slot,
+                                                       const int32_t* __restrict__ tile_count,
+                                                       int32_t* __restrict__ act_off, int32_t* __restrict__ act_cur,
+                                                       int32_t* __restrict__ act_heavy,
+                                                       int32_t* __restrict__ heavy_list,
+                                                       int2* __restrict__ items, unsigned long long* cnt) {
   __shared__ int64_t ws[17][3];
   __shared__ int32_t soff[kShards + 1];
-  const int tid = threadIdx.x;
-  if (tid == 0) {
-    int32_t run = 0;
-    for (int s = 0; s < kShards; ++s) {
-      soff[s] = run;
-      run += (int32_t)min((unsigned long long)g.act_cap, ish[s * kShardWords + SH_ACT]);
+  const int tid = threadIdx.x, lane = __lane_id();
+  if (tid < 64) {  // shard offsets: one wave, one load per lane, shuffle scan
+    const int32_t c = tid < kShards ? (int32_t)min((unsigned long long)g.act_cap, ish[tid * kShardWords + SH_ACT]) : 0;
+    int32_t incl = c;
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t t = __shfl_up(incl, d);
+      if (lane >= d) incl += t;
     }
-    soff[kShards] = run;
+    if (tid < kShards) soff[tid] = incl - c;
+    if (tid == kShards - 1) soff[kShards] = incl;
   }
   __syncthreads();
   const int64_t n = min((int64_t)soff[kShards], (int64_t)g.act_cap);
-  const int64_t per = (n + 1023) / 1024;
-  const int64_t lo = min((int64_t)tid * per, n), hi = min(lo + per, n);
   // compact the per-shard first-touch lists: active tile j -> tile
   auto tile_of = [&](int64_t j) {
     int s = 0;
     while (s + 1 < kShards && soff[s + 1] <= j) ++s;
     return act_raw[(int64_t)s * g.act_cap + (j - soff[s])];
   };
-  int64_t v[3] = {0, 0, 0};
-  for (int64_t j = lo; j < hi; ++j) {
-    const int32_t t = tile_of(j);
-    act_tiles[j] = t;
-    tile_slot[t] = (int32_t)j;
-    const int64_t c = tile_count[t];
-    v[0] += c;
-    v[1] += (c + kChunk - 1) / kChunk;
-    v[2] += c > kChunk;
+  int64_t carry[3] = {0, 0, 0};
+  for (int64_t base = 0; base < n; base += (int64_t)kPlanThreads * kPlanPer) {
+    const int64_t lo = base + (int64_t)tid * kPlanPer;
+    int32_t t[kPlanPer], c[kPlanPer];
+#pragma unroll
+    for (int q = 0; q < kPlanPer; ++q) t[q] = lo + q < n ? tile_of(lo + q) : -1;
+#pragma unroll
+    for (int q = 0; q < kPlanPer; ++q) c[q] = t[q] >= 0 ? tile_count[t[q]] : 0;
+    int64_t v[3] = {0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < kPlanPer; ++q) {
+      v[0] += c[q];
+      v[1] += (c[q] + kChunk - 1) / kChunk;
+      v[2] += c[q] > kChunk;
+    }
+    int64_t ex[3], tot[3];
+    block_scan3(v, ex, tot, ws);
+    for (int k = 0; k < 3; ++k) ex[k] += carry[k];
+#pragma unroll
+    for (int q = 0; q < kPlanPer; ++q) {
+      if (t[q] < 0) continue;
+      const int64_t j = lo + q;
+      act_tiles[j] = t[q];
+      tile_slot[t[q]] = (int32_t)j;
+      act_off[j] = (int32_t)ex[0];
+      act_cur[j] = (int32_t)ex[0];
+      const int64_t ni = (c[q] + kChunk - 1) / kChunk;
+      const bool heavy = c[q] > kChunk;
+      act_heavy[j] = heavy && ex[2] < g.heavy_cap ? (int32_t)ex[2] : -1;
+      if (heavy && ex[2] < g.heavy_cap) heavy_list[ex[2]] = (int32_t)j;
+      for (int64_t w = 0; w < ni; ++w)
+        if (ex[1] + w < g.item_cap) items[ex[1] + w] = make_int2((int32_t)j, (int32_t)w);
+      ex[0] += c[q];
+      ex[1] += ni;
+      ex[2] += heavy;
+    }
+    for (int k = 0; k < 3; ++k) carry[k] += tot[k];
+    __syncthreads();  // ws is reused by the next round's scan
   }
-  int64_t ex[3], tot[3];
-  block_scan3(v, ex, tot, ws);
   if (tid == 0) {
     cnt[CNT_ACTIVE] = (unsigned long long)n;
-    cnt[CNT_SEGS] = (unsigned long long)tot[0];
-    cnt[CNT_ITEMS] = (unsigned long long)min(tot[1], g.item_cap);
-    cnt[CNT_HEAVY] = (unsigned long long)min(tot[2], g.heavy_cap);
-    if (tot[1] > g.item_cap || tot[2] > g.heavy_cap) atomicOr(&cnt[CNT_OVERFLOW], 8ull);
-  }
-  for (int64_t j = lo; j < hi; ++j) {
-    const int64_t c = tile_count[tile_of(j)];
-    act_off[j] = (int32_t)ex[0];
-    act_cur[j] = (int32_t)ex[0];
-    const int64_t ni = (c + kChunk - 1) / kChunk;
-    const bool heavy = c > kChunk;
-    act_heavy[j] = heavy && ex[2] < g.heavy_cap ? (int32_t)ex[2] : -1;
-    if (heavy && ex[2] < g.heavy_cap) heavy_list[ex[2]] = (int32_t)j;
-    for (int64_t q = 0; q < ni; ++q)
-      if (ex[1] + q < g.item_cap) items[ex[1] + q] = make_int2((int32_t)j, (int32_t)q);
-    ex[0] += c;
-    ex[1] += ni;
-    ex[2] += heavy;
+    cnt[CNT_SEGS] = (unsigned long long)carry[0];
+    cnt[CNT_ITEMS] = (unsigned long long)min(carry[1], g.item_cap);
+    cnt[CNT_HEAVY] = (unsigned long long)min(carry[2], g.heavy_cap);
+    if (carry[1] > g.item_cap || carry[2] > g.heavy_cap) atomicOr(&cnt[CNT_OVERFLOW], 8ull);
   }
 }
 
@@ -694,7 +710,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "plan", &t);
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, g->stream, ge, g->act_raw, g->ish, g->act_tiles,
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(kPlanThreads), 0, g->stream, ge, g->act_raw, g->ish, g->act_tiles,
                      g->tile_slot, g->tile_count, g->act_off, g->act_cur, g->act_heavy,
                      g->heavy_list, g->items, g->cnt);
   dm_timer_end(g, &t);

@@ -35,7 +35,7 @@ enum {
   CNT_U = 1,        // beam-cell updates
   CNT_T = 2,        // touched cells
   CNT_SEGS = 3,     // segments emitted
-  CNT_FTILES = 4,   // tiles visited by the frontier pass
+  CNT_FTILES = 4,   // tiles visited by the frontier pass (tile_free > 0)
   CNT_SLOTS = 5,    // tile-local frontier components
   CNT_CLUSTERS = 6, // output clusters
   CNT_OVERFLOW = 7, // capacity overflow flags
@@ -43,7 +43,9 @@ enum {
   CNT_HEAVY = 9,    // tiles split over several work items
   CNT_TH = 10,      // touched cells applied by k_heavy_apply
   CNT_SORTED = 11,  // 1: out_clu holds the clusters sorted by label
-  CNT_N = 12
+  CNT_FL0 = 12,     // frontier tile-list length, even calls (zeroed by the odd calls)
+  CNT_FL1 = 13,     // frontier tile-list length, odd calls (zeroed by the even calls)
+  CNT_N = 14
 };
 
 // Sharded counters: same-address device atomics serialise at the memory side
@@ -110,9 +112,9 @@ struct dm_grid {
   int32_t last_S = 0, last_N = 0;
 
   // frontier workspace
-  int32_t* ftiles = nullptr;   // list of tiles visited
-  int32_t* fmap = nullptr;     // tile -> index in ftiles or -1
-  int32_t* border = nullptr;   // [ftile][4][64] slot ids
+  int32_t* ftiles = nullptr;   // tiles with free cells (built by k_frontier_prep)
+  int32_t* border = nullptr;   // [tile][4][64] slot ids (listed tiles)
+  int32_t fparity = 0;         // which CNT_FL* counter the last frontier call used
   int64_t border_cap = 0;      // in tiles
   int64_t slot_cap = 0;
   long long* slot_label = nullptr;
