@@ -91,7 +91,7 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   }
   const int64_t segs = nb * per_beam;
   if (segs > g->segs_cap) {
-    int rc = dev_alloc(&g->segs, segs, "segments");
+    int rc = dev_alloc(&g->pieces, segs, "ray pieces");
     if (rc) return rc;
     g->segs_cap = segs;
   }
@@ -101,20 +101,20 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   if (act > g->act_cap) {
     int rc = dev_alloc(&g->act_tiles, act, "active tiles");
     if (!rc) rc = dev_alloc(&g->act_raw, act * kShards, "first-touch lists");
-    if (!rc) rc = dev_alloc(&g->act_off, act, "active offsets");
     if (!rc) rc = dev_alloc(&g->act_cur, act, "active cursors");
+    if (!rc) rc = dev_alloc(&g->litems, act, "light work items");
     if (rc) return rc;
     g->act_cap = act;
-    if ((rc = dev_alloc(&g->act_heavy, act, "heavy map"))) return rc;
   }
-  // work items / heavy tiles of the apply phase (exact bounds, see k_plan)
+  // heavy work items / heavy tiles (exact bounds: a heavy tile has > 256
+  // pieces, its items ceil(pieces / 256) <= pieces / 256 + 1)
   const int64_t chunk = 256;
   const int64_t heavy = std::max<int64_t>(1, std::min<int64_t>(g->act_cap, segs / (chunk + 1) + 1));
-  const int64_t items = segs / chunk + g->act_cap + 1;
-  if (items > g->item_cap) {
-    int rc = dev_alloc(&g->items, items, "apply work items");
+  const int64_t hitems = segs / chunk + heavy + 1;
+  if (hitems > g->hitem_cap) {
+    int rc = dev_alloc(&g->hitems, hitems, "heavy work items");
     if (rc) return rc;
-    g->item_cap = items;
+    g->hitem_cap = hitems;
   }
   if (heavy > g->heavy_cap) {
     int rc = dev_alloc(&g->heavy_list, heavy, "heavy tiles");
@@ -386,9 +386,9 @@ int dm_destroy(dm_grid* g) {
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
   dev_free(g->L); dev_free(g->state); dev_free(g->tile_count); dev_free(g->tile_slot);
-  dev_free(g->tile_free); dev_free(g->cnt); dev_free(g->beams); dev_free(g->segs);
-  dev_free(g->act_tiles); dev_free(g->act_off); dev_free(g->act_cur); dev_free(g->trig);
-  dev_free(g->act_heavy); dev_free(g->heavy_list); dev_free(g->items); dev_free(g->slabs);
+  dev_free(g->tile_free); dev_free(g->cnt); dev_free(g->beams); dev_free(g->pieces);
+  dev_free(g->act_tiles); dev_free(g->act_cur); dev_free(g->trig);
+  dev_free(g->hitems); dev_free(g->litems); dev_free(g->heavy_list); dev_free(g->slabs);
   dev_free(g->pose4); dev_free(g->ranges); 
   dev_free(g->border); dev_free(g->ftiles); dev_free(g->slot_label); dev_free(g->slot_parent); dev_free(g->slot_root);
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
@@ -502,9 +502,10 @@ int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out) {
   DM_HIP(dm_copy_shards(g));
   DM_HIP(hipStreamSynchronize(g->stream));
   const unsigned long long* fs = g->h_sh + kShards * kShardWords;
+  const uint64_t items = g->h_cnt[CNT_ITEMS] + g->h_cnt[CNT_LITEMS];  // heavy + light work items
   const uint64_t v[10] = {dm_shard_sum(g->h_sh, SH_U),  dm_shard_sum(g->h_sh, SH_T),
                           dm_shard_sum(g->h_sh, SH_TH), g->h_cnt[CNT_SEGS],
-                          g->h_cnt[CNT_ACTIVE],         g->h_cnt[CNT_ITEMS],
+                          g->h_cnt[CNT_ACTIVE],         items,
                           g->h_cnt[CNT_HEAVY],          g->h_cnt[g->fparity ? CNT_FL1 : CNT_FL0],
                           dm_shard_sum(fs, SH_SLOT),    g->h_cnt[CNT_CLUSTERS]};
   for (int32_t i = 0; i < cap && i < 10; ++i) out[i] = v[i];

@@ -22,8 +22,11 @@
 //   k_frontier_resolve / k_frontier_compact  roots, int64 sums, cluster list
 #include "dm_internal.h"
 #include "dm_uf.h"
+#include "dm_phase.h"
 
 #include <algorithm>
+
+DM_PH_DECL(frontier)
 
 namespace {
 
@@ -156,9 +159,11 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
   __shared__ long long sbase;
   const int tid = threadIdx.x, lane = __lane_id();
   const int64_t nft = (int64_t)*list_n;
+  DM_PH_INIT();
   for (int64_t jj = blockIdx.x; jj < nft; jj += gridDim.x) {
     const int32_t tile = ftiles[jj];
     const int64_t j = tile;  // border records are indexed by tile
+    DM_PH_COUNT(dm_phase_acc_frontier, 16, 1);
     const int32_t tx0 = (tile % g.TX) * DM_TS;
     const int32_t ty0 = (tile / g.TX) * DM_TS;  // band-local
     // ---- 1. bit rows ------------------------------------------------------
@@ -216,6 +221,7 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
       }
     }
     __syncthreads();
+    DM_PH(dm_phase_acc_frontier, 0);
     // ---- 2. frontier bits + runs -------------------------------------------
     int any = 0;
     if (tid < DM_TS) {
@@ -241,9 +247,11 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
       if (y == 63) s_rbase[DM_TS] = incl;
     }
     any = __syncthreads_or(any);
+    DM_PH(dm_phase_acc_frontier, 1);
     if (!any) {
       border[j * 256 + tid] = -1;
       __syncthreads();
+      DM_PH(dm_phase_acc_frontier, 8);
       continue;
     }
     if (tid < DM_TS) {  // enumerate runs of row tid
@@ -267,6 +275,9 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
     for (int r = tid; r < kMaxRoots; r += kFT) { ssz[r] = 0; ssx[r] = 0; ssy[r] = 0; }
     __syncthreads();
     const int nruns = s_rbase[DM_TS];
+    DM_PH(dm_phase_acc_frontier, 2);
+    DM_PH_COUNT(dm_phase_acc_frontier, 17, nruns);
+    DM_PH_COUNT(dm_phase_acc_frontier, 18, 1);
     // ---- 3. union with overlapping runs of the row above ---------------------
     for (int r = tid; r < nruns; r += kFT) {
       const int y = r_y[r];
@@ -285,8 +296,10 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
       }
     }
     __syncthreads();
+    DM_PH(dm_phase_acc_frontier, 3);
     for (int r = tid; r < nruns; r += kFT) r_par[r] = lds_find(r_par, r);
     __syncthreads();
+    DM_PH(dm_phase_acc_frontier, 4);
     // ---- 4. components, sums, slots ------------------------------------------
     for (int r = tid; r < nruns; r += kFT) {
       if (r_par[r] == r) {
@@ -296,6 +309,7 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
       }
     }
     __syncthreads();
+    DM_PH(dm_phase_acc_frontier, 5);
     // slots come from this workgroup's shard region [shard*slot_per, +slot_per)
     if (tid == 0)
       sbase = (long long)atomicAdd(&fsh[(blockIdx.x % kShards) * kShardWords + SH_SLOT],
@@ -308,6 +322,7 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
       atomicAdd(&ssy[c], (uint32_t)r_y[r] * len);
     }
     __syncthreads();
+    DM_PH(dm_phase_acc_frontier, 6);
     const long long base = sbase;
     const long long sh0 = (long long)(blockIdx.x % kShards) * g.slot_per;
     const int nr = nroots;
@@ -362,7 +377,9 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
       }
     }
     __syncthreads();
+    DM_PH(dm_phase_acc_frontier, 7);
   }
+  DM_PH_FLUSH(dm_phase_acc_frontier);
 }
 
 // Unions across tile borders.  Consecutive border cells of a frontier that
@@ -613,6 +630,8 @@ static FGeom make_fgeom(const dm_grid* g, bool want_mask, bool want_labels) {
   fg.min_size = g->p.min_frontier_size;
   return fg;
 }
+
+DM_PH_READER(frontier)
 
 int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const unsigned long long* d_count,
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,

@@ -22,18 +22,20 @@
 //   k_tile_apply  one workgroup per active tile (grid-stride): LDS counts +
 //                 fused apply, tile summaries, counter reset
 #include "dm_internal.h"
+#include "dm_phase.h"
+
+#include <algorithm>
+
+DM_PH_DECL(integrate)
 
 namespace {
 
-constexpr int kApplyThreads = 256;
 constexpr int kLdsPitch = DM_TS + 1;  // +1 dword: y-major pieces hit distinct banks
 
 struct Geom {
   RayGeom r;
   int32_t act_cap;
   int64_t seg_cap;
-  int64_t item_cap;
-  int64_t heavy_cap;
   int64_t nb;  // beams in this call
 };
 
@@ -153,34 +155,44 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
   }
 }
 
-// Work plan for the apply phase (one block).  Per active tile j with c_j
-// pieces: exclusive scans of c_j (bin offsets), of ceil(c_j / kChunk) (work
-// items) and of [c_j > kChunk] (heavy-tile ordinals).  A light tile is one
-// work item that accumulates AND applies; a heavy tile's pieces are split
-// into kChunk-piece items on different CUs that merge their counts in a
-// per-tile slab, applied by k_heavy_apply.
+// Work plan for the apply phase (one block).  A tile's pieces are cut into
+// work items of at most kChunk (= one per thread of a 256-thread workgroup).
+// A light tile (<= kChunk pieces) is one item that accumulates AND applies;
+// a heavy tile (around a sensor: up to every beam of a scan starts there) is
+// split into several items on different CUs that merge their counts in a
+// per-tile slab, applied by k_heavy_apply.  Per active tile j with c_j
+// pieces, exclusive scans of: c_j (bin offsets), heavy items, light items,
+// heavy ordinals.  Heavy items are listed first (they are the long ones).
+// Item = {tile, first piece, pieces, heavy ordinal or -1}.
 constexpr int kChunk = 256;
+constexpr int kTileWords = DM_TS * kLdsPitch;
+constexpr int kQuarter = 256;  // threads of an apply workgroup (= kChunk)
 static_assert(kChunk < 65536, "packed 16-bit LDS counts");
+static_assert(kChunk == kQuarter, "one piece per thread");
 
-__device__ inline void block_scan3(int64_t v[3], int64_t excl[3], int64_t tot[3], int64_t (*ws)[3]) {
+template <int K>
+__device__ inline void block_scan(const int64_t (&v)[K], int64_t (&excl)[K], int64_t (&tot)[K],
+                                  int64_t (*ws)[K]) {
   const int tid = threadIdx.x, lane = __lane_id(), wid = tid >> 6;
-  int64_t incl[3] = {v[0], v[1], v[2]};
+  int64_t incl[K];
+  for (int q = 0; q < K; ++q) incl[q] = v[q];
   for (int d = 1; d < 64; d <<= 1) {
-    for (int q = 0; q < 3; ++q) {
+    for (int q = 0; q < K; ++q) {
       const int64_t t = __shfl_up(incl[q], d);
       if (lane >= d) incl[q] += t;
     }
   }
-  if (lane == 63) for (int q = 0; q < 3; ++q) ws[wid][q] = incl[q];
+  if (lane == 63) for (int q = 0; q < K; ++q) ws[wid][q] = incl[q];
   __syncthreads();
   if (tid == 0) {
-    int64_t run[3] = {0, 0, 0};
+    int64_t run[K];
+    for (int q = 0; q < K; ++q) run[q] = 0;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w)
-      for (int q = 0; q < 3; ++q) { const int64_t t = ws[w][q]; ws[w][q] = run[q]; run[q] += t; }
-    for (int q = 0; q < 3; ++q) ws[16][q] = run[q];
+      for (int q = 0; q < K; ++q) { const int64_t t = ws[w][q]; ws[w][q] = run[q]; run[q] += t; }
+    for (int q = 0; q < K; ++q) ws[16][q] = run[q];
   }
   __syncthreads();
-  for (int q = 0; q < 3; ++q) {
+  for (int q = 0; q < K; ++q) {
     excl[q] = ws[wid][q] + incl[q] - v[q];
     tot[q] = ws[16][q];
   }
@@ -193,11 +205,11 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __
                                                        const unsigned long long* __restrict__ ish,
                                                        int32_t* __restrict__ act_tiles, int32_t* __restrict__ tile_slot,
                                                        const int32_t* __restrict__ tile_count,
-                                                       int32_t* __restrict__ act_off, int32_t* __restrict__ act_cur,
-                                                       int32_t* __restrict__ act_heavy,
+                                                       int32_t* __restrict__ act_cur,
+                                                       int4* __restrict__ hitems, int4* __restrict__ litems,
                                                        int32_t* __restrict__ heavy_list,
-                                                       int2* __restrict__ items, unsigned long long* cnt) {
-  __shared__ int64_t ws[17][3];
+                                                       unsigned long long* cnt) {
+  __shared__ int64_t ws[17][4];
   __shared__ int32_t soff[kShards + 1];
   const int tid = threadIdx.x, lane = __lane_id();
   if (tid < 64) {  // shard offsets: one wave, one load per lane, shuffle scan
@@ -212,68 +224,79 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __
   }
   __syncthreads();
   const int64_t n = min((int64_t)soff[kShards], (int64_t)g.act_cap);
-  // compact the per-shard first-touch lists: active tile j -> tile
-  auto tile_of = [&](int64_t j) {
-    int s = 0;
-    while (s + 1 < kShards && soff[s + 1] <= j) ++s;
-    return act_raw[(int64_t)s * g.act_cap + (j - soff[s])];
-  };
-  int64_t carry[3] = {0, 0, 0};
+  // compact the per-shard first-touch lists: active tile j -> tile.  The
+  // shard of a thread's first j by binary search over the offsets (LDS
+  // reads are dependent: 5 steps, not a 32-step scan), then incrementally.
+  int64_t carry[4] = {0, 0, 0, 0};
   for (int64_t base = 0; base < n; base += (int64_t)kPlanThreads * kPlanPer) {
     const int64_t lo = base + (int64_t)tid * kPlanPer;
+    int sh = 0;
+    {
+      int a = 0, b = kShards - 1;  // largest shard with soff[shard] <= lo
+      while (a < b) {
+        const int mid = (a + b + 1) >> 1;
+        if (soff[mid] <= lo) a = mid; else b = mid - 1;
+      }
+      sh = a;
+    }
     int32_t t[kPlanPer], c[kPlanPer];
 #pragma unroll
-    for (int q = 0; q < kPlanPer; ++q) t[q] = lo + q < n ? tile_of(lo + q) : -1;
+    for (int q = 0; q < kPlanPer; ++q) {
+      const int64_t j = lo + q;
+      while (sh + 1 < kShards && soff[sh + 1] <= j) ++sh;
+      t[q] = j < n ? act_raw[(int64_t)sh * g.act_cap + (j - soff[sh])] : -1;
+    }
 #pragma unroll
     for (int q = 0; q < kPlanPer; ++q) c[q] = t[q] >= 0 ? tile_count[t[q]] : 0;
-    int64_t v[3] = {0, 0, 0};
+    int64_t v[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int q = 0; q < kPlanPer; ++q) {
+      const bool heavy = c[q] > kChunk;
       v[0] += c[q];
-      v[1] += (c[q] + kChunk - 1) / kChunk;
-      v[2] += c[q] > kChunk;
+      v[1] += heavy ? (c[q] + kChunk - 1) / kChunk : 0;
+      v[2] += (t[q] >= 0 && !heavy) ? 1 : 0;
+      v[3] += heavy ? 1 : 0;
     }
-    int64_t ex[3], tot[3];
-    block_scan3(v, ex, tot, ws);
-    for (int k = 0; k < 3; ++k) ex[k] += carry[k];
+    int64_t ex[4], tot[4];
+    block_scan<4>(v, ex, tot, ws);
+    for (int k = 0; k < 4; ++k) ex[k] += carry[k];
 #pragma unroll
     for (int q = 0; q < kPlanPer; ++q) {
       if (t[q] < 0) continue;
       const int64_t j = lo + q;
       act_tiles[j] = t[q];
       tile_slot[t[q]] = (int32_t)j;
-      act_off[j] = (int32_t)ex[0];
       act_cur[j] = (int32_t)ex[0];
-      const int64_t ni = (c[q] + kChunk - 1) / kChunk;
-      const bool heavy = c[q] > kChunk;
-      act_heavy[j] = heavy && ex[2] < g.heavy_cap ? (int32_t)ex[2] : -1;
-      if (heavy && ex[2] < g.heavy_cap) heavy_list[ex[2]] = (int32_t)j;
-      for (int64_t w = 0; w < ni; ++w)
-        if (ex[1] + w < g.item_cap) items[ex[1] + w] = make_int2((int32_t)j, (int32_t)w);
+      if (c[q] > kChunk) {
+        heavy_list[ex[3]] = t[q];
+        for (int32_t p0 = 0; p0 < c[q]; p0 += kChunk)
+          hitems[ex[1]++] = make_int4(t[q], (int32_t)ex[0] + p0, min(kChunk, c[q] - p0), (int32_t)ex[3]);
+        ++ex[3];
+      } else {
+        litems[ex[2]++] = make_int4(t[q], (int32_t)ex[0], c[q], -1);
+      }
       ex[0] += c[q];
-      ex[1] += ni;
-      ex[2] += heavy;
     }
-    for (int k = 0; k < 3; ++k) carry[k] += tot[k];
+    for (int k = 0; k < 4; ++k) carry[k] += tot[k];
     __syncthreads();  // ws is reused by the next round's scan
   }
   if (tid == 0) {
     cnt[CNT_ACTIVE] = (unsigned long long)n;
     cnt[CNT_SEGS] = (unsigned long long)carry[0];
-    cnt[CNT_ITEMS] = (unsigned long long)min(carry[1], g.item_cap);
-    cnt[CNT_HEAVY] = (unsigned long long)min(carry[2], g.heavy_cap);
-    if (carry[1] > g.item_cap || carry[2] > g.heavy_cap) atomicOr(&cnt[CNT_OVERFLOW], 8ull);
+    cnt[CNT_ITEMS] = (unsigned long long)carry[1];   // heavy items
+    cnt[CNT_LITEMS] = (unsigned long long)carry[2];  // light items (= light tiles)
+    cnt[CNT_HEAVY] = (unsigned long long)carry[3];   // heavy tiles
   }
 }
 
-__device__ inline void put_seg(const Geom& g, Seg* segs, int64_t idx, int64_t b, int32_t k0,
-                               int32_t k1, unsigned long long* cnt) {
+// A piece as k_tile_accum consumes it: tile-local LDS addresses (pitch
+// kLdsPitch), packed to 16 bytes (dm_ray.h).
+__device__ inline void put_piece(const Geom& g, PackedPiece* pieces, int64_t idx, const Beam& bm,
+                                 int32_t tile, int32_t k0, int32_t k1, unsigned long long* cnt) {
   if (idx >= 0 && idx < g.seg_cap) {
-    Seg sg;
-    sg.beam = (uint32_t)b;
-    sg.k0 = (uint16_t)k0;
-    sg.k1 = (uint16_t)k1;
-    segs[idx] = sg;
+    const int32_t tx0 = (tile % g.r.TX) * DM_TS;
+    const int32_t ty0 = (tile / g.r.TX) * DM_TS;
+    pieces[idx] = dm_pack_piece(dm_tile_piece(bm, k0, k1, g.r.row0, tx0, ty0, kLdsPitch));
   } else {
     atomicOr(&cnt[CNT_OVERFLOW], 2ull);
   }
@@ -283,7 +306,7 @@ __device__ inline void put_seg(const Geom& g, Seg* segs, int64_t idx, int64_t b,
 // cursor bump per (block, tile), then LDS cursors place each piece.
 __global__ __launch_bounds__(256) void k_scatter(RayArgs a, Geom g, const Beam* __restrict__ beams,
                                                  const int32_t* __restrict__ tile_slot,
-                                                 int32_t* act_cur, Seg* __restrict__ segs,
+                                                 int32_t* act_cur, PackedPiece* __restrict__ pieces,
                                                  unsigned long long* cnt) {
   __shared__ int32_t hkey[kHash];
   __shared__ int32_t hcnt[kHash];
@@ -313,7 +336,7 @@ __global__ __launch_bounds__(256) void k_scatter(RayArgs a, Geom g, const Beam* 
       }
       h = __shfl(h, run.head_lane);
       base = __shfl(base, run.head_lane);
-      if (h < 0) put_seg(g, segs, base >= 0 ? (int64_t)base + run.rank : -1, b, k0, k1, cnt);
+      if (h < 0) put_piece(g, pieces, base >= 0 ? (int64_t)base + run.rank : -1, bm, tile, k0, k1, cnt);
     });
   }
   __syncthreads();
@@ -337,7 +360,7 @@ __global__ __launch_bounds__(256) void k_scatter(RayArgs a, Geom g, const Beam* 
       h = __shfl(h, run.head_lane);
       pos = __shfl(pos, run.head_lane);
       if (h < 0) return;  // placed by the global path above
-      put_seg(g, segs, pos >= 0 ? (int64_t)pos + run.rank : -1, b, k0, k1, cnt);
+      put_piece(g, pieces, pos >= 0 ? (int64_t)pos + run.rank : -1, bm, tile, k0, k1, cnt);
     });
   }
 }
@@ -364,232 +387,251 @@ __device__ inline float apply_one(const ApplyArgs& p, float L, uint32_t h, uint3
   return L;
 }
 
-// Log-odds update of one tile from per-cell counts (SPEC a6/a7): thread ->
-// 4 consecutive cells of a row (float4 / char4 accesses), 16 threads per row.
-// counts(ly, cx, h4, m4) supplies the counts.  Adds to *sh_T / *sh_free.
-template <class Counts>
-__device__ inline void apply_tile(const Geom& g, const ApplyArgs& p, int32_t tx0, int32_t ty0,
-                                  float* __restrict__ L, int8_t* __restrict__ state, int vec_ok,
-                                  Counts&& counts, int32_t* sh_T, int32_t* sh_free, uint32_t* sh_U) {
-  constexpr int kRows = DM_TS / 16;
-  const int tid = threadIdx.x;
-  int32_t dT = 0, dFree = 0;
-  uint32_t dU = 0;
-  const int cx = (tid & 15) * 4;
-  uint32_t h4[kRows][4], m4[kRows][4];
-  bool any[kRows];
-  int64_t base[kRows];
+// Cells of one tile owned by one thread: 4 consecutive cells (float4 / char4)
+// of ROWS rows ly0, ly0 + dly, ...  Their L / state are loaded BEFORE the
+// pieces are accumulated (they do not depend on the counts), so the apply
+// step finds them in registers: one memory latency hidden behind the
+// accumulation instead of one exposed after it.
+template <int ROWS>
+struct CellRows {
+  float4 l[ROWS];
+  char4 s[ROWS];
+  bool vec;
+
+  __device__ void prefetch(const Geom& g, int32_t tx0, int32_t ty0, int ly0, int dly, int cx,
+                           const float* __restrict__ L, const int8_t* __restrict__ state, int vec_ok) {
+    vec = vec_ok && tx0 + cx + 4 <= g.r.W;
+    if (!vec) return;
 #pragma unroll
-  for (int rr = 0; rr < kRows; ++rr) {
-    const int ly = (tid >> 4) + 16 * rr;
-    counts(ly, cx, h4[rr], m4[rr]);
-    any[rr] = (ty0 + ly < g.r.R) &&
-              ((h4[rr][0] | m4[rr][0]) | (h4[rr][1] | m4[rr][1]) | (h4[rr][2] | m4[rr][2]) |
-               (h4[rr][3] | m4[rr][3])) != 0u;
-    base[rr] = (int64_t)(ty0 + ly) * g.r.W + tx0 + cx;
-  }
-  const bool vec = vec_ok && tx0 + cx + 4 <= g.r.W;
-  if (vec) {
-    // issue every row's loads before the first use: one memory latency
-    float4 l4[kRows];
-    char4 s4[kRows];
-#pragma unroll
-    for (int rr = 0; rr < kRows; ++rr) {
-      if (any[rr]) {
-        l4[rr] = *reinterpret_cast<const float4*>(L + base[rr]);
-        s4[rr] = *reinterpret_cast<const char4*>(state + base[rr]);
-      }
-    }
-#pragma unroll
-    for (int rr = 0; rr < kRows; ++rr) {
-      if (!any[rr]) continue;
-      float lv[4] = {l4[rr].x, l4[rr].y, l4[rr].z, l4[rr].w};
-      int8_t sv[4] = {(int8_t)s4[rr].x, (int8_t)s4[rr].y, (int8_t)s4[rr].z, (int8_t)s4[rr].w};
-      for (int e = 0; e < 4; ++e) {
-        if ((h4[rr][e] | m4[rr][e]) == 0u) continue;
-        dU += h4[rr][e] + m4[rr][e];
-        const int8_t old = sv[e];
-        lv[e] = apply_one(p, lv[e], h4[rr][e], m4[rr][e]);
-        sv[e] = state_of(p, lv[e]);
-        dT += 1;
-        dFree += (sv[e] == 0) - (old == 0);
-      }
-      *reinterpret_cast<float4*>(L + base[rr]) = make_float4(lv[0], lv[1], lv[2], lv[3]);
-      *reinterpret_cast<char4*>(state + base[rr]) = make_char4(sv[0], sv[1], sv[2], sv[3]);
-    }
-  } else {
-    for (int rr = 0; rr < kRows; ++rr) {
-      if (!any[rr]) continue;
-      for (int e = 0; e < 4; ++e) {
-        if ((h4[rr][e] | m4[rr][e]) == 0u) continue;
-        if (tx0 + cx + e >= g.r.W) continue;
-        dU += h4[rr][e] + m4[rr][e];
-        const int64_t i = base[rr] + e;
-        const int8_t old = state[i];
-        const float nl = apply_one(p, L[i], h4[rr][e], m4[rr][e]);
-        const int8_t ns = state_of(p, nl);
-        L[i] = nl;
-        state[i] = ns;
-        dT += 1;
-        dFree += (ns == 0) - (old == 0);
+    for (int rr = 0; rr < ROWS; ++rr) {
+      const int32_t y = ty0 + ly0 + rr * dly;
+      if (y < g.r.R) {
+        const int64_t base = (int64_t)y * g.r.W + tx0 + cx;
+        l[rr] = *reinterpret_cast<const float4*>(L + base);
+        s[rr] = *reinterpret_cast<const char4*>(state + base);
       }
     }
   }
-  if (dT) atomicAdd(sh_T, dT);
-  if (dFree) atomicAdd(sh_free, dFree);
-  if (dU) atomicAdd(sh_U, dU);
+
+  // counts(ly, h4, m4) supplies the counts of this thread's 4 cells of row ly
+  template <class Counts>
+  __device__ void apply(const Geom& g, const ApplyArgs& p, int32_t tx0, int32_t ty0, int ly0, int dly,
+                        int cx, float* __restrict__ L, int8_t* __restrict__ state, Counts&& counts,
+                        int32_t* sh_T, int32_t* sh_free, uint32_t* sh_U) {
+    int32_t dT = 0, dFree = 0;
+    uint32_t dU = 0;
+#pragma unroll
+    for (int rr = 0; rr < ROWS; ++rr) {
+      const int ly = ly0 + rr * dly;
+      const int32_t y = ty0 + ly;
+      if (y >= g.r.R) continue;
+      uint32_t h4[4], m4[4];
+      counts(ly, h4, m4);
+      if (((h4[0] | m4[0]) | (h4[1] | m4[1]) | (h4[2] | m4[2]) | (h4[3] | m4[3])) == 0u) continue;
+      const int64_t base = (int64_t)y * g.r.W + tx0 + cx;
+      if (vec) {
+        float lv[4] = {l[rr].x, l[rr].y, l[rr].z, l[rr].w};
+        int8_t sv[4] = {(int8_t)s[rr].x, (int8_t)s[rr].y, (int8_t)s[rr].z, (int8_t)s[rr].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if ((h4[e] | m4[e]) == 0u) continue;
+          dU += h4[e] + m4[e];
+          const int8_t old = sv[e];
+          lv[e] = apply_one(p, lv[e], h4[e], m4[e]);
+          sv[e] = state_of(p, lv[e]);
+          dT += 1;
+          dFree += (sv[e] == 0) - (old == 0);
+        }
+        *reinterpret_cast<float4*>(L + base) = make_float4(lv[0], lv[1], lv[2], lv[3]);
+        *reinterpret_cast<char4*>(state + base) = make_char4(sv[0], sv[1], sv[2], sv[3]);
+      } else {
+        for (int e = 0; e < 4; ++e) {
+          if ((h4[e] | m4[e]) == 0u || tx0 + cx + e >= g.r.W) continue;
+          dU += h4[e] + m4[e];
+          const int64_t i = base + e;
+          const int8_t old = state[i];
+          const float nl = apply_one(p, L[i], h4[e], m4[e]);
+          const int8_t ns = state_of(p, nl);
+          L[i] = nl;
+          state[i] = ns;
+          dT += 1;
+          dFree += (ns == 0) - (old == 0);
+        }
+      }
+    }
+    if (dT) atomicAdd(sh_T, dT);
+    if (dFree) atomicAdd(sh_free, dFree);
+    if (dU) atomicAdd(sh_U, dU);
+  }
+};
+
+__device__ inline PackedPiece no_piece() {
+  PackedPiece q;
+  q.x = 0u; q.y = 0u; q.z = 0u; q.w = 1u;
+  return q;
 }
 
-// One work item = up to kChunk (= 256) pieces of one tile.  Each piece is
-// turned into tile-local LDS addresses once (dm_tile_piece: one division per
-// piece) and then walked without divisions or bounds checks (every cell of a
-// piece lies in its tile).  Counts go to a packed LDS tile (hits << 16 |
-// misses): every cell adds 1, the hit cell of a beam then adds 0xFFFF, which
-// turns that miss into a hit (an item's 256 pieces visit a cell at most 256
-// times, so the miss half never carries on its own).  U is counted by the
-// apply step over in-grid cells.
-//  * light tile (one item): one piece per lane, incremental PieceCursor walk;
-//    the counts are applied to L / state right away;
-//  * heavy tile (around a sensor, > kChunk pieces): the pieces converge on
-//    the same cells, so each wave takes one piece at a time with one lane per
-//    cell (distinct cells: conflict-free LDS atomics) and the item's counts
-//    are added to the tile's slab with row-contiguous global atomics.
-__global__ __launch_bounds__(kApplyThreads) void k_tile_accum(
-    Geom g, ApplyArgs p, const int2* __restrict__ items, const int32_t* __restrict__ act_tiles,
-    const int32_t* __restrict__ act_off, const int32_t* __restrict__ act_heavy,
-    const Seg* __restrict__ segs, const Beam* __restrict__ beams, int32_t* tile_count,
-    int32_t* tile_free, uint32_t* __restrict__ slabs, float* __restrict__ L,
-    int8_t* __restrict__ state, unsigned long long* cnt, unsigned long long* ish, int vec_ok) {
-  __shared__ uint32_t cnt16[DM_TS * kLdsPitch];
-  __shared__ TilePiece s_tp[kChunk];
-  __shared__ float s_rcp[kChunk];
-  __shared__ int32_t sh_free, sh_T;
-  __shared__ uint32_t sh_U;
-  const int tid = threadIdx.x, lane = lane_id();
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t n_items = (int64_t)cnt[CNT_ITEMS];
+__device__ inline void finish_tile(const Geom& g, int32_t tile, int32_t T, int32_t dfree, uint32_t U,
+                                   bool heavy, int32_t* tile_count, int32_t* tile_free,
+                                   unsigned long long* ish) {
+  unsigned long long* sh = ish + (blockIdx.x % kShards) * kShardWords;
+  if (T) {
+    atomicAdd(&sh[SH_T], (unsigned long long)T);
+    if (heavy) atomicAdd(&sh[SH_TH], (unsigned long long)T);
+  }
+  if (U) atomicAdd(&sh[SH_U], (unsigned long long)U);
+  if (dfree) atomicAdd(&tile_free[tile], dfree);  // no returned value: nothing to wait for
+  tile_count[tile] = 0;                            // ready for the next call
+}
+
+// Per-cell hit/miss counts never touch HBM: a 256-thread workgroup takes one
+// work item (<= kChunk pieces of one tile, one piece per thread), gathers
+// them in a packed LDS count tile (hits << 16 | misses) with wave_pieces,
+// and then
+//  * light item (the whole tile): applies the log-odds update to the tile's
+//    cells right away, from L / state loaded before the accumulation;
+//  * heavy item: adds its counts to the tile's slab (row-contiguous global
+//    atomics); k_heavy_apply applies the merged slab.
+// The next item's descriptor is loaded while the current one is processed.
+__global__ __launch_bounds__(kQuarter) void k_tile_accum(
+    Geom g, ApplyArgs p, const int4* __restrict__ hitems, const int4* __restrict__ litems,
+    const PackedPiece* __restrict__ pieces, int32_t* tile_count, int32_t* tile_free,
+    uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
+    const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok) {
+  __shared__ uint32_t tl[kTileWords];
+  __shared__ PackedPiece s_pp[kChunk];
+  __shared__ int32_t s_T, s_free;
+  __shared__ uint32_t s_U;
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const int64_t HI = (int64_t)cnt[CNT_ITEMS], LI = (int64_t)cnt[CNT_LITEMS];
+  const int64_t n_items = HI + LI;
+  auto item_of = [&](int64_t it) { return it < HI ? hitems[it] : litems[it - HI]; };
+  int4 next = make_int4(0, 0, 0, -1);
+  if ((int64_t)blockIdx.x < n_items) next = item_of(blockIdx.x);
+  DM_PH_INIT();
   for (int64_t it = blockIdx.x; it < n_items; it += gridDim.x) {
-    const int2 item = items[it];
-    const int32_t j = item.x;
-    const int32_t tile = act_tiles[j];
-    const int32_t count = tile_count[tile];
-    const int32_t heavy = act_heavy[j];
-    const int32_t c0 = act_off[j] + item.y * kChunk;
-    const int32_t nseg = min(kChunk, act_off[j] + count - c0);
-    const int32_t tx0 = (tile % g.r.TX) * DM_TS;
-    const int32_t ty0 = (tile / g.r.TX) * DM_TS;  // band-local
-    for (int e = tid; e < DM_TS * kLdsPitch; e += kApplyThreads) cnt16[e] = 0u;
-    if (tid == 0) { sh_free = 0; sh_T = 0; sh_U = 0u; }
-    // this thread's piece
-    TilePiece tp;
-    tp.addr0 = 0; tp.addr_end = -1; tp.len = 0; tp.da = tp.db = 0;
-    tp.rem0 = 0; tp.two_adb = 0; tp.two_n = 1;
-    if (tid < nseg) {
-      const Seg sg = segs[c0 + tid];
-      if ((int64_t)sg.beam < g.nb) {
-        const Beam bm = beams[sg.beam];
-        if (bm.flags & 1) tp = dm_tile_piece(bm, sg.k0, sg.k1, g.r.row0, tx0, ty0, kLdsPitch);
-      }
-    }
+    const int4 info = next;
+    if (it + gridDim.x < n_items) next = item_of(it + gridDim.x);
+    // the descriptor is workgroup-uniform: scalar registers, scalar branches
+    const int32_t tile = __builtin_amdgcn_readfirstlane(info.x);
+    const int32_t c0 = __builtin_amdgcn_readfirstlane(info.y);
+    const int32_t c = __builtin_amdgcn_readfirstlane(info.z);
+    const int32_t heavy = __builtin_amdgcn_readfirstlane(info.w);
+    const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
+    PackedPiece mine = no_piece();
+    if (tid < c) mine = pieces[c0 + tid];
+    CellRows<4> cells;
+    const int cx = (tid & 15) * 4;
+    if (heavy < 0) cells.prefetch(g, tx0, ty0, tid >> 4, 16, cx, L, state, vec_ok);
+    for (int e = tid; e < kTileWords; e += kQuarter) tl[e] = 0u;
+    if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; }
+    __syncthreads();
+    DM_PH(dm_phase_acc_integrate, 0);
     if (heavy >= 0) {
-      if (tid < nseg) {
-        s_tp[tid] = tp;
-        s_rcp[tid] = __builtin_amdgcn_rcpf((float)tp.two_n);
-      }
+      // heavy: the pieces converge on the sensor's cells, so a wave takes
+      // one piece at a time with one lane per cell (distinct cells:
+      // conflict-free LDS atomics); pieces are broadcast from LDS
+      s_pp[tid] = mine;
       __syncthreads();
-      for (int si = wid; si < nseg; si += kApplyThreads / 64) {
-        const TilePiece q = s_tp[si];
-        if (lane < q.len) {
-          const int32_t a = dm_piece_addr(q, lane, s_rcp[si]);
-          atomicAdd(&cnt16[a], (lane == q.len - 1 && q.addr_end >= 0) ? 0x10000u : 1u);
+      for (int si = w; si < c; si += kQuarter / 64) {
+        const PackedPiece q = s_pp[si];
+        const TilePiece tp = dm_unpack_piece(q.x, q.y, q.z, q.w);
+        if (lane < tp.len) {
+          const int32_t a = dm_piece_addr(tp, lane, __builtin_amdgcn_rcpf((float)tp.two_n));
+          atomicAdd(&tl[a], (lane == tp.len - 1 && tp.addr_end >= 0) ? 0x10000u : 1u);
         }
       }
       __syncthreads();
+      DM_PH(dm_phase_acc_integrate, 1);
+      DM_PH_COUNT(dm_phase_acc_integrate, 17, 1);
+      DM_PH_COUNT(dm_phase_acc_integrate, 19, c);
       uint32_t* sh = slabs + (int64_t)heavy * (2 * DM_TS * DM_TS);
-      for (int e = tid; e < DM_TS * DM_TS; e += kApplyThreads) {
-        const int ly = e >> 6, lx = e & 63;
-        const uint32_t v = cnt16[ly * kLdsPitch + lx];
+      for (int e = tid; e < DM_TS * DM_TS; e += kQuarter) {
+        const uint32_t v = tl[(e >> 6) * kLdsPitch + (e & 63)];
         const uint32_t h = v >> 16, m = v & 0xFFFFu;
         if (h) atomicAdd(&sh[e], h);
         if (m) atomicAdd(&sh[DM_TS * DM_TS + e], m);
       }
       __syncthreads();
+      DM_PH(dm_phase_acc_integrate, 2);
       continue;
     }
-    __syncthreads();  // cnt16 cleared
-    // light tile: wave-uniform trip count = the longest piece of the wave
-    int32_t wl = tp.len;
-    for (int o = 32; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o));
-    PieceCursor cur;
-    cur.init(tp);
-    for (int32_t st = 0; st < wl; ++st) {
-      if (st < tp.len) {
-        atomicAdd(&cnt16[cur.addr], 1u);
-        cur.step(tp);
+    // light: one piece per thread, walked cell by cell (PieceCursor: no
+    // division per cell); the wave's trip count is its longest piece
+    {
+      const TilePiece tp = dm_unpack_piece(mine.x, mine.y, mine.z, mine.w);
+      const int32_t len = tid < c ? tp.len : 0;
+      int32_t wl = len;
+      for (int o = 32; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o));
+      PieceCursor cur;
+      cur.init(tp);
+      for (int32_t st = 0; st < wl; ++st) {
+        if (st < len) {
+          atomicAdd(&tl[cur.addr], 1u);
+          cur.step(tp);
+        }
       }
-    }
-    if (tp.addr_end >= 0) atomicAdd(&cnt16[tp.addr_end], 0xFFFFu);
-    __syncthreads();
-    apply_tile(g, p, tx0, ty0, L, state, vec_ok,
-               [&](int ly, int cx, uint32_t* h4, uint32_t* m4) {
-                 for (int e = 0; e < 4; ++e) {
-                   const uint32_t v = cnt16[ly * kLdsPitch + cx + e];
-                   h4[e] = v >> 16;
-                   m4[e] = v & 0xFFFFu;
-                 }
-               },
-               &sh_T, &sh_free, &sh_U);
-    __syncthreads();
-    if (tid == 0) {
-      unsigned long long* sh = ish + (blockIdx.x % kShards) * kShardWords;
-      if (sh_T) atomicAdd(&sh[SH_T], (unsigned long long)sh_T);
-      if (sh_U) atomicAdd(&sh[SH_U], (unsigned long long)sh_U);
-      tile_free[tile] += sh_free;
-      tile_count[tile] = 0;  // ready for the next call
+      if (len > 0 && tp.addr_end >= 0) atomicAdd(&tl[tp.addr_end], 0xFFFFu);  // that miss becomes a hit
     }
     __syncthreads();
+    DM_PH(dm_phase_acc_integrate, 3);
+    DM_PH_COUNT(dm_phase_acc_integrate, 16, 1);
+    DM_PH_COUNT(dm_phase_acc_integrate, 18, c);
+    cells.apply(g, p, tx0, ty0, tid >> 4, 16, cx, L, state,
+                [&](int ly, uint32_t* h4, uint32_t* m4) {
+                  for (int e = 0; e < 4; ++e) {
+                    const uint32_t v = tl[ly * kLdsPitch + cx + e];
+                    h4[e] = v >> 16;
+                    m4[e] = v & 0xFFFFu;
+                  }
+                },
+                &s_T, &s_free, &s_U);
+    __syncthreads();
+    DM_PH(dm_phase_acc_integrate, 4);
+    if (tid == 0) finish_tile(g, tile, s_T, s_free, s_U, false, tile_count, tile_free, ish);
   }
+  DM_PH_FLUSH(dm_phase_acc_integrate);
 }
 
 // Heavy tiles: apply the merged slab counts, then clear the slab and the
 // tile's piece count for the next call.
-__global__ __launch_bounds__(kApplyThreads) void k_heavy_apply(
-    Geom g, ApplyArgs p, const int32_t* __restrict__ heavy_list, const int32_t* __restrict__ act_tiles,
-    int32_t* tile_count, int32_t* tile_free, uint32_t* __restrict__ slabs, float* __restrict__ L,
-    int8_t* __restrict__ state, unsigned long long* cnt, unsigned long long* ish, int vec_ok) {
-  __shared__ int32_t sh_free, sh_T;
-  __shared__ uint32_t sh_U;
+__global__ __launch_bounds__(kQuarter) void k_heavy_apply(
+    Geom g, ApplyArgs p, const int32_t* __restrict__ heavy_list, int32_t* tile_count, int32_t* tile_free,
+    uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
+    const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok) {
+  __shared__ int32_t s_T, s_free;
+  __shared__ uint32_t s_U;
   const int tid = threadIdx.x;
   const int64_t nh = (int64_t)cnt[CNT_HEAVY];
   for (int64_t h = blockIdx.x; h < nh; h += gridDim.x) {
-    const int32_t tile = act_tiles[heavy_list[h]];
-    if (tid == 0) { sh_free = 0; sh_T = 0; sh_U = 0u; }
-    __syncthreads();
+    const int32_t tile = heavy_list[h];
+    const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
     uint32_t* sh = slabs + h * (2 * DM_TS * DM_TS);
-    const int32_t tx0 = (tile % g.r.TX) * DM_TS;
-    const int32_t ty0 = (tile / g.r.TX) * DM_TS;
-    apply_tile(g, p, tx0, ty0, L, state, vec_ok,
-               [&](int ly, int cx, uint32_t* h4, uint32_t* m4) {
-                 const uint4 a = *reinterpret_cast<const uint4*>(sh + ly * DM_TS + cx);
-                 const uint4 b = *reinterpret_cast<const uint4*>(sh + DM_TS * DM_TS + ly * DM_TS + cx);
-                 h4[0] = a.x; h4[1] = a.y; h4[2] = a.z; h4[3] = a.w;
-                 m4[0] = b.x; m4[1] = b.y; m4[2] = b.z; m4[3] = b.w;
-               },
-               &sh_T, &sh_free, &sh_U);
-    // clear all 64 rows (apply_tile stops at the band's last row)
-    for (int e = tid * 4; e < 2 * DM_TS * DM_TS; e += kApplyThreads * 4)
+    const int cx = (tid & 15) * 4;
+    CellRows<4> cells;
+    cells.prefetch(g, tx0, ty0, tid >> 4, 16, cx, L, state, vec_ok);
+    uint4 hv[4], mv[4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int ly = (tid >> 4) + 16 * rr;
+      hv[rr] = *reinterpret_cast<const uint4*>(sh + ly * DM_TS + cx);
+      mv[rr] = *reinterpret_cast<const uint4*>(sh + DM_TS * DM_TS + ly * DM_TS + cx);
+    }
+    if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; }
+    __syncthreads();
+    cells.apply(g, p, tx0, ty0, tid >> 4, 16, cx, L, state,
+                [&](int ly, uint32_t* h4, uint32_t* m4) {
+                  const int rr = ly >> 4;
+                  const uint4 a = hv[rr], b = mv[rr];
+                  h4[0] = a.x; h4[1] = a.y; h4[2] = a.z; h4[3] = a.w;
+                  m4[0] = b.x; m4[1] = b.y; m4[2] = b.z; m4[3] = b.w;
+                },
+                &s_T, &s_free, &s_U);
+    // clear all 64 rows (the apply stops at the band's last row)
+    for (int e = tid * 4; e < 2 * DM_TS * DM_TS; e += kQuarter * 4)
       *reinterpret_cast<uint4*>(sh + e) = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
-    if (tid == 0) {
-      unsigned long long* shd = ish + (blockIdx.x % kShards) * kShardWords;
-      if (sh_T) {
-        atomicAdd(&shd[SH_T], (unsigned long long)sh_T);
-        atomicAdd(&shd[SH_TH], (unsigned long long)sh_T);
-      }
-      if (sh_U) atomicAdd(&shd[SH_U], (unsigned long long)sh_U);
-      tile_free[tile] += sh_free;
-      tile_count[tile] = 0;
-    }
+    if (tid == 0) finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
     __syncthreads();
   }
 }
@@ -660,8 +702,6 @@ Geom make_geom(const dm_grid* g) {
   ge.r.TY = (int32_t)g->TY;
   ge.act_cap = (int32_t)g->act_cap;
   ge.seg_cap = g->segs_cap;
-  ge.item_cap = g->item_cap;
-  ge.heavy_cap = g->heavy_cap;
   ge.nb = 0;
   return ge;
 }
@@ -685,6 +725,8 @@ int grid_for(int64_t n, int threads, int64_t cap = 8192) {
 }
 
 }  // namespace
+
+DM_PH_READER(integrate)
 
 int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                         const float* d_ranges, const double* d_trig) {
@@ -711,27 +753,25 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "plan", &t);
   hipLaunchKernelGGL(k_plan, dim3(1), dim3(kPlanThreads), 0, g->stream, ge, g->act_raw, g->ish, g->act_tiles,
-                     g->tile_slot, g->tile_count, g->act_off, g->act_cur, g->act_heavy,
-                     g->heavy_list, g->items, g->cnt);
+                     g->tile_slot, g->tile_count, g->act_cur, g->hitems, g->litems, g->heavy_list, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "scatter", &t);
   hipLaunchKernelGGL(k_scatter, dim3(nblk), dim3(256), 0, g->stream, a, ge, g->beams,
-                     g->tile_slot, g->act_cur, g->segs, g->cnt);
+                     g->tile_slot, g->act_cur, g->pieces, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   const int vec_ok = (g->W % 4 == 0) ? 1 : 0;
   dm_timer_begin(g, "tile_accum", &t);
-  hipLaunchKernelGGL(k_tile_accum, dim3(grid_for(g->item_cap, 1, 4096)), dim3(kApplyThreads), 0,
-                     g->stream, ge, make_apply(g), g->items, g->act_tiles, g->act_off, g->act_heavy,
-                     g->segs, g->beams, g->tile_count, g->tile_free, g->slabs, g->L, g->state,
-                     g->cnt, g->ish, vec_ok);
+  hipLaunchKernelGGL(k_tile_accum, dim3(grid_for(g->hitem_cap + g->act_cap, 1, 2048)), dim3(kQuarter), 0,
+                     g->stream, ge, make_apply(g), g->hitems, g->litems, g->pieces, g->tile_count,
+                     g->tile_free, g->slabs, g->L, g->state, g->cnt, g->ish, vec_ok);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "heavy_apply", &t);
-  hipLaunchKernelGGL(k_heavy_apply, dim3(grid_for(g->heavy_cap, 1, 2048)), dim3(kApplyThreads), 0,
-                     g->stream, ge, make_apply(g), g->heavy_list, g->act_tiles, g->tile_count,
-                     g->tile_free, g->slabs, g->L, g->state, g->cnt, g->ish, vec_ok);
+  hipLaunchKernelGGL(k_heavy_apply, dim3(grid_for(g->heavy_cap, 1, 1024)), dim3(kQuarter), 0, g->stream, ge,
+                     make_apply(g), g->heavy_list, g->tile_count, g->tile_free, g->slabs, g->L, g->state,
+                     g->cnt, g->ish, vec_ok);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   return DM_OK;

@@ -8,7 +8,7 @@
 //          number of free cells (drives which tiles the frontier pass visits)
 // Per-call workspace (grown on demand, reused across calls):
 //   beams  Beam[S*N]     endpoint cells + Bresenham parameters per beam
-//   segs   Seg[...]      (beam, k0, k1) ray pieces binned by tile
+//   pieces PackedPiece[] ray pieces binned by tile, tile-local addresses
 //   active tile lists, frontier slots (one per tile-local component), borders.
 #pragma once
 
@@ -22,12 +22,6 @@
 
 #include "dm_ray.h"
 
-// One ray piece inside one tile: cells k0..k1 of beam `beam`.
-struct Seg {
-  uint32_t beam;
-  uint16_t k0, k1;
-};
-static_assert(sizeof(Seg) == 8, "Seg layout");
 
 // device counters (uint64 each)
 enum {
@@ -39,13 +33,14 @@ enum {
   CNT_SLOTS = 5,    // tile-local frontier components
   CNT_CLUSTERS = 6, // output clusters
   CNT_OVERFLOW = 7, // capacity overflow flags
-  CNT_ITEMS = 8,    // apply work items
-  CNT_HEAVY = 9,    // tiles split over several work items
-  CNT_TH = 10,      // touched cells applied by k_heavy_apply
+  CNT_ITEMS = 8,    // heavy work items (<= 256 pieces of a heavy tile each)
+  CNT_HEAVY = 9,    // heavy tiles (> 256 pieces)
+  CNT_TH = 10,      // touched cells of heavy tiles
   CNT_SORTED = 11,  // 1: out_clu holds the clusters sorted by label
   CNT_FL0 = 12,     // frontier tile-list length, even calls (zeroed by the odd calls)
   CNT_FL1 = 13,     // frontier tile-list length, odd calls (zeroed by the even calls)
-  CNT_N = 14
+  CNT_LITEMS = 14,  // light work items (= light tiles)
+  CNT_N = 15
 };
 
 // Sharded counters: same-address device atomics serialise at the memory side
@@ -94,16 +89,16 @@ struct dm_grid {
 
   // integrate workspace
   Beam* beams = nullptr; int64_t beams_cap = 0;
-  Seg* segs = nullptr; int64_t segs_cap = 0;
-  int32_t* act_tiles = nullptr; int32_t* act_off = nullptr; int32_t* act_cur = nullptr;
+  PackedPiece* pieces = nullptr; int64_t segs_cap = 0;  // ray pieces binned by tile
+  int32_t* act_tiles = nullptr; int32_t* act_cur = nullptr;
   int32_t* act_raw = nullptr;    // [kShards][act_cap] first-touch lists per shard
   int64_t act_cap = 0;
-  int32_t* act_heavy = nullptr;  // active tile -> heavy ordinal or -1
-  int32_t* heavy_list = nullptr; // heavy ordinal -> active tile
+  int4* hitems = nullptr;        // heavy work items {tile, first piece, pieces, heavy ordinal}
+  int64_t hitem_cap = 0;
+  int4* litems = nullptr;        // light work items {tile, first piece, pieces, -1} [act_cap]
+  int32_t* heavy_list = nullptr; // heavy ordinal -> tile
   int64_t heavy_cap = 0;
-  int2* items = nullptr;         // (active tile, chunk) work items
-  int64_t item_cap = 0;
-  uint32_t* slabs = nullptr;     // [heavy][2][64*64] merged counts
+  uint32_t* slabs = nullptr;     // [heavy][2][64*64] merged hit / miss counts
   double* trig = nullptr; int32_t trig_n = -1; float trig_amin = 0, trig_inc = 0;
   int64_t trig_cap = 0;
   double* pose4 = nullptr; int64_t pose_cap = 0;

@@ -271,6 +271,42 @@ DM_HD inline int32_t dm_piece_addr(const TilePiece& tp, int32_t j, float rtwo_n)
   return tp.addr0 + j * tp.da + dq * tp.db;
 }
 
+// A TilePiece packed into 16 bytes (k_scatter writes them, k_tile_accum
+// reads one per lane): every field fits 16 bits because a piece lies in one
+// 64x64 tile (addresses < 64*65, len <= 64) and rays are at most 16386
+// cells (validate_params: range_max / resolution <= 16384), so
+// rem0 < two_n <= 32774 and two_adb <= two_n.  da / db are +-1 or +-pitch
+// (pitch 65 fits int8) or 0.
+//   x: addr0 | len << 16      y: (addr_end + 1) | (u8)da << 16 | (u8)db << 24
+//   z: rem0 | two_adb << 16   w: two_n
+struct PackedPiece {
+  uint32_t x, y, z, w;
+};
+static_assert(sizeof(PackedPiece) == 16, "PackedPiece layout");
+
+DM_HD inline PackedPiece dm_pack_piece(const TilePiece& tp) {
+  PackedPiece p;
+  p.x = (uint32_t)tp.addr0 | ((uint32_t)tp.len << 16);
+  p.y = (uint32_t)(tp.addr_end + 1) | ((uint32_t)(uint8_t)(int8_t)tp.da << 16) |
+        ((uint32_t)(uint8_t)(int8_t)tp.db << 24);
+  p.z = (uint32_t)tp.rem0 | ((uint32_t)tp.two_adb << 16);
+  p.w = (uint32_t)tp.two_n;
+  return p;
+}
+
+DM_HD inline TilePiece dm_unpack_piece(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+  TilePiece tp;
+  tp.addr0 = (int32_t)(x & 0xFFFFu);
+  tp.len = (int32_t)(x >> 16);
+  tp.addr_end = (int32_t)(y & 0xFFFFu) - 1;
+  tp.da = (int32_t)(int8_t)(uint8_t)(y >> 16);
+  tp.db = (int32_t)(int8_t)(uint8_t)(y >> 24);
+  tp.rem0 = (int32_t)(z & 0xFFFFu);
+  tp.two_adb = (int32_t)(z >> 16);
+  tp.two_n = (int32_t)w;
+  return tp;
+}
+
 // Incremental form: the address of the current cell, then one step per k.
 struct PieceCursor {
   int32_t addr, rem;

@@ -54,7 +54,13 @@ extern "C" int emu_integrate(int32_t W, int32_t R, int32_t row0, double ox, doub
     std::fill(miss.begin(), miss.end(), 0u);
     for (int64_t s = off[j]; s < off[j + 1]; ++s) {
       const Beam& bm = beams[segs[s].beam];
-      const TilePiece tp = dm_tile_piece(bm, segs[s].k0, segs[s].k1, row0, tx0, ty0, kPitch);
+      const TilePiece tp0 = dm_tile_piece(bm, segs[s].k0, segs[s].k1, row0, tx0, ty0, kPitch);
+      // k_scatter stores the piece packed (16 B); k_tile_accum unpacks it
+      const PackedPiece pk = dm_pack_piece(tp0);
+      const TilePiece tp = dm_unpack_piece(pk.x, pk.y, pk.z, pk.w);
+      if (tp.addr0 != tp0.addr0 || tp.addr_end != tp0.addr_end || tp.len != tp0.len || tp.da != tp0.da ||
+          tp.db != tp0.db || tp.rem0 != tp0.rem0 || tp.two_adb != tp0.two_adb || tp.two_n != tp0.two_n)
+        return -105;
       const float rtwo_n = 1.0f / (float)tp.two_n;
       PieceCursor cur;
       cur.init(tp);

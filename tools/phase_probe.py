@@ -1,0 +1,73 @@
+"""Per-phase timing of k_tile_accum and k_frontier_tile on the bench workload
+(C3, one GPU), from the opt-in timing build (csrc `make phase` ->
+dm/libdm_phase.so, dm_phase.h).  Prints, per kernel phase, the summed
+workgroup time per step (thread 0's wall-clock ticks between marks, 10 ns),
+i.e. workgroup-microseconds: divide by the resident workgroups for a feel of
+the wall-time share.  Diagnostic only; never part of the product path."""
+import ctypes
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "distributed-autonomous-exploration-and-mapping_amd")
+os.environ["DM_LIB"] = os.path.join(PKG, "dm", "libdm_phase.so")
+sys.path.insert(0, PKG)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import dm  # noqa: E402
+from dm import synth  # noqa: E402
+
+NAMES = {
+    "frontier": {0: "load+bitrows", 1: "F+run scan", 2: "enum runs", 3: "unions", 4: "compress",
+                 5: "roots", 6: "sums+slot atomic", 7: "slot/border/edge writes", 8: "empty tile exit",
+                 16: "#tiles", 17: "#runs", 18: "#tiles with F"},
+    "integrate": {0: "item setup (pieces, prefetch)", 1: "heavy accum", 2: "heavy slab flush",
+                  3: "light accum", 4: "light apply", 16: "#light items",
+                  17: "#heavy items", 18: "#light pieces", 19: "#heavy pieces"},
+}
+
+
+def main():
+    G, res, S, N, steps = 16384, 0.05, 64, 4096, 10
+    half = G * res / 2
+    world = synth.make_world(0, -half, -half, half, half)
+    st = synth.ScanStream(world, S, N, 500, region=(-half + 1, -half + 1, half - 1, half - 1))
+    pool = [st.next_batch() for _ in range(3)]
+    dev = torch.device("cuda", 0)
+    dpool = [(torch.from_numpy(synth.pose4(p)).to(dev), torch.from_numpy(r).to(dev)) for p, r in pool]
+    torch.cuda.synchronize()
+    amin, inc = float(synth.LD06_ANGLE_MIN), float(synth.ld06_angle_increment(N))
+    lib = dm._ffi.load_library()
+    readers = {tu: getattr(lib, f"dm_debug_phases_{tu}") for tu in NAMES}
+    buf = (ctypes.c_ulonglong * 64)()
+    m = dm.OccupancyMapper(dm.default_params(G, G, resolution=res))
+    for k in range(6):
+        p4, r = dpool[k % 3]
+        m.integrate_device(p4.data_ptr(), S, r.data_ptr(), N, amin, inc)
+        m.frontiers()
+    for rd in readers.values():
+        rd(buf, 64, 1)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        p4, r = dpool[k % 3]
+        m.integrate_device(p4.data_ptr(), S, r.data_ptr(), N, amin, inc)
+        m.frontiers()
+    m.synchronize()
+    print(f"{steps} steps, {1e3 * (time.perf_counter() - t0) / steps:.3f} ms/step (timing build)")
+    for tu, names in NAMES.items():
+        readers[tu](buf, 64, 1)
+        print(f"[{tu}]")
+        for k, name in names.items():  # noqa: B007
+            v = buf[k] / steps
+            if k >= 16:
+                print(f"  {name:28s} {v:12.1f} per step")
+            else:
+                print(f"  {name:28s} {v * 0.01:12.1f} workgroup-us per step")
+    m.close()
+
+
+if __name__ == "__main__":
+    main()
