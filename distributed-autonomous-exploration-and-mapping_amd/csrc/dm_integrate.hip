@@ -268,9 +268,13 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __
       tile_slot[t[q]] = (int32_t)j;
       act_cur[j] = (int32_t)ex[0];
       if (c[q] > kChunk) {
-        heavy_list[ex[3]] = t[q];
+        // a cell's count in this call is at most the tile's piece count: below
+        // 65536 the slab is packed (hits << 16 | misses, one word per cell)
+        const int32_t wide = c[q] >= 65536 ? 1 : 0;
+        heavy_list[ex[3]] = t[q] | (wide << 31);
         for (int32_t p0 = 0; p0 < c[q]; p0 += kChunk)
-          hitems[ex[1]++] = make_int4(t[q], (int32_t)ex[0] + p0, min(kChunk, c[q] - p0), (int32_t)ex[3]);
+          hitems[ex[1]++] = make_int4(t[q], (int32_t)ex[0] + p0, min(kChunk, c[q] - p0),
+                                      (int32_t)(2 * ex[3] + wide));
         ++ex[3];
       } else {
         litems[ex[2]++] = make_int4(t[q], (int32_t)ex[0], c[q], -1);
@@ -545,12 +549,19 @@ __global__ __launch_bounds__(kQuarter) void k_tile_accum(
       DM_PH(dm_phase_acc_integrate, 1);
       DM_PH_COUNT(dm_phase_acc_integrate, 17, 1);
       DM_PH_COUNT(dm_phase_acc_integrate, 19, c);
-      uint32_t* sh = slabs + (int64_t)heavy * (2 * DM_TS * DM_TS);
-      for (int e = tid; e < DM_TS * DM_TS; e += kQuarter) {
-        const uint32_t v = tl[(e >> 6) * kLdsPitch + (e & 63)];
-        const uint32_t h = v >> 16, m = v & 0xFFFFu;
-        if (h) atomicAdd(&sh[e], h);
-        if (m) atomicAdd(&sh[DM_TS * DM_TS + e], m);
+      uint32_t* sh = slabs + (int64_t)(heavy >> 1) * (2 * DM_TS * DM_TS);
+      if (heavy & 1) {  // wide slab: separate 32-bit hit and miss counts
+        for (int e = tid; e < DM_TS * DM_TS; e += kQuarter) {
+          const uint32_t v = tl[(e >> 6) * kLdsPitch + (e & 63)];
+          const uint32_t h = v >> 16, m = v & 0xFFFFu;
+          if (h) atomicAdd(&sh[e], h);
+          if (m) atomicAdd(&sh[DM_TS * DM_TS + e], m);
+        }
+      } else {  // packed slab: the LDS word as is (no carry: counts < 65536)
+        for (int e = tid; e < DM_TS * DM_TS; e += kQuarter) {
+          const uint32_t v = tl[(e >> 6) * kLdsPitch + (e & 63)];
+          if (v) atomicAdd(&sh[e], v);
+        }
       }
       __syncthreads();
       DM_PH(dm_phase_acc_integrate, 2);
@@ -603,22 +614,32 @@ __global__ __launch_bounds__(kQuarter) void k_heavy_apply(
   __shared__ uint32_t s_U;
   const int tid = threadIdx.x;
   const int64_t nh = (int64_t)cnt[CNT_HEAVY];
+  DM_PH_INIT();
   for (int64_t h = blockIdx.x; h < nh; h += gridDim.x) {
-    const int32_t tile = heavy_list[h];
+    const int32_t hl = __builtin_amdgcn_readfirstlane(heavy_list[h]);
+    const int32_t tile = hl & 0x7FFFFFFF;
+    const bool wide = hl < 0;
     const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
     uint32_t* sh = slabs + h * (2 * DM_TS * DM_TS);
     const int cx = (tid & 15) * 4;
-    CellRows<4> cells;
-    cells.prefetch(g, tx0, ty0, tid >> 4, 16, cx, L, state, vec_ok);
     uint4 hv[4], mv[4];
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int ly = (tid >> 4) + 16 * rr;
       hv[rr] = *reinterpret_cast<const uint4*>(sh + ly * DM_TS + cx);
-      mv[rr] = *reinterpret_cast<const uint4*>(sh + DM_TS * DM_TS + ly * DM_TS + cx);
+      if (wide) {
+        mv[rr] = *reinterpret_cast<const uint4*>(sh + DM_TS * DM_TS + ly * DM_TS + cx);
+      } else {  // packed: split the word
+        const uint4 v = hv[rr];
+        mv[rr] = make_uint4(v.x & 0xFFFFu, v.y & 0xFFFFu, v.z & 0xFFFFu, v.w & 0xFFFFu);
+        hv[rr] = make_uint4(v.x >> 16, v.y >> 16, v.z >> 16, v.w >> 16);
+      }
     }
+    CellRows<4> cells;
+    cells.prefetch(g, tx0, ty0, tid >> 4, 16, cx, L, state, vec_ok);
     if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; }
     __syncthreads();
+    DM_PH(dm_phase_acc_integrate, 8);
     cells.apply(g, p, tx0, ty0, tid >> 4, 16, cx, L, state,
                 [&](int ly, uint32_t* h4, uint32_t* m4) {
                   const int rr = ly >> 4;
@@ -628,12 +649,14 @@ __global__ __launch_bounds__(kQuarter) void k_heavy_apply(
                 },
                 &s_T, &s_free, &s_U);
     // clear all 64 rows (the apply stops at the band's last row)
-    for (int e = tid * 4; e < 2 * DM_TS * DM_TS; e += kQuarter * 4)
+    for (int e = tid * 4; e < (wide ? 2 : 1) * DM_TS * DM_TS; e += kQuarter * 4)
       *reinterpret_cast<uint4*>(sh + e) = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
+    DM_PH(dm_phase_acc_integrate, 9);
     if (tid == 0) finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
     __syncthreads();
   }
+  DM_PH_FLUSH(dm_phase_acc_integrate);
 }
 
 // ---- maintenance kernels ----------------------------------------------------

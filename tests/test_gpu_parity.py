@@ -309,3 +309,27 @@ def test_c5_beam_density_sweep(oracle_lib, N):
         assert_map_equal(m, om)
         assert_frontiers_equal(m.frontiers(), None, None, om.frontiers(want_mask=False,
                                                                          want_labels=False)[2])
+
+
+@pytest.mark.parametrize("S", [15, 17])
+def test_colocated_scans_heavy_slab_widths(oracle_lib, S):
+    """S scans of 4096 beams from one pose in one call: the sensor's tile gets
+    S*4096 pieces, so its cells' counts approach (S=15: 61440, packed 16-bit
+    slab) or exceed (S=17: 69632, wide slab) 65535 (csrc/dm_integrate.hip,
+    k_plan's per-tile slab width)."""
+    p = cases.make_params(300, 300)
+    rng = np.random.Generator(np.random.PCG64(7 + S))
+    poses = np.tile(np.array([[0.013, -0.021, 0.3]]), (S, 1))
+    poses[:, 2] += rng.uniform(-0.01, 0.01, S)
+    N = 4096
+    ranges = (np.round(rng.uniform(0.05, 8.0, (S, N)) * 1000) / 1000).astype(np.float32)
+    amin, inc = 0.0, float(np.float32(2 * np.pi / (N - 1)))
+    om = oracle_lib.OracleMap(p)
+    with dm.OccupancyMapper(p) as m:
+        for k in range(2):
+            assert m.integrate(poses, ranges, amin, inc) == om.integrate(poses, ranges, amin, inc)
+        st = m.last_stats()
+        assert st["heavy_tiles"] >= 1
+        assert_map_equal(m, om)
+        fr = m.frontiers(want_mask=True, want_labels=True)
+        assert_frontiers_equal(fr, *om.frontiers())
