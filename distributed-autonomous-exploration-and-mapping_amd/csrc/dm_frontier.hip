@@ -77,10 +77,19 @@ __global__ __launch_bounds__(256) void k_frontier_prep(int64_t NT, const int32_t
   }
 }
 
+// Find with path halving: every other node on the way is re-pointed to its
+// grandparent, so later finds (the unions of the next rows, the final
+// compression) walk shorter chains.  Only non-roots are re-pointed, to an
+// ancestor: a halving store racing an atomicMin hook on the same node can
+// drop that hook, but lds_unite then continues with the node's previous
+// parent (atomicMin's return value), which is still an ancestor, so no
+// union is lost.
 __device__ inline int32_t lds_find(volatile int32_t* par, int32_t x) {
   int32_t p = par[x];
   while (p != x) {
-    x = p;
+    const int32_t gp = par[p];
+    if (gp != p) par[x] = gp;
+    x = gp;
     p = par[x];
   }
   return x;
@@ -297,7 +306,21 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
     }
     __syncthreads();
     DM_PH(dm_phase_acc_frontier, 3);
-    for (int r = tid; r < nruns; r += kFT) r_par[r] = lds_find(r_par, r);
+    {  // roots first, writes after a barrier: a final root written early
+       // could be overwritten by another thread's path-halving store
+      int32_t root[kMaxRuns / kFT];
+#pragma unroll
+      for (int q = 0; q < kMaxRuns / kFT; ++q) {
+        const int r = tid + q * kFT;
+        root[q] = r < nruns ? lds_find(r_par, r) : 0;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < kMaxRuns / kFT; ++q) {
+        const int r = tid + q * kFT;
+        if (r < nruns) r_par[r] = root[q];
+      }
+    }
     __syncthreads();
     DM_PH(dm_phase_acc_frontier, 4);
     // ---- 4. components, sums, slots ------------------------------------------

@@ -4,17 +4,27 @@
 //
 // Labels are the SPEC's min row-major index: the root of a
 // set is always the element with the smallest label, so the final labels do
-// not depend on the order in which unions land.  Every access to parent[] is
-// an atomic RMW, performed at the device-coherent point (per-XCD L2s are not
-// coherent; MI355X_MICROARCH.md §Workgroup dispatch).
+// not depend on the order in which unions land.  Hooks are CAS at the
+// device-coherent point (per-XCD L2s are not coherent; MI355X_MICROARCH.md
+// §Workgroup dispatch); reads are relaxed agent-scope loads (below).
 #pragma once
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-__device__ inline int32_t dm_uf_load(int32_t* p) { return atomicOr(p, 0); }
+// Reads of parent[] are relaxed agent-scope loads (global_load sc1: past
+// the CU's L1, served by the XCD's L2), not atomic RMWs: a find costs one
+// L2 round trip per step instead of one memory-side atomic.  Such a read may
+// be stale, but only in one way: a node is hooked exactly once, while it is
+// a root, and parents never change otherwise, so a stale read can only show
+// a hooked node as still being a root.  dm_uf_unite repairs that with the
+// value its failed CAS returns (the node's real parent, read at the
+// coherence point), so every retry climbs at least one real edge.
+__device__ inline int32_t dm_uf_load(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
-__device__ inline int32_t dm_uf_find(int32_t* par, int32_t x) {
+__device__ inline int32_t dm_uf_find(const int32_t* par, int32_t x) {
   for (int it = 0; it < (1 << 22); ++it) {
     const int32_t p = dm_uf_load(par + x);
     if (p == x) return x;
@@ -24,13 +34,20 @@ __device__ inline int32_t dm_uf_find(int32_t* par, int32_t x) {
 }
 
 // Lock-free union: hook the root with the larger label under the other.
+// Two nodes found in the same set stay in it (sets only merge), so a == b
+// is final even from stale reads.
 __device__ inline void dm_uf_unite(int32_t* par, const long long* label, int32_t a, int32_t b) {
   for (int it = 0; it < (1 << 20); ++it) {
     a = dm_uf_find(par, a);
     b = dm_uf_find(par, b);
     if (a == b) return;
     if (label[a] < label[b]) { const int32_t t = a; a = b; b = t; }
-    if (atomicCAS(&par[a], a, b) == a) return;
+    const int32_t old = atomicCAS(&par[a], a, b);
+    if (old == a) return;
+    // a was hooked meanwhile (or read stale): continue from its real parent
+    a = old;
+    b = dm_uf_find(par, b);
+    if (a == b) return;
   }
 }
 
