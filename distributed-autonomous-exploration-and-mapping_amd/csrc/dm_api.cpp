@@ -159,7 +159,11 @@ int grow_slots(dm_grid* g, int64_t need) {
   if (!rc) rc = dev_alloc(&g->slot_own, 3 * cap, "slot sums");
   if (!rc) rc = dev_alloc(&g->slot_acc, 3 * cap, "slot totals");
   if (!rc) rc = dev_alloc(&g->clusters, 4 * cap, "clusters");
-  if (!rc) rc = dev_alloc(&g->out_clu, cap, "sorted clusters");
+  if (!rc) {
+    dm_cluster* base = g->out_clu ? g->out_clu - kRbRecords : nullptr;
+    rc = dev_alloc(&base, cap + kRbRecords, "sorted clusters");
+    g->out_clu = base ? base + kRbRecords : nullptr;
+  }
   if (!rc) rc = dev_alloc(&g->slot_k, cap, "slot cluster index");
   if (!rc) rc = dev_alloc(&g->rank_of, cap, "cluster sorted position");
   if (rc) return rc;
@@ -171,10 +175,12 @@ int grow_host_out(dm_grid* g, int64_t need) {
   if (need <= g->h_out_cap) return DM_OK;
   int64_t cap = std::max<int64_t>(need, 2 * g->h_out_cap);
   if (g->stream) DM_HIP(hipStreamSynchronize(g->stream));
-  if (g->h_out) (void)hipHostFree(g->h_out);
+  if (g->h_out) (void)hipHostFree(g->h_out - kRbRecords);
   g->h_out = nullptr;
   g->h_out_cap = 0;
-  DM_HIP(hipHostMalloc((void**)&g->h_out, sizeof(dm_cluster) * (size_t)cap, hipHostMallocDefault));
+  dm_cluster* base = nullptr;
+  DM_HIP(hipHostMalloc((void**)&base, sizeof(dm_cluster) * (size_t)(cap + kRbRecords), hipHostMallocDefault));
+  g->h_out = base + kRbRecords;
   g->h_out_cap = cap;
   return DM_OK;
 }
@@ -393,13 +399,14 @@ int dm_destroy(dm_grid* g) {
   dev_free(g->border); dev_free(g->ftiles); dev_free(g->slot_label); dev_free(g->slot_parent); dev_free(g->slot_root);
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
   dev_free(g->edge_slot); dev_free(g->edge_label); dev_free(g->mask); dev_free(g->labels);
-  dev_free(g->halo); dev_free(g->out_clu); dev_free(g->ish); dev_free(g->act_raw);
+  dev_free(g->halo); if (g->out_clu) (void)hipFree(g->out_clu - kRbRecords);
+  g->out_clu = nullptr; dev_free(g->ish); dev_free(g->act_raw);
   dev_free(g->slot_k); dev_free(g->rank_of); dev_free(g->m_parent); dev_free(g->m_label);
   dev_free(g->m_acc); dev_free(g->m_clu); dev_free(g->m_out); dev_free(g->m_cnt);
   if (g->h_mcnt) (void)hipHostFree(g->h_mcnt);
   if (g->h_cnt) (void)hipHostFree(g->h_cnt);
   if (g->h_sh) (void)hipHostFree(g->h_sh);
-  if (g->h_out) (void)hipHostFree(g->h_out);
+  if (g->h_out) (void)hipHostFree(g->h_out - kRbRecords);
   if (g->h_pose4) (void)hipHostFree(g->h_pose4);
   if (g->stream && g->own_stream) (void)hipStreamDestroy(g->stream);
   delete g;

@@ -24,6 +24,8 @@
 #include "dm_uf.h"
 #include "dm_phase.h"
 
+#include <string.h>
+
 #include <algorithm>
 
 DM_PH_DECL(frontier)
@@ -558,12 +560,26 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
                                                             const unsigned long long* __restrict__ count,
                                                             int64_t cap, dm_cluster* __restrict__ out,
                                                             int32_t* __restrict__ rank_of,
-                                                            unsigned long long* sorted) {
+                                                            unsigned long long* sorted,
+                                                            const unsigned long long* __restrict__ cnt,
+                                                            const unsigned long long* __restrict__ fsh,
+                                                            unsigned long long* __restrict__ header) {
   __shared__ long long keys[kSortChunk];
   __shared__ int32_t part[kSortWaves][64];
   const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
   const int64_t K = (int64_t)*count;
   if (blockIdx.x == 0 && tid == 0) *sorted = K <= cap ? 1ull : 0ull;
+  if (header && blockIdx.x == 0) {
+    // readback header (this is the pipeline's last kernel: every counter is
+    // final): the counters, then the fullest slot shard; the host copies it
+    // together with the first sorted records in ONE transfer
+    if (tid < CNT_N) header[tid] = tid == CNT_SORTED ? (K <= cap ? 1ull : 0ull) : cnt[tid];
+    if (tid == CNT_N) {
+      unsigned long long most = 0;
+      for (int i = 0; i < kShards; ++i) most = max(most, fsh[i * kShardWords + SH_SLOT]);
+      header[CNT_N] = most;
+    }
+  }
   if (K > cap) return;
   const int64_t i = (int64_t)blockIdx.x * 64 + lane;
   if ((int64_t)blockIdx.x * 64 >= K) return;  // whole workgroup: no barrier skipped
@@ -658,10 +674,11 @@ DM_PH_READER(frontier)
 
 int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const unsigned long long* d_count,
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
-                        int32_t* rank_of, unsigned long long* d_sorted) {
+                        int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
+                        const unsigned long long* fsh, unsigned long long* header) {
   const int64_t cap = std::min<int64_t>(max_records, kRankSortCap);
   hipLaunchKernelGGL(k_rank_sort, dim3(grid_for(cap, 64, 1 << 20)), dim3(kSortThreads), 0, stream,
-                     ox, oy, res, clusters, d_count, cap, out, rank_of, d_sorted);
+                     ox, oy, res, clusters, d_count, cap, out, rank_of, d_sorted, cnt, fsh, header);
   DM_HIP(hipGetLastError());
   return DM_OK;
 }
@@ -715,7 +732,8 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   }
   dm_timer_begin(g, "sort_clusters", &t);
   const int rc = dm_launch_rank_sort(g->stream, g->clusters, g->cnt + CNT_CLUSTERS, g->slot_cap, g->p.origin_x,
-                           g->p.origin_y, g->p.resolution, g->out_clu, g->rank_of, g->cnt + CNT_SORTED);
+                           g->p.origin_y, g->p.resolution, g->out_clu, g->rank_of, g->cnt + CNT_SORTED,
+                           g->cnt, g->fsh, dm_rb_header(g->out_clu));
   dm_timer_end(g, &t);
   if (rc) return rc;
   return DM_OK;
@@ -729,18 +747,16 @@ int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n
                         int64_t* copied) {
   int rc = dm_enqueue_frontiers(g, want_mask, want_labels);
   if (rc) return rc;
+  // ONE transfer: the readback header (counters + fullest slot shard, written
+  // by k_rank_sort) and the first sorted records behind it
   const int64_t hint = std::min<int64_t>(std::min<int64_t>(g->clu_hint, g->h_out_cap), g->slot_cap);
-  DM_HIP(hipMemcpyAsync(g->h_cnt, g->cnt, sizeof(unsigned long long) * CNT_N, hipMemcpyDeviceToHost,
-                        g->stream));
-  if (hint > 0)
-    DM_HIP(hipMemcpyAsync(g->h_out, g->out_clu, sizeof(dm_cluster) * (size_t)hint,
-                          hipMemcpyDeviceToHost, g->stream));
-  DM_HIP(dm_copy_shards(g));
+  DM_HIP(hipMemcpyAsync(g->h_out - kRbRecords, g->out_clu - kRbRecords,
+                        sizeof(dm_cluster) * (size_t)(kRbRecords + hint), hipMemcpyDeviceToHost, g->stream));
   DM_HIP(hipStreamSynchronize(g->stream));
+  const unsigned long long* hdr = dm_rb_header(g->h_out);
+  memcpy(g->h_cnt, hdr, sizeof(unsigned long long) * CNT_N);
   *copied = hint;
-  unsigned long long most = 0;
-  const unsigned long long* fs = g->h_sh + kShards * kShardWords;
-  for (int i = 0; i < kShards; ++i) most = std::max(most, fs[i * kShardWords + SH_SLOT]);
+  const unsigned long long most = hdr[CNT_N];
   if ((int64_t)most > g->slot_cap / kShards || (g->h_cnt[CNT_OVERFLOW] & 4ull)) {
     *n_clusters = (int64_t)most * kShards;  // slot capacity that fits the fullest shard
     return DM_ERR_CAPACITY;

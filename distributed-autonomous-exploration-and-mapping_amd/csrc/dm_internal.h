@@ -53,6 +53,19 @@ static_assert(kShards * kShardWords == 512, "k_integrate_reset covers 512 shard 
 enum { SH_U = 0, SH_T = 1, SH_TH = 2, SH_ACT = 3 };  // integrate shard fields
 enum { SH_SLOT = 0 };                                 // frontier shard fields
 
+// Readback header in front of the sorted cluster records (device out_clu and
+// pinned h_out both point kRbRecords records into their allocation): the
+// frontier counters [CNT_N] and the fullest slot shard [CNT_N], so one D2H
+// transfer returns counters and records together.
+constexpr int kRbRecords = 6;  // 6 * 48 B = 288 B >= (CNT_N + 1) * 8 B
+static_assert(kRbRecords * sizeof(dm_cluster) >= (CNT_N + 1) * sizeof(unsigned long long), "readback header");
+inline unsigned long long* dm_rb_header(dm_cluster* records) {
+  return reinterpret_cast<unsigned long long*>(records - kRbRecords);
+}
+inline const unsigned long long* dm_rb_header(const dm_cluster* records) {
+  return reinterpret_cast<const unsigned long long*>(records - kRbRecords);
+}
+
 struct dm_grid;
 // async D2H of both shard-counter blocks into g->h_sh (pinned)
 hipError_t dm_copy_shards(dm_grid* g);
@@ -162,7 +175,8 @@ int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n
                         int64_t* copied);
 int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const unsigned long long* d_count,
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
-                        int32_t* rank_of, unsigned long long* d_sorted);
+                        int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
+                        const unsigned long long* fsh, unsigned long long* header);
 // cross-band exchange (dm_merge.hip)
 int64_t dm_export_nbytes(int64_t W, int64_t rec_cap);
 int dm_launch_export(dm_grid* g, void* d_export, int64_t rec_cap);
