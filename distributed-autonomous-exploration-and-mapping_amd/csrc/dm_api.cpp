@@ -178,9 +178,19 @@ int grow_host_out(dm_grid* g, int64_t need) {
   if (g->h_out) (void)hipHostFree(g->h_out - kRbRecords);
   g->h_out = nullptr;
   g->h_out_cap = 0;
+  // mapped + coherent: k_rank_sort writes the readback header and the first
+  // records straight into it over PCIe (no D2H copy command per call)
   dm_cluster* base = nullptr;
-  DM_HIP(hipHostMalloc((void**)&base, sizeof(dm_cluster) * (size_t)(cap + kRbRecords), hipHostMallocDefault));
+  DM_HIP(hipHostMalloc((void**)&base, sizeof(dm_cluster) * (size_t)(cap + kRbRecords),
+                       hipHostMallocMapped | hipHostMallocCoherent));
+  dm_cluster* dbase = nullptr;
+  const hipError_t e = hipHostGetDevicePointer((void**)&dbase, base, 0);
+  if (e != hipSuccess) {
+    (void)hipHostFree(base);
+    return dm_hip_check(e, "hipHostGetDevicePointer(cluster readback)");
+  }
   g->h_out = base + kRbRecords;
+  g->h_out_dev = dbase + kRbRecords;
   g->h_out_cap = cap;
   return DM_OK;
 }

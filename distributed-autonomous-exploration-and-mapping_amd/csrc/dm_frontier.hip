@@ -563,13 +563,15 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
                                                             unsigned long long* sorted,
                                                             const unsigned long long* __restrict__ cnt,
                                                             const unsigned long long* __restrict__ fsh,
-                                                            unsigned long long* __restrict__ header) {
+                                                            dm_cluster* __restrict__ host_out,
+                                                            int64_t host_cap) {
   __shared__ long long keys[kSortChunk];
   __shared__ int32_t part[kSortWaves][64];
   const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
   const int64_t K = (int64_t)*count;
   if (blockIdx.x == 0 && tid == 0) *sorted = K <= cap ? 1ull : 0ull;
-  if (header && blockIdx.x == 0) {
+  if (host_out && blockIdx.x == 0) {
+    unsigned long long* header = dm_rb_header(host_out);
     // readback header (this is the pipeline's last kernel: every counter is
     // final): the counters, then the fullest slot shard; the host copies it
     // together with the first sorted records in ONE transfer
@@ -625,6 +627,7 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
     c.cx_m = ox + (mx + 0.5) * res;
     c.cy_m = oy + (my + 0.5) * res;
     out[rank] = c;
+    if (host_out && rank < host_cap) host_out[rank] = c;  // mapped host readback
     if (rank_of) rank_of[i] = rank;
   }
 }
@@ -675,10 +678,11 @@ DM_PH_READER(frontier)
 int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const unsigned long long* d_count,
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
                         int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
-                        const unsigned long long* fsh, unsigned long long* header) {
+                        const unsigned long long* fsh, dm_cluster* host_out, int64_t host_cap) {
   const int64_t cap = std::min<int64_t>(max_records, kRankSortCap);
   hipLaunchKernelGGL(k_rank_sort, dim3(grid_for(cap, 64, 1 << 20)), dim3(kSortThreads), 0, stream,
-                     ox, oy, res, clusters, d_count, cap, out, rank_of, d_sorted, cnt, fsh, header);
+                     ox, oy, res, clusters, d_count, cap, out, rank_of, d_sorted, cnt, fsh, host_out,
+                     host_cap);
   DM_HIP(hipGetLastError());
   return DM_OK;
 }
@@ -733,7 +737,7 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   dm_timer_begin(g, "sort_clusters", &t);
   const int rc = dm_launch_rank_sort(g->stream, g->clusters, g->cnt + CNT_CLUSTERS, g->slot_cap, g->p.origin_x,
                            g->p.origin_y, g->p.resolution, g->out_clu, g->rank_of, g->cnt + CNT_SORTED,
-                           g->cnt, g->fsh, dm_rb_header(g->out_clu));
+                           g->cnt, g->fsh, g->h_out_dev, g->h_out_cap);
   dm_timer_end(g, &t);
   if (rc) return rc;
   return DM_OK;
@@ -747,11 +751,10 @@ int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n
                         int64_t* copied) {
   int rc = dm_enqueue_frontiers(g, want_mask, want_labels);
   if (rc) return rc;
-  // ONE transfer: the readback header (counters + fullest slot shard, written
-  // by k_rank_sort) and the first sorted records behind it
-  const int64_t hint = std::min<int64_t>(std::min<int64_t>(g->clu_hint, g->h_out_cap), g->slot_cap);
-  DM_HIP(hipMemcpyAsync(g->h_out - kRbRecords, g->out_clu - kRbRecords,
-                        sizeof(dm_cluster) * (size_t)(kRbRecords + hint), hipMemcpyDeviceToHost, g->stream));
+  // no copy command: k_rank_sort wrote the readback header (counters + the
+  // fullest slot shard) and the first h_out_cap sorted records straight into
+  // the mapped host buffer
+  const int64_t hint = std::min<int64_t>(g->h_out_cap, g->slot_cap);
   DM_HIP(hipStreamSynchronize(g->stream));
   const unsigned long long* hdr = dm_rb_header(g->h_out);
   memcpy(g->h_cnt, hdr, sizeof(unsigned long long) * CNT_N);

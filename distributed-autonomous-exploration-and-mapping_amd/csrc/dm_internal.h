@@ -55,14 +55,14 @@ enum { SH_SLOT = 0 };                                 // frontier shard fields
 
 // Readback header in front of the sorted cluster records (device out_clu and
 // pinned h_out both point kRbRecords records into their allocation): the
-// frontier counters [CNT_N] and the fullest slot shard [CNT_N], so one D2H
-// transfer returns counters and records together.
+// frontier counters [CNT_N] and the fullest slot shard [CNT_N], written by
+// k_rank_sort into the mapped host buffer together with the first records.
 constexpr int kRbRecords = 6;  // 6 * 48 B = 288 B >= (CNT_N + 1) * 8 B
 static_assert(kRbRecords * sizeof(dm_cluster) >= (CNT_N + 1) * sizeof(unsigned long long), "readback header");
-inline unsigned long long* dm_rb_header(dm_cluster* records) {
+__host__ __device__ inline unsigned long long* dm_rb_header(dm_cluster* records) {
   return reinterpret_cast<unsigned long long*>(records - kRbRecords);
 }
-inline const unsigned long long* dm_rb_header(const dm_cluster* records) {
+__host__ __device__ inline const unsigned long long* dm_rb_header(const dm_cluster* records) {
   return reinterpret_cast<const unsigned long long*>(records - kRbRecords);
 }
 
@@ -134,7 +134,8 @@ struct dm_grid {
   int32_t* slot_k = nullptr;      // [slot_cap] root slot -> compact cluster index
   int32_t* rank_of = nullptr;     // [slot_cap] compact cluster index -> sorted position
   dm_cluster* out_clu = nullptr;  // [slot_cap] sorted cluster records (k_rank_sort)
-  dm_cluster* h_out = nullptr;    // pinned staging for sorted cluster records
+  dm_cluster* h_out = nullptr;    // pinned (mapped, coherent) readback: header + sorted records
+  dm_cluster* h_out_dev = nullptr;  // its device address
   int64_t h_out_cap = 0;
   int64_t clu_hint = 1024;        // records copied speculatively with the counters
   int32_t* cell_slot = nullptr;   // dense [R][W] (only when labels requested)
@@ -176,7 +177,7 @@ int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n
 int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const unsigned long long* d_count,
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
                         int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
-                        const unsigned long long* fsh, unsigned long long* header);
+                        const unsigned long long* fsh, dm_cluster* host_out, int64_t host_cap);
 // cross-band exchange (dm_merge.hip)
 int64_t dm_export_nbytes(int64_t W, int64_t rec_cap);
 int dm_launch_export(dm_grid* g, void* d_export, int64_t rec_cap);

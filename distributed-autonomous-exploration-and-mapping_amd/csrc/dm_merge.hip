@@ -286,7 +286,7 @@ int dm_launch_merge(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t 
   DM_HIP(hipGetLastError());
   const int rc = dm_launch_rank_sort(g->stream, g->m_clu, g->m_cnt + M_K, n, g->p.origin_x, g->p.origin_y,
                                      g->p.resolution, g->m_out, nullptr, g->m_cnt + M_SORTED, nullptr,
-                                     nullptr, nullptr);
+                                     nullptr, nullptr, 0);
   dm_timer_end(g, &t);
   return rc;
 }

@@ -80,7 +80,7 @@ class OccupancyMapper:
         self.width = int(out.width)
         self.rows = int(out.band_rows)
         self.row0 = int(out.band_row0)
-        self._cbuf = np.empty(1 << 14, dtype=np.dtype(CLUSTER_DTYPE))
+        self._cap = 1 << 12  # cluster records per frontiers() buffer (grown on demand)
 
     # -- lifetime ---------------------------------------------------------
     def close(self):
@@ -218,18 +218,20 @@ class OccupancyMapper:
         labels = np.empty((self.rows, self.width), np.int64) if want_labels else None
         n = ctypes.c_int64(0)
         with self._lock:
-            if cap is not None and (self._cbuf is None or self._cbuf.shape[0] < cap):
-                self._cbuf = np.empty(max(1, int(cap)), dtype=np.dtype(CLUSTER_DTYPE))
+            if cap is not None and self._cap < cap:
+                self._cap = max(1, int(cap))
             while True:
-                buf = self._cbuf
+                # a fresh array per call: the library writes the records straight
+                # into it and the caller owns the result (no second copy)
+                buf = np.empty(self._cap, dtype=np.dtype(CLUSTER_DTYPE))
                 rc = self._lib.dm_frontiers(self._handle(), _vp(mask), _vp(labels), _vp(buf),
                                             buf.shape[0], ctypes.byref(n))
                 if rc == _ffi.DM_ERR_CAPACITY and n.value > buf.shape[0]:
-                    self._cbuf = np.empty(int(n.value) * 2, dtype=np.dtype(CLUSTER_DTYPE))
+                    self._cap = int(n.value) * 2
                     continue
                 check(rc)
                 break
-            clusters = buf[: int(n.value)].copy()
+            clusters = buf[: int(n.value)]
         return Frontiers(clusters=clusters, mask=mask, labels=labels)
 
     # -- sharding support -------------------------------------------------
