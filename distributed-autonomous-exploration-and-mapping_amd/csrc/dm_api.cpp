@@ -603,8 +603,7 @@ int dm_frontiers(dm_grid* g, uint8_t* mask, int64_t* labels, dm_cluster* out, in
   const int64_t nw = std::min<int64_t>(n, cap);
   if ((rc = copy_clusters(g, g->h_cnt[CNT_SORTED] != 0, n, nw, copied, g->out_clu, g->clusters, out)))
     return rc;
-  g->clu_hint = std::max<int64_t>(1024, n + n / 4 + 64);
-  if (g->clu_hint > g->h_out_cap && (rc = grow_host_out(g, g->clu_hint))) return rc;
+  if (n + n / 4 + 64 > g->h_out_cap && (rc = grow_host_out(g, n + n / 4 + 64))) return rc;
   if (mask) DM_HIP(hipMemcpy(mask, g->mask, (size_t)cells, hipMemcpyDeviceToHost));
   if (labels) DM_HIP(hipMemcpy(labels, g->labels, sizeof(int64_t) * (size_t)cells, hipMemcpyDeviceToHost));
   if (n_out) *n_out = n;
@@ -646,13 +645,11 @@ int dm_merge_bands(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t r
   if (n >= (1ll << 31)) return dm_set_error(DM_ERR_SHAPE, "nranks * rec_cap must be < 2^31");
   if ((rc = grow_merge(g, n))) return rc;
   if ((rc = dm_launch_merge(g, d_gathered, nranks, rec_cap, min_size))) return rc;
-  const int64_t hint = std::min<int64_t>(std::min<int64_t>(g->m_hint, g->h_out_cap), n);
-  DM_HIP(hipMemcpyAsync(g->h_mcnt, g->m_cnt, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost,
-                        g->stream));
-  if (hint > 0)
-    DM_HIP(hipMemcpyAsync(g->h_out, g->m_out, sizeof(dm_cluster) * (size_t)hint, hipMemcpyDeviceToHost,
-                          g->stream));
+  // the merge's sort kernel wrote the merge counters and the first h_out_cap
+  // records into the mapped host readback buffer: no copy command
+  const int64_t hint = std::min<int64_t>(g->h_out_cap, n);
   DM_HIP(hipStreamSynchronize(g->stream));
+  memcpy(g->h_mcnt, dm_rb_header(g->h_out), sizeof(unsigned long long) * 4);
   if (g->h_mcnt[1]) {
     if (n_out) *n_out = (int64_t)g->h_mcnt[3];
     return dm_set_error(DM_ERR_INCOMPLETE,
@@ -663,8 +660,7 @@ int dm_merge_bands(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t r
   const int64_t K = (int64_t)g->h_mcnt[0];
   const int64_t nw = std::min<int64_t>(K, cap);
   if ((rc = copy_clusters(g, g->h_mcnt[2] != 0, K, nw, hint, g->m_out, g->m_clu, out))) return rc;
-  g->m_hint = std::max<int64_t>(1024, K + K / 4 + 64);
-  if (g->m_hint > g->h_out_cap && (rc = grow_host_out(g, g->m_hint))) return rc;
+  if (K + K / 4 + 64 > g->h_out_cap && (rc = grow_host_out(g, K + K / 4 + 64))) return rc;
   if (n_out) *n_out = K;
   if (K > cap) return dm_set_error(DM_ERR_CAPACITY, "%lld clusters, capacity %lld", (long long)K,
                                    (long long)cap);

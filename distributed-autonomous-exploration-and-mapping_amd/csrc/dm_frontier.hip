@@ -562,6 +562,7 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
                                                             int32_t* __restrict__ rank_of,
                                                             unsigned long long* sorted,
                                                             const unsigned long long* __restrict__ cnt,
+                                                            int ncnt, int sorted_idx,
                                                             const unsigned long long* __restrict__ fsh,
                                                             dm_cluster* __restrict__ host_out,
                                                             int64_t host_cap) {
@@ -575,11 +576,11 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
     // readback header (this is the pipeline's last kernel: every counter is
     // final): the counters, then the fullest slot shard; the host copies it
     // together with the first sorted records in ONE transfer
-    if (tid < CNT_N) header[tid] = tid == CNT_SORTED ? (K <= cap ? 1ull : 0ull) : cnt[tid];
-    if (tid == CNT_N) {
+    if (tid < ncnt) header[tid] = tid == sorted_idx ? (K <= cap ? 1ull : 0ull) : cnt[tid];
+    if (tid == ncnt && fsh) {
       unsigned long long most = 0;
       for (int i = 0; i < kShards; ++i) most = max(most, fsh[i * kShardWords + SH_SLOT]);
-      header[CNT_N] = most;
+      header[ncnt] = most;
     }
   }
   if (K > cap) return;
@@ -678,11 +679,12 @@ DM_PH_READER(frontier)
 int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const unsigned long long* d_count,
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
                         int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
-                        const unsigned long long* fsh, dm_cluster* host_out, int64_t host_cap) {
+                        int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
+                        int64_t host_cap) {
   const int64_t cap = std::min<int64_t>(max_records, kRankSortCap);
   hipLaunchKernelGGL(k_rank_sort, dim3(grid_for(cap, 64, 1 << 20)), dim3(kSortThreads), 0, stream,
-                     ox, oy, res, clusters, d_count, cap, out, rank_of, d_sorted, cnt, fsh, host_out,
-                     host_cap);
+                     ox, oy, res, clusters, d_count, cap, out, rank_of, d_sorted, cnt, ncnt, sorted_idx,
+                     fsh, host_out, host_cap);
   DM_HIP(hipGetLastError());
   return DM_OK;
 }
@@ -737,7 +739,7 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   dm_timer_begin(g, "sort_clusters", &t);
   const int rc = dm_launch_rank_sort(g->stream, g->clusters, g->cnt + CNT_CLUSTERS, g->slot_cap, g->p.origin_x,
                            g->p.origin_y, g->p.resolution, g->out_clu, g->rank_of, g->cnt + CNT_SORTED,
-                           g->cnt, g->fsh, g->h_out_dev, g->h_out_cap);
+                           g->cnt, CNT_N, CNT_SORTED, g->fsh, g->h_out_dev, g->h_out_cap);
   dm_timer_end(g, &t);
   if (rc) return rc;
   return DM_OK;

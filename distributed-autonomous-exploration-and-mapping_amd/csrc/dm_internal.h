@@ -137,7 +137,6 @@ struct dm_grid {
   dm_cluster* h_out = nullptr;    // pinned (mapped, coherent) readback: header + sorted records
   dm_cluster* h_out_dev = nullptr;  // its device address
   int64_t h_out_cap = 0;
-  int64_t clu_hint = 1024;        // records copied speculatively with the counters
   int32_t* cell_slot = nullptr;   // dense [R][W] (only when labels requested)
   int32_t* edge_slot = nullptr;   // [2][W] slots of the band's first / last row
   long long* edge_label = nullptr;// [2][W]
@@ -149,7 +148,6 @@ struct dm_grid {
 
   // cross-band merge workspace (dm_merge.hip), sized nranks * rec_cap
   int64_t m_cap = 0;
-  int64_t m_hint = 1024;          // merged records copied speculatively with the counters
   int32_t* m_parent = nullptr;
   long long* m_label = nullptr;
   long long* m_acc = nullptr;     // [m_cap][3] size, sum_x, sum_y
@@ -177,7 +175,8 @@ int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n
 int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const unsigned long long* d_count,
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
                         int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
-                        const unsigned long long* fsh, dm_cluster* host_out, int64_t host_cap);
+                        int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
+                        int64_t host_cap);
 // cross-band exchange (dm_merge.hip)
 int64_t dm_export_nbytes(int64_t W, int64_t rec_cap);
 int dm_launch_export(dm_grid* g, void* d_export, int64_t rec_cap);
