@@ -719,6 +719,8 @@ int dm_get_edge_labels(dm_grid* g, int64_t* first_row, int64_t* last_row) {
   if (rc || (rc = use_device(g))) return rc;
   if (!g->frontier_valid)
     return dm_set_error(DM_ERR_STATE, "call dm_frontiers first (map or halo changed since)");
+  if ((rc = dm_launch_edge_labels(g))) return rc;
+  DM_HIP(hipStreamSynchronize(g->stream));
   if (first_row)
     DM_HIP(hipMemcpy(first_row, g->edge_label, sizeof(int64_t) * (size_t)g->W, hipMemcpyDeviceToHost));
   if (last_row)

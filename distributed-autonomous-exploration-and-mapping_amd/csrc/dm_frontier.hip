@@ -676,6 +676,15 @@ static FGeom make_fgeom(const dm_grid* g, bool want_mask, bool want_labels) {
 
 DM_PH_READER(frontier)
 
+// Band edge-row labels (dm_get_edge_labels; only the host-side band merge
+// reads them), from the last frontier call's slots.
+int dm_launch_edge_labels(dm_grid* g) {
+  hipLaunchKernelGGL(k_slot_labels, dim3(grid_for(2 * g->W, 256, 1024)), dim3(256), 0, g->stream,
+                     2 * g->W, g->slot_cap, g->edge_slot, g->slot_root, g->slot_label, g->edge_label);
+  DM_HIP(hipGetLastError());
+  return DM_OK;
+}
+
 int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const unsigned long long* d_count,
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
                         int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
@@ -727,9 +736,6 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   hipLaunchKernelGGL(k_frontier_compact, dim3(sgrid), dim3(256), 0, g->stream, fg,
                      g->slot_root, g->slot_label, g->slot_acc, g->clusters, g->slot_k, g->cnt, g->fsh);
   dm_timer_end(g, &t);
-  DM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_slot_labels, dim3(grid_for(2 * g->W, 256, 1024)), dim3(256), 0, g->stream,
-                     2 * g->W, g->slot_cap, g->edge_slot, g->slot_root, g->slot_label, g->edge_label);
   DM_HIP(hipGetLastError());
   if (want_labels) {
     hipLaunchKernelGGL(k_slot_labels, dim3(grid_for(cells, 256, 8192)), dim3(256), 0, g->stream,

@@ -163,8 +163,14 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
 // per-tile slab, applied by k_heavy_apply.  Per active tile j with c_j
 // pieces, exclusive scans of: c_j (bin offsets), heavy items, light items,
 // heavy ordinals.  Heavy items are listed first (they are the long ones).
-// Item = {tile, first piece, pieces, heavy ordinal or -1}.
+// Item = {tile, first piece, pieces, slab code or -1 (light / medium)}.
 constexpr int kChunk = 256;
+// Tiles with more pieces than kChunk but at most kMedium (the ring around a
+// sensor: rays fan out, so a per-thread walk does not pile onto one cell) are
+// one item walked in rounds; only tiles beyond kMedium (the sensor's own)
+// are split over workgroups and merged in a slab.
+constexpr int kMedium = 1024;
+static_assert(kMedium < 65536, "packed 16-bit LDS counts of medium tiles");
 constexpr int kTileWords = DM_TS * kLdsPitch;
 constexpr int kQuarter = 256;  // threads of an apply workgroup (= kChunk)
 static_assert(kChunk < 65536, "packed 16-bit LDS counts");
@@ -251,10 +257,11 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __
     int64_t v[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int q = 0; q < kPlanPer; ++q) {
-      const bool heavy = c[q] > kChunk;
+      const bool heavy = c[q] > kMedium;
+      const bool medium = c[q] > kChunk && !heavy;
       v[0] += c[q];
-      v[1] += heavy ? (c[q] + kChunk - 1) / kChunk : 0;
-      v[2] += (t[q] >= 0 && !heavy) ? 1 : 0;
+      v[1] += heavy ? (c[q] + kChunk - 1) / kChunk : (medium ? 1 : 0);
+      v[2] += (t[q] >= 0 && c[q] <= kChunk) ? 1 : 0;
       v[3] += heavy ? 1 : 0;
     }
     int64_t ex[4], tot[4];
@@ -267,7 +274,10 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __
       act_tiles[j] = t[q];
       tile_slot[t[q]] = (int32_t)j;
       act_cur[j] = (int32_t)ex[0];
-      if (c[q] > kChunk) {
+      if (c[q] > kChunk && c[q] <= kMedium) {
+        // medium tile: one item, walked in rounds of kChunk, applied directly
+        hitems[ex[1]++] = make_int4(t[q], (int32_t)ex[0], c[q], -1);
+      } else if (c[q] > kChunk) {
         // a cell's count in this call is at most the tile's piece count: below
         // 65536 the slab is packed (hits << 16 | misses, one word per cell)
         const int32_t wide = c[q] >= 65536 ? 1 : 0;
@@ -523,7 +533,7 @@ __global__ __launch_bounds__(kQuarter) void k_tile_accum(
     const int32_t heavy = __builtin_amdgcn_readfirstlane(info.w);
     const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
     PackedPiece mine = no_piece();
-    if (tid < c) mine = pieces[c0 + tid];
+    if (tid < c) mine = pieces[c0 + tid];  // first round (light / medium) or the heavy chunk
     CellRows<4> cells;
     const int cx = (tid & 15) * 4;
     if (heavy < 0) cells.prefetch(g, tx0, ty0, tid >> 4, 16, cx, L, state, vec_ok);
@@ -567,11 +577,16 @@ __global__ __launch_bounds__(kQuarter) void k_tile_accum(
       DM_PH(dm_phase_acc_integrate, 2);
       continue;
     }
-    // light: one piece per thread, walked cell by cell (PieceCursor: no
-    // division per cell); the wave's trip count is its longest piece
-    {
+    // light / medium: one piece per thread per round, walked cell by cell
+    // (PieceCursor: no division per cell); the wave's trip count is its
+    // longest piece
+    for (int32_t r0 = 0; r0 < c; r0 += kChunk) {
+      if (r0 > 0) {
+        mine = no_piece();
+        if (r0 + tid < c) mine = pieces[c0 + r0 + tid];
+      }
       const TilePiece tp = dm_unpack_piece(mine.x, mine.y, mine.z, mine.w);
-      const int32_t len = tid < c ? tp.len : 0;
+      const int32_t len = r0 + tid < c ? tp.len : 0;
       int32_t wl = len;
       for (int o = 32; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o));
       PieceCursor cur;

@@ -170,6 +170,7 @@ int dm_launch_state_from_logodds(dm_grid* g);
 int dm_launch_map_image(dm_grid* g, uint8_t* d_img);
 int dm_launch_set_state(dm_grid* g, const int8_t* d_state_in);
 int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels);
+int dm_launch_edge_labels(dm_grid* g);
 int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters,
                         int64_t* copied);
 int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const unsigned long long* d_count,
