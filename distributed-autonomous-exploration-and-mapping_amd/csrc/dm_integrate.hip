@@ -513,10 +513,9 @@ __global__ __launch_bounds__(kQuarter) void k_tile_accum(
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
     const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok) {
   __shared__ uint32_t tl[kTileWords];
-  __shared__ PackedPiece s_pp[kChunk];
   __shared__ int32_t s_T, s_free;
   __shared__ uint32_t s_U;
-  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const int tid = threadIdx.x, lane = lane_id();
   const int64_t HI = (int64_t)cnt[CNT_ITEMS], LI = (int64_t)cnt[CNT_LITEMS];
   const int64_t n_items = HI + LI;
   auto item_of = [&](int64_t it) { return it < HI ? hitems[it] : litems[it - HI]; };
@@ -542,18 +541,34 @@ __global__ __launch_bounds__(kQuarter) void k_tile_accum(
     __syncthreads();
     DM_PH(dm_phase_acc_integrate, 0);
     if (heavy >= 0) {
-      // heavy: the pieces converge on the sensor's cells, so a wave takes
-      // one piece at a time with one lane per cell (distinct cells:
-      // conflict-free LDS atomics); pieces are broadcast from LDS
-      s_pp[tid] = mine;
-      __syncthreads();
-      for (int si = w; si < c; si += kQuarter / 64) {
-        const PackedPiece q = s_pp[si];
-        const TilePiece tp = dm_unpack_piece(q.x, q.y, q.z, q.w);
-        if (lane < tp.len) {
-          const int32_t a = dm_piece_addr(tp, lane, __builtin_amdgcn_rcpf((float)tp.two_n));
-          atomicAdd(&tl[a], (lane == tp.len - 1 && tp.addr_end >= 0) ? 0x10000u : 1u);
+      // heavy (a sensor's tile): the pieces all start at the sensor's cell,
+      // so a plain per-thread walk would pile a wave's atomics onto one LDS
+      // word.  Each thread walks its piece from a staggered start step
+      // (lane mod length) and wraps around: at any step the wave's lanes
+      // sit at different distances from the sensor, on different cells.
+      {
+        const TilePiece tp = dm_unpack_piece(mine.x, mine.y, mine.z, mine.w);
+        const int32_t len = tid < c ? tp.len : 0;
+        int32_t wl = len;
+        for (int o = 32; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o));
+        const int32_t s0 = len > 0 ? lane % len : 0;
+        PieceCursor cur;
+        cur.init(tp);
+        if (s0 > 0) {  // jump to step s0: the closed form once (dm_piece_addr)
+          const int32_t num = tp.rem0 + s0 * tp.two_adb;
+          const int32_t dq = dm_udiv_small(num, tp.two_n, __builtin_amdgcn_rcpf((float)tp.two_n));
+          cur.addr = tp.addr0 + s0 * tp.da + dq * tp.db;
+          cur.rem = num - dq * tp.two_n;
         }
+        int32_t k = s0;
+        for (int32_t st = 0; st < wl; ++st) {
+          if (st < len) {
+            atomicAdd(&tl[cur.addr], 1u);
+            cur.step(tp);
+            if (++k == len) cur.init(tp);  // wrap to the piece's first cell
+          }
+        }
+        if (len > 0 && tp.addr_end >= 0) atomicAdd(&tl[tp.addr_end], 0xFFFFu);  // that miss becomes a hit
       }
       __syncthreads();
       DM_PH(dm_phase_acc_integrate, 1);
@@ -637,23 +652,29 @@ __global__ __launch_bounds__(kQuarter) void k_heavy_apply(
     const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
     uint32_t* sh = slabs + h * (2 * DM_TS * DM_TS);
     const int cx = (tid & 15) * 4;
+    // read-and-clear with atomics: the slab was only ever written by the
+    // items' device-scope atomics, so its lines live at the memory-side
+    // coherence point; exchanging them there avoids a plain-load round trip
+    // plus a clearing store per word
     uint4 hv[4], mv[4];
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
-      const int ly = (tid >> 4) + 16 * rr;
-      hv[rr] = *reinterpret_cast<const uint4*>(sh + ly * DM_TS + cx);
+      const int e0 = ((tid >> 4) + 16 * rr) * DM_TS + cx;
+      uint32_t a[4], m[4];
+      for (int e = 0; e < 4; ++e) a[e] = atomicExch(&sh[e0 + e], 0u);
       if (wide) {
-        mv[rr] = *reinterpret_cast<const uint4*>(sh + DM_TS * DM_TS + ly * DM_TS + cx);
+        for (int e = 0; e < 4; ++e) m[e] = atomicExch(&sh[DM_TS * DM_TS + e0 + e], 0u);
       } else {  // packed: split the word
-        const uint4 v = hv[rr];
-        mv[rr] = make_uint4(v.x & 0xFFFFu, v.y & 0xFFFFu, v.z & 0xFFFFu, v.w & 0xFFFFu);
-        hv[rr] = make_uint4(v.x >> 16, v.y >> 16, v.z >> 16, v.w >> 16);
+        for (int e = 0; e < 4; ++e) { m[e] = a[e] & 0xFFFFu; a[e] >>= 16; }
       }
+      hv[rr] = make_uint4(a[0], a[1], a[2], a[3]);
+      mv[rr] = make_uint4(m[0], m[1], m[2], m[3]);
     }
     CellRows<4> cells;
     cells.prefetch(g, tx0, ty0, tid >> 4, 16, cx, L, state, vec_ok);
     if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; }
     __syncthreads();
+    DM_PH(dm_phase_acc_integrate, 8);
     DM_PH(dm_phase_acc_integrate, 8);
     cells.apply(g, p, tx0, ty0, tid >> 4, 16, cx, L, state,
                 [&](int ly, uint32_t* h4, uint32_t* m4) {
@@ -663,13 +684,13 @@ __global__ __launch_bounds__(kQuarter) void k_heavy_apply(
                   m4[0] = b.x; m4[1] = b.y; m4[2] = b.z; m4[3] = b.w;
                 },
                 &s_T, &s_free, &s_U);
-    // clear all 64 rows (the apply stops at the band's last row)
-    for (int e = tid * 4; e < (wide ? 2 : 1) * DM_TS * DM_TS; e += kQuarter * 4)
-      *reinterpret_cast<uint4*>(sh + e) = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
+    DM_PH(dm_phase_acc_integrate, 9);
     DM_PH(dm_phase_acc_integrate, 9);
     if (tid == 0) finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
     __syncthreads();
+    DM_PH(dm_phase_acc_integrate, 10);
+    DM_PH_COUNT(dm_phase_acc_integrate, 20, 1);
   }
   DM_PH_FLUSH(dm_phase_acc_integrate);
 }
