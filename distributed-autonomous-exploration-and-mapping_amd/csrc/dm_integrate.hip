@@ -479,6 +479,38 @@ struct CellRows {
   }
 };
 
+// One piece per thread, walked cell by cell into the packed LDS count tile
+// (PieceCursor: no division per cell; +1 per cell, then +0xFFFF at the hit
+// cell turns that miss into a hit).  The walk starts at a staggered step
+// (lane mod length) and wraps around: pieces that share their first cells
+// (every ray of a scan starts at the sensor's cell) then sit on different
+// cells at every step instead of piling a wave's atomics onto one LDS word.
+// The wave's trip count is its longest piece.
+__device__ inline void walk_piece(uint32_t* tl, const PackedPiece& mine, bool valid, int lane) {
+  const TilePiece tp = dm_unpack_piece(mine.x, mine.y, mine.z, mine.w);
+  const int32_t len = valid ? tp.len : 0;
+  int32_t wl = len;
+  for (int o = 32; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o));
+  const int32_t s0 = len > 0 ? lane % len : 0;
+  PieceCursor cur;
+  cur.init(tp);
+  if (s0 > 0) {  // jump to step s0: the closed form once (dm_piece_addr)
+    const int32_t num = tp.rem0 + s0 * tp.two_adb;
+    const int32_t dq = dm_udiv_small(num, tp.two_n, __builtin_amdgcn_rcpf((float)tp.two_n));
+    cur.addr = tp.addr0 + s0 * tp.da + dq * tp.db;
+    cur.rem = num - dq * tp.two_n;
+  }
+  int32_t k = s0;
+  for (int32_t st = 0; st < wl; ++st) {
+    if (st < len) {
+      atomicAdd(&tl[cur.addr], 1u);
+      cur.step(tp);
+      if (++k == len) cur.init(tp);  // wrap to the piece's first cell
+    }
+  }
+  if (len > 0 && tp.addr_end >= 0) atomicAdd(&tl[tp.addr_end], 0xFFFFu);
+}
+
 __device__ inline PackedPiece no_piece() {
   PackedPiece q;
   q.x = 0u; q.y = 0u; q.z = 0u; q.w = 1u;
@@ -546,30 +578,7 @@ __global__ __launch_bounds__(kQuarter) void k_tile_accum(
       // word.  Each thread walks its piece from a staggered start step
       // (lane mod length) and wraps around: at any step the wave's lanes
       // sit at different distances from the sensor, on different cells.
-      {
-        const TilePiece tp = dm_unpack_piece(mine.x, mine.y, mine.z, mine.w);
-        const int32_t len = tid < c ? tp.len : 0;
-        int32_t wl = len;
-        for (int o = 32; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o));
-        const int32_t s0 = len > 0 ? lane % len : 0;
-        PieceCursor cur;
-        cur.init(tp);
-        if (s0 > 0) {  // jump to step s0: the closed form once (dm_piece_addr)
-          const int32_t num = tp.rem0 + s0 * tp.two_adb;
-          const int32_t dq = dm_udiv_small(num, tp.two_n, __builtin_amdgcn_rcpf((float)tp.two_n));
-          cur.addr = tp.addr0 + s0 * tp.da + dq * tp.db;
-          cur.rem = num - dq * tp.two_n;
-        }
-        int32_t k = s0;
-        for (int32_t st = 0; st < wl; ++st) {
-          if (st < len) {
-            atomicAdd(&tl[cur.addr], 1u);
-            cur.step(tp);
-            if (++k == len) cur.init(tp);  // wrap to the piece's first cell
-          }
-        }
-        if (len > 0 && tp.addr_end >= 0) atomicAdd(&tl[tp.addr_end], 0xFFFFu);  // that miss becomes a hit
-      }
+      walk_piece(tl, mine, tid < c, lane);
       __syncthreads();
       DM_PH(dm_phase_acc_integrate, 1);
       DM_PH_COUNT(dm_phase_acc_integrate, 17, 1);
@@ -600,19 +609,7 @@ __global__ __launch_bounds__(kQuarter) void k_tile_accum(
         mine = no_piece();
         if (r0 + tid < c) mine = pieces[c0 + r0 + tid];
       }
-      const TilePiece tp = dm_unpack_piece(mine.x, mine.y, mine.z, mine.w);
-      const int32_t len = r0 + tid < c ? tp.len : 0;
-      int32_t wl = len;
-      for (int o = 32; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o));
-      PieceCursor cur;
-      cur.init(tp);
-      for (int32_t st = 0; st < wl; ++st) {
-        if (st < len) {
-          atomicAdd(&tl[cur.addr], 1u);
-          cur.step(tp);
-        }
-      }
-      if (len > 0 && tp.addr_end >= 0) atomicAdd(&tl[tp.addr_end], 0xFFFFu);  // that miss becomes a hit
+      walk_piece(tl, mine, r0 + tid < c, lane);
     }
     __syncthreads();
     DM_PH(dm_phase_acc_integrate, 3);
