@@ -124,16 +124,48 @@ __device__ inline int run_of(const int32_t* rbase, const uint64_t* starts, int y
   return rbase[y] + __popcll(starts[y] & upto_mask(p)) - 1;
 }
 
-// Unknown-cell bit of one halo cell (global column x, band-local row y);
-// out-of-grid cells and missing halos are "not unknown".
-__device__ inline uint32_t halo_unknown(const FGeom& g, const int8_t* state, const int8_t* halo,
-                                        int32_t x, int32_t y) {
-  if (x < 0 || x >= g.W) return 0u;
-  int8_t v = 0;
-  if (y >= 0 && y < g.R) v = state[(int64_t)y * g.W + x];
-  else if (y == -1 && g.has_before) v = halo[x];
-  else if (y == g.R && g.has_after) v = halo[g.W + x];
-  return v == -1 ? 1u : 0u;
+// State byte of one halo cell (global column x, band-local row y), or
+// nullptr for out-of-grid cells and missing halos ("not unknown").
+__device__ inline const int8_t* halo_ptr(const FGeom& g, const int8_t* state, const int8_t* halo, int32_t x,
+                                         int32_t y) {
+  if (x < 0 || x >= g.W) return nullptr;
+  if (y >= 0 && y < g.R) return state + (int64_t)y * g.W + x;
+  if (y == -1 && g.has_before) return halo + x;
+  if (y == g.R && g.has_after) return halo + g.W + x;
+  return nullptr;
+}
+
+// The global loads of one tile, issued one tile ahead by k_frontier_tile so
+// that they are in flight while the previous tile is labelled: this
+// thread's 16 interior cells (one uint4 when the row segment is whole and
+// aligned; ragged tiles read byte-wise when consumed) and its halo cell
+// (waves 0/1: the rows above / below; threads 128..255: the columns left /
+// right) and corner cell (threads 0..3).  A missing cell reads as 0 (free:
+// "not unknown").
+struct TileLoads {
+  uint4 v;
+  int8_t hb, cb;
+};
+
+__device__ inline void tile_issue(const FGeom& g, const int8_t* __restrict__ state,
+                                  const int8_t* __restrict__ halo, int32_t tile, int tid, TileLoads& t) {
+  const int32_t tx0 = (tile % g.TX) * DM_TS, ty0 = (tile / g.TX) * DM_TS;
+  const int y = tid >> 2, q = tid & 3;
+  const int32_t gy = ty0 + y, x0 = tx0 + q * 16;
+  const int64_t off = (int64_t)gy * g.W + x0;
+  t.v = make_uint4(0u, 0u, 0u, 0u);
+  if (gy < g.R && x0 + 16 <= g.W && (off & 15) == 0) t.v = *reinterpret_cast<const uint4*>(state + off);
+  const int lane = tid & 63, hr = (tid - 128) & 63;
+  const bool left = tid < 192;
+  const int8_t* hp = tid < 128 ? halo_ptr(g, state, halo, tx0 + lane, tid < 64 ? ty0 - 1 : ty0 + DM_TS)
+                               : halo_ptr(g, state, halo, left ? tx0 - 1 : tx0 + DM_TS, ty0 + hr);
+  t.hb = hp ? *hp : (int8_t)0;
+  t.cb = 0;
+  if (tid < 4) {
+    const int8_t* cp = halo_ptr(g, state, halo, tx0 + ((tid & 1) ? DM_TS : -1),
+                                (tid & 2) ? ty0 + DM_TS : ty0 - 1);
+    t.cb = cp ? *cp : (int8_t)0;
+  }
 }
 
 // One workgroup per listed tile.  Each 64-cell tile row is a 64-bit word:
@@ -170,9 +202,20 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
   __shared__ long long sbase;
   const int tid = threadIdx.x, lane = __lane_id();
   const int64_t nft = (int64_t)*list_n;
+  // software pipeline: the next tile's loads (and the one after's index) are
+  // issued before the current tile is labelled
+  const int64_t G = gridDim.x;
+  int32_t tile_n = (int64_t)blockIdx.x < nft ? ftiles[blockIdx.x] : -1;
+  int32_t tile_nn = (int64_t)blockIdx.x + G < nft ? ftiles[blockIdx.x + G] : -1;
+  TileLoads ld_n;
+  if (tile_n >= 0) tile_issue(g, state, halo, tile_n, tid, ld_n);
   DM_PH_INIT();
-  for (int64_t jj = blockIdx.x; jj < nft; jj += gridDim.x) {
-    const int32_t tile = ftiles[jj];
+  for (int64_t jj = blockIdx.x; jj < nft; jj += G) {
+    const int32_t tile = tile_n;
+    const TileLoads cur = ld_n;
+    tile_n = tile_nn;
+    if (tile_n >= 0) tile_issue(g, state, halo, tile_n, tid, ld_n);
+    tile_nn = jj + 2 * G < nft ? ftiles[jj + 2 * G] : -1;
     const int64_t j = tile;  // border records are indexed by tile
     DM_PH_COUNT(dm_phase_acc_frontier, 16, 1);
     const int32_t tx0 = (tile % g.TX) * DM_TS;
@@ -186,7 +229,7 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
         const int32_t x0 = tx0 + q * 16;
         const int64_t off = (int64_t)gy * g.W + x0;
         if (x0 + 16 <= g.W && (off & 15) == 0) {
-          const uint4 v = *reinterpret_cast<const uint4*>(state + off);
+          const uint4 v = cur.v;
           const uint32_t w[4] = {v.x, v.y, v.z, v.w};
           for (int k = 0; k < 16; ++k) {
             const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xFFu;
@@ -210,16 +253,14 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
       }
       reinterpret_cast<uint16_t*>(&s_unk[y + 1])[q] = (uint16_t)unk;
       reinterpret_cast<uint16_t*>(&s_free[y])[q] = (uint16_t)fre;
-      // halo, issued together with the interior loads: waves 0/1 the row above
-      // / below (one ballot each), threads 128..255 the columns left / right,
-      // threads 0..3 the four corners
+      // halo (loaded with the interior, a tile ahead): waves 0/1 the row
+      // above / below (one ballot each), threads 128..255 the columns left /
+      // right, threads 0..3 the four corners
       const int hr = (tid - 128) & 63;
       const bool left = tid < 192;
-      uint32_t hu = 0u, su = 0u, cu = 0u;
-      if (tid < 128) hu = halo_unknown(g, state, halo, tx0 + lane, tid < 64 ? ty0 - 1 : ty0 + DM_TS);
-      else su = halo_unknown(g, state, halo, left ? tx0 - 1 : tx0 + DM_TS, ty0 + hr);
-      if (tid < 4)
-        cu = halo_unknown(g, state, halo, tx0 + ((tid & 1) ? DM_TS : -1), (tid & 2) ? ty0 + DM_TS : ty0 - 1);
+      const uint32_t hu = (tid < 128 && cur.hb == -1) ? 1u : 0u;
+      const uint32_t su = (tid >= 128 && cur.hb == -1) ? 1u : 0u;
+      const uint32_t cu = (tid < 4 && cur.cb == -1) ? 1u : 0u;
       const uint64_t hm = __ballot(hu != 0u);
       if (tid == 0) s_unk[0] = hm;
       if (tid == 64) s_unk[DM_TS + 1] = hm;
@@ -407,10 +448,17 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
   DM_PH_FLUSH(dm_phase_acc_frontier);
 }
 
-// Unions across tile borders.  Consecutive border cells of a frontier that
-// crosses the border usually join the same two slots; a lane skips every pair
-// its predecessor lane (the previous border cell) already issued, so repeated
-// unions do not queue same-address atomics behind each other.
+// Unions across tile borders, one wave per (listed tile, edge) — edge 0: the
+// tile's last column against its right neighbour's first column; edge 1: its
+// last row against the next tile row's first row, plus the two corners
+// (lane 63: (63,63) vs the lower-right tile's (0,0); lane 0: (0,63) vs the
+// lower-left tile's (63,0)).  The waves are independent (no workgroup
+// barrier), so every (tile, edge) of the call is in flight at once and the
+// kernel takes about one unit's chain of dependent loads.  Consecutive
+// border cells of a frontier that crosses the border usually join the same
+// two slots; a lane skips every pair its predecessor lane (the previous
+// border cell) already issued, so repeated unions do not queue same-address
+// atomics behind each other.
 __global__ __launch_bounds__(256) void k_frontier_merge(FGeom g, const int32_t* __restrict__ ftiles,
                                                         const unsigned long long* __restrict__ list_n,
                                                         const int32_t* __restrict__ tile_free,
@@ -418,54 +466,45 @@ __global__ __launch_bounds__(256) void k_frontier_merge(FGeom g, const int32_t* 
                                                         const long long* __restrict__ slot_label,
                                                         int32_t* slot_parent,
                                                         const unsigned long long* cnt) {
-  const int tid = threadIdx.x, lane = __lane_id();
-  const int64_t nft = (int64_t)*list_n;
-  for (int64_t jj = blockIdx.x; jj < nft; jj += gridDim.x) {
-    const int32_t tile = ftiles[jj];
-    const int64_t j = tile;
+  const int lane = __lane_id();
+  const int64_t nunits = 2 * (int64_t)*list_n;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t u = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); u < nunits; u += waves) {
+    const int32_t tile = __builtin_amdgcn_readfirstlane(ftiles[u >> 1]);
+    const bool right = (u & 1) == 0;
     const int32_t tx = tile % g.TX, ty = tile / g.TX;
-    const int32_t* bA = border + j * 256;
-    // candidate pairs of this lane: (sa, sb[0..2]); -1 = none
-    int32_t sa = -1, sb[3] = {-1, -1, -1};
-    if (tid < 64) {  // our last column vs the right neighbour's first column
-      sa = bA[3 * 64 + tid];
-      int32_t nb;
-      if (sa >= 0 && tx + 1 < g.TX && tile_free[nb = ty * g.TX + tx + 1] > 0) {
-        const int32_t* bB = border + (int64_t)nb * 256 + 2 * 64;
-        for (int d = -1; d <= 1; ++d)
-          if (tid + d >= 0 && tid + d < 64) sb[d + 1] = bB[tid + d];
-      }
-    } else if (tid < 128) {  // our last row vs the next tile row's first row
-      const int x = tid - 64;
-      sa = bA[1 * 64 + x];
-      int32_t nb;
-      if (sa >= 0 && ty + 1 < g.TY && tile_free[nb = (ty + 1) * g.TX + tx] > 0) {
-        const int32_t* bC = border + (int64_t)nb * 256;
-        for (int d = -1; d <= 1; ++d)
-          if (x + d >= 0 && x + d < 64) sb[d + 1] = bC[x + d];
-      }
-    } else if (tid == 128) {  // our (63,63) vs (tx+1,ty+1)'s (0,0)
-      sa = bA[1 * 64 + 63];
-      int32_t nb;
-      if (sa >= 0 && tx + 1 < g.TX && ty + 1 < g.TY && tile_free[nb = (ty + 1) * g.TX + tx + 1] > 0)
-        sb[1] = border[(int64_t)nb * 256 + 0];
-    } else if (tid == 129) {  // our (0,63) vs (tx-1,ty+1)'s (63,0)
-      sa = bA[1 * 64 + 0];
-      int32_t nb;
-      if (sa >= 0 && tx > 0 && ty + 1 < g.TY && tile_free[nb = (ty + 1) * g.TX + tx - 1] > 0)
-        sb[1] = border[(int64_t)nb * 256 + 63];
+    const int32_t* bA = border + (int64_t)tile * 256;
+    // this lane's border cell and the neighbour tile's (independent loads)
+    const int32_t nb = right ? (tx + 1 < g.TX ? ty * g.TX + tx + 1 : -1)
+                             : (ty + 1 < g.TY ? (ty + 1) * g.TX + tx : -1);
+    const int32_t sa = bA[(right ? 3 : 1) * 64 + lane];
+    const bool nb_ok = nb >= 0 && tile_free[nb] > 0;
+    // corners (edge 1 only): lane 63 -> the lower-right tile's (0,0),
+    // lane 0 -> the lower-left tile's (63,0)
+    int32_t nc = -1, cpos = 0;
+    if (!right && ty + 1 < g.TY) {
+      if (lane == 63 && tx + 1 < g.TX) { nc = (ty + 1) * g.TX + tx + 1; cpos = 0; }
+      if (lane == 0 && tx > 0) { nc = (ty + 1) * g.TX + tx - 1; cpos = 63; }
     }
-    // predecessor lane's pairs (lanes 0 of waves 0/1 start an edge: none)
+    const bool nc_ok = nc >= 0 && tile_free[nc] > 0;
+    // candidate pairs of this lane: (sa, sb[0..3]); -1 = none
+    int32_t sb[4] = {-1, -1, -1, -1};
+    if (sa >= 0 && nb_ok) {
+      const int32_t* bB = border + (int64_t)nb * 256 + (right ? 2 * 64 : 0);
+      for (int d = -1; d <= 1; ++d)
+        if (lane + d >= 0 && lane + d < 64) sb[d + 1] = bB[lane + d];
+    }
+    if (sa >= 0 && nc_ok) sb[3] = border[(int64_t)nc * 256 + cpos];
+    // predecessor lane's pairs (lane 0 starts an edge: none)
     const int32_t psa = __shfl_up(sa, 1);
     int32_t psb[3];
     for (int q = 0; q < 3; ++q) psb[q] = __shfl_up(sb[q], 1);
-    const bool has_prev = lane > 0 && tid < 128;
-    for (int q = 0; q < 3; ++q) {
+    for (int q = 0; q < 4; ++q) {
       const int32_t b = sb[q];
       if (sa < 0 || b < 0) continue;
       bool dup = false;
       for (int r = 0; r < q; ++r) dup |= sb[r] == b;
-      if (has_prev && psa == sa) dup |= (psb[0] == b) | (psb[1] == b) | (psb[2] == b);
+      if (lane > 0 && psa == sa) dup |= (psb[0] == b) | (psb[1] == b) | (psb[2] == b);
       if (!dup) dm_uf_unite(slot_parent, slot_label, sa, b);
     }
   }
