@@ -99,9 +99,7 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   int64_t act = std::min<int64_t>(g->NT, std::min<int64_t>(segs, (int64_t)S * side * side));
   if (act < 1) act = 1;
   if (act > g->act_cap) {
-    int rc = dev_alloc(&g->act_tiles, act, "active tiles");
-    if (!rc) rc = dev_alloc(&g->act_raw, act * kShards, "first-touch lists");
-    if (!rc) rc = dev_alloc(&g->act_cur, act, "active cursors");
+    int rc = dev_alloc(&g->act_raw, act * kShards, "first-touch lists");
     if (!rc) rc = dev_alloc(&g->litems, act, "light work items");
     if (rc) return rc;
     g->act_cap = act;
@@ -368,7 +366,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if ((rc = dev_alloc(&g->L, cells, "log-odds"))) return fail(rc);
   if ((rc = dev_alloc(&g->state, cells, "state"))) return fail(rc);
   if ((rc = dev_alloc(&g->tile_count, g->NT, "tile counts"))) return fail(rc);
-  if ((rc = dev_alloc(&g->tile_slot, g->NT, "tile slots"))) return fail(rc);
+  if ((rc = dev_alloc(&g->tile_cur, g->NT, "tile bin cursors"))) return fail(rc);
   if ((rc = dev_alloc(&g->tile_free, g->NT, "tile free counts"))) return fail(rc);
   if ((rc = dev_alloc(&g->cnt, CNT_N, "counters"))) return fail(rc);
   if ((rc = dev_alloc(&g->ish, 2 * kShards * kShardWords, "shard counters"))) return fail(rc);
@@ -401,9 +399,9 @@ int dm_destroy(dm_grid* g) {
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
-  dev_free(g->L); dev_free(g->state); dev_free(g->tile_count); dev_free(g->tile_slot);
+  dev_free(g->L); dev_free(g->state); dev_free(g->tile_count); dev_free(g->tile_cur);
   dev_free(g->tile_free); dev_free(g->cnt); dev_free(g->beams); dev_free(g->pieces);
-  dev_free(g->act_tiles); dev_free(g->act_cur); dev_free(g->trig);
+  dev_free(g->trig);
   dev_free(g->hitems); dev_free(g->litems); dev_free(g->heavy_list); dev_free(g->slabs);
   dev_free(g->pose4); dev_free(g->ranges); 
   dev_free(g->border); dev_free(g->ftiles); dev_free(g->slot_label); dev_free(g->slot_parent); dev_free(g->slot_root);

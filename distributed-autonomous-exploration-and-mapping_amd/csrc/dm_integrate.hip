@@ -205,19 +205,19 @@ __device__ inline void block_scan(const int64_t (&v)[K], int64_t (&excl)[K], int
 }
 
 constexpr int kPlanThreads = 1024;
-constexpr int kPlanPer = 8;  // active tiles per thread per round, loads batched in registers
+constexpr int kPlanPer = 4;  // active tiles per thread per round, loads batched in registers
 
 __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __restrict__ act_raw,
                                                        const unsigned long long* __restrict__ ish,
-                                                       int32_t* __restrict__ act_tiles, int32_t* __restrict__ tile_slot,
+                                                       int32_t* __restrict__ tile_cur,
                                                        const int32_t* __restrict__ tile_count,
-                                                       int32_t* __restrict__ act_cur,
                                                        int4* __restrict__ hitems, int4* __restrict__ litems,
                                                        int32_t* __restrict__ heavy_list,
                                                        unsigned long long* cnt) {
   __shared__ int64_t ws[17][4];
   __shared__ int32_t soff[kShards + 1];
   const int tid = threadIdx.x, lane = __lane_id();
+  DM_PH_INIT();
   if (tid < 64) {  // shard offsets: one wave, one load per lane, shuffle scan
     const int32_t c = tid < kShards ? (int32_t)min((unsigned long long)g.act_cap, ish[tid * kShardWords + SH_ACT]) : 0;
     int32_t incl = c;
@@ -229,6 +229,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __
     if (tid == kShards - 1) soff[kShards] = incl;
   }
   __syncthreads();
+  DM_PH(dm_phase_acc_integrate, 11);
   const int64_t n = min((int64_t)soff[kShards], (int64_t)g.act_cap);
   // compact the per-shard first-touch lists: active tile j -> tile.  The
   // shard of a thread's first j by binary search over the offsets (LDS
@@ -265,15 +266,14 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __
       v[3] += heavy ? 1 : 0;
     }
     int64_t ex[4], tot[4];
+    DM_PH(dm_phase_acc_integrate, 12);
     block_scan<4>(v, ex, tot, ws);
+    DM_PH(dm_phase_acc_integrate, 13);
     for (int k = 0; k < 4; ++k) ex[k] += carry[k];
 #pragma unroll
     for (int q = 0; q < kPlanPer; ++q) {
       if (t[q] < 0) continue;
-      const int64_t j = lo + q;
-      act_tiles[j] = t[q];
-      tile_slot[t[q]] = (int32_t)j;
-      act_cur[j] = (int32_t)ex[0];
+      tile_cur[t[q]] = (int32_t)ex[0];  // k_scatter's cursor: the tile's bin start
       if (c[q] > kChunk && c[q] <= kMedium) {
         // medium tile: one item, walked in rounds of kChunk, applied directly
         hitems[ex[1]++] = make_int4(t[q], (int32_t)ex[0], c[q], -1);
@@ -293,6 +293,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __
     }
     for (int k = 0; k < 4; ++k) carry[k] += tot[k];
     __syncthreads();  // ws is reused by the next round's scan
+    DM_PH(dm_phase_acc_integrate, 14);
   }
   if (tid == 0) {
     cnt[CNT_ACTIVE] = (unsigned long long)n;
@@ -301,6 +302,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __
     cnt[CNT_LITEMS] = (unsigned long long)carry[2];  // light items (= light tiles)
     cnt[CNT_HEAVY] = (unsigned long long)carry[3];   // heavy tiles
   }
+  DM_PH_FLUSH(dm_phase_acc_integrate);
 }
 
 // A piece as k_tile_accum consumes it: tile-local LDS addresses (pitch
@@ -319,8 +321,7 @@ __device__ inline void put_piece(const Geom& g, PackedPiece* pieces, int64_t idx
 // Pieces -> per-tile bins.  Same LDS histogram as k_beam_prep; one global
 // cursor bump per (block, tile), then LDS cursors place each piece.
 __global__ __launch_bounds__(256) void k_scatter(RayArgs a, Geom g, const Beam* __restrict__ beams,
-                                                 const int32_t* __restrict__ tile_slot,
-                                                 int32_t* act_cur, PackedPiece* __restrict__ pieces,
+                                                 int32_t* tile_cur, PackedPiece* __restrict__ pieces,
                                                  unsigned long long* cnt) {
   __shared__ int32_t hkey[kHash];
   __shared__ int32_t hcnt[kHash];
@@ -344,8 +345,7 @@ __global__ __launch_bounds__(256) void k_scatter(RayArgs a, Geom g, const Beam* 
         if (h >= 0) {
           atomicAdd(&hcnt[h], run.len);
         } else {  // table full: place the run's pieces straight from the global cursor
-          const int32_t slot = tile_slot[tile];
-          base = (slot >= 0 && slot < g.act_cap) ? atomicAdd(&act_cur[slot], run.len) : -1;
+          base = atomicAdd(&tile_cur[tile], run.len);
         }
       }
       h = __shfl(h, run.head_lane);
@@ -357,8 +357,7 @@ __global__ __launch_bounds__(256) void k_scatter(RayArgs a, Geom g, const Beam* 
   for (int e = tid; e < kHash; e += 256) {
     const int32_t tile = hkey[e];
     if (tile < 0) continue;
-    const int32_t slot = tile_slot[tile];
-    hbase[e] = (slot >= 0 && slot < g.act_cap) ? atomicAdd(&act_cur[slot], hcnt[e]) : -1;
+    hbase[e] = atomicAdd(&tile_cur[tile], hcnt[e]);
     hcnt[e] = 0;
   }
   __syncthreads();
@@ -808,13 +807,13 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "plan", &t);
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(kPlanThreads), 0, g->stream, ge, g->act_raw, g->ish, g->act_tiles,
-                     g->tile_slot, g->tile_count, g->act_cur, g->hitems, g->litems, g->heavy_list, g->cnt);
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(kPlanThreads), 0, g->stream, ge, g->act_raw, g->ish, g->tile_cur,
+                     g->tile_count, g->hitems, g->litems, g->heavy_list, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "scatter", &t);
   hipLaunchKernelGGL(k_scatter, dim3(nblk), dim3(256), 0, g->stream, a, ge, g->beams,
-                     g->tile_slot, g->act_cur, g->pieces, g->cnt);
+                     g->tile_cur, g->pieces, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   const int vec_ok = (g->W % 4 == 0) ? 1 : 0;

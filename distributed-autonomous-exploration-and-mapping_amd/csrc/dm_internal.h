@@ -92,7 +92,7 @@ struct dm_grid {
   float* L = nullptr;
   int8_t* state = nullptr;
   int32_t* tile_count = nullptr;
-  int32_t* tile_slot = nullptr;
+  int32_t* tile_cur = nullptr;   // [NT] k_scatter's bin cursor per active tile (k_plan)
   int32_t* tile_free = nullptr;
   unsigned long long* cnt = nullptr;  // CNT_N device counters
   unsigned long long* h_cnt = nullptr;  // pinned mirror
@@ -103,7 +103,6 @@ struct dm_grid {
   // integrate workspace
   Beam* beams = nullptr; int64_t beams_cap = 0;
   PackedPiece* pieces = nullptr; int64_t segs_cap = 0;  // ray pieces binned by tile
-  int32_t* act_tiles = nullptr; int32_t* act_cur = nullptr;
   int32_t* act_raw = nullptr;    // [kShards][act_cap] first-touch lists per shard
   int64_t act_cap = 0;
   int4* hitems = nullptr;        // heavy work items {tile, first piece, pieces, heavy ordinal}
