@@ -538,7 +538,7 @@ __device__ inline void finish_tile(const Geom& g, int32_t tile, int32_t T, int32
 //  * heavy item: adds its counts to the tile's slab (row-contiguous global
 //    atomics); k_heavy_apply applies the merged slab.
 // The next item's descriptor is loaded while the current one is processed.
-__global__ __launch_bounds__(kQuarter) void k_tile_accum(
+__global__ __launch_bounds__(kQuarter, 6) void k_tile_accum(
     Geom g, ApplyArgs p, const int4* __restrict__ hitems, const int4* __restrict__ litems,
     const PackedPiece* __restrict__ pieces, int32_t* tile_count, int32_t* tile_free,
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
