@@ -85,7 +85,10 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   const int64_t nb = (int64_t)S * N;
   const int64_t per_beam = 2 * (g->nmax / DM_TILE) + 8;
   if (nb > g->beams_cap) {
+    const int64_t blocks = ceil_div(nb, 256);
     int rc = dev_alloc(&g->beams, nb, "beams");
+    if (!rc) rc = dev_alloc(&g->blk_hist, blocks * 1024, "per-block tile histograms");
+    if (!rc) rc = dev_alloc(&g->blk_n, blocks, "per-block histogram sizes");
     if (rc) return rc;
     g->beams_cap = nb;
   }
@@ -400,7 +403,7 @@ int dm_destroy(dm_grid* g) {
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
   dev_free(g->L); dev_free(g->state); dev_free(g->tile_count); dev_free(g->tile_cur);
-  dev_free(g->tile_free); dev_free(g->cnt); dev_free(g->beams); dev_free(g->pieces);
+  dev_free(g->tile_free); dev_free(g->cnt); dev_free(g->beams); dev_free(g->blk_hist); dev_free(g->blk_n); dev_free(g->pieces);
   dev_free(g->trig);
   dev_free(g->hitems); dev_free(g->litems); dev_free(g->heavy_list); dev_free(g->slabs);
   dev_free(g->pose4); dev_free(g->ranges); 

@@ -119,9 +119,11 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
                                                    const double* __restrict__ trig,
                                                    Beam* __restrict__ beams, int32_t* tile_count,
                                                    int32_t* act_raw, unsigned long long* ish,
+                                                   int2* __restrict__ blk_hist, int32_t* __restrict__ blk_n,
                                                    unsigned long long* cnt) {
   __shared__ int32_t hkey[kHash];
   __shared__ int32_t hcnt[kHash];
+  __shared__ int32_t s_nh;
   const int tid = threadIdx.x;
   for (int e = tid; e < kHash; e += 256) { hkey[e] = -1; hcnt[e] = 0; }
   __syncthreads();
@@ -146,13 +148,20 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
       });
     }
   }
+  if (tid == 0) s_nh = 0;
   __syncthreads();
+  // flush the histogram, and keep it (compacted) for k_scatter: its single
+  // placement pass then needs no counting pass of its own
+  int2* my_hist = blk_hist + (int64_t)blockIdx.x * kHash;
   for (int e = tid; e < kHash; e += 256) {
     const int32_t tile = hkey[e];
     if (tile < 0) continue;
     const int32_t old = atomicAdd(&tile_count[tile], hcnt[e]);
     first_touch(g, tile, old, act_raw, ish, cnt);
+    my_hist[atomicAdd(&s_nh, 1)] = make_int2(tile, hcnt[e]);
   }
+  __syncthreads();
+  if (tid == 0) blk_n[blockIdx.x] = s_nh;
 }
 
 // Work plan for the apply phase (one block).  A tile's pieces are cut into
@@ -318,62 +327,46 @@ __device__ inline void put_piece(const Geom& g, PackedPiece* pieces, int64_t idx
   }
 }
 
-// Pieces -> per-tile bins.  Same LDS histogram as k_beam_prep; one global
-// cursor bump per (block, tile), then LDS cursors place each piece.
+// Pieces -> per-tile bins, in ONE enumeration pass: the workgroup's
+// (tile, count) histogram comes from k_beam_prep (same 256 beams), one
+// global cursor bump per histogram entry reserves the workgroup's range of
+// each tile's bin, LDS cursors place the pieces.  Runs whose tile is not in
+// the histogram (k_beam_prep's LDS table was full: those counted straight
+// into tile_count) bump the global cursor themselves.
 __global__ __launch_bounds__(256) void k_scatter(RayArgs a, Geom g, const Beam* __restrict__ beams,
-                                                 int32_t* tile_cur, PackedPiece* __restrict__ pieces,
-                                                 unsigned long long* cnt) {
+                                                 int32_t* tile_cur, const int2* __restrict__ blk_hist,
+                                                 const int32_t* __restrict__ blk_n,
+                                                 PackedPiece* __restrict__ pieces, unsigned long long* cnt) {
   __shared__ int32_t hkey[kHash];
   __shared__ int32_t hcnt[kHash];
   __shared__ int32_t hbase[kHash];
   const int tid = threadIdx.x;
   for (int e = tid; e < kHash; e += 256) { hkey[e] = -1; hcnt[e] = 0; }
-  __syncthreads();
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + tid;
   const int64_t nb = (int64_t)a.S * a.N;
   Beam bm;
   bm.flags = 0;
   if (b < nb) bm = beams[b];
+  const int32_t nh = blk_n[blockIdx.x];
+  __syncthreads();
+  const int2* my_hist = blk_hist + (int64_t)blockIdx.x * kHash;
+  for (int e = tid; e < nh; e += 256) {
+    const int2 te = my_hist[e];
+    const int h = hash_insert(hkey, te.x);  // the same entries fit: same table size
+    if (h >= 0) hbase[h] = atomicAdd(&tile_cur[te.x], te.y);
+  }
+  __syncthreads();
   const bool valid = (b < nb) && (bm.flags & 1);
   if (valid) {
     dm_for_each_piece(bm, g.r, [&](int32_t tile, int32_t k0, int32_t k1) {
       const LaneRun run = lane_run(tile);
-      int h = -1;
-      int32_t base = -1;
-      if (run.head) {
-        h = hash_insert(hkey, tile);
-        if (h >= 0) {
-          atomicAdd(&hcnt[h], run.len);
-        } else {  // table full: place the run's pieces straight from the global cursor
-          base = atomicAdd(&tile_cur[tile], run.len);
-        }
-      }
-      h = __shfl(h, run.head_lane);
-      base = __shfl(base, run.head_lane);
-      if (h < 0) put_piece(g, pieces, base >= 0 ? (int64_t)base + run.rank : -1, bm, tile, k0, k1, cnt);
-    });
-  }
-  __syncthreads();
-  for (int e = tid; e < kHash; e += 256) {
-    const int32_t tile = hkey[e];
-    if (tile < 0) continue;
-    hbase[e] = atomicAdd(&tile_cur[tile], hcnt[e]);
-    hcnt[e] = 0;
-  }
-  __syncthreads();
-  if (valid) {
-    dm_for_each_piece(bm, g.r, [&](int32_t tile, int32_t k0, int32_t k1) {
-      const LaneRun run = lane_run(tile);
-      int h = -1;
       int32_t pos = -1;
       if (run.head) {
-        h = hash_find(hkey, tile);
-        if (h >= 0 && hbase[h] >= 0) pos = hbase[h] + atomicAdd(&hcnt[h], run.len);
+        const int h = hash_find(hkey, tile);
+        pos = h >= 0 ? hbase[h] + atomicAdd(&hcnt[h], run.len) : atomicAdd(&tile_cur[tile], run.len);
       }
-      h = __shfl(h, run.head_lane);
       pos = __shfl(pos, run.head_lane);
-      if (h < 0) return;  // placed by the global path above
-      put_piece(g, pieces, pos >= 0 ? (int64_t)pos + run.rank : -1, bm, tile, k0, k1, cnt);
+      put_piece(g, pieces, (int64_t)pos + run.rank, bm, tile, k0, k1, cnt);
     });
   }
 }
@@ -803,7 +796,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   KernelTimer t;
   dm_timer_begin(g, "beam_prep", &t);
   hipLaunchKernelGGL(k_beam_prep, dim3(nblk), dim3(256), 0, g->stream, a, ge, d_pose4, d_ranges,
-                     d_trig, g->beams, g->tile_count, g->act_raw, g->ish, g->cnt);
+                     d_trig, g->beams, g->tile_count, g->act_raw, g->ish, g->blk_hist, g->blk_n, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "plan", &t);
@@ -813,7 +806,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "scatter", &t);
   hipLaunchKernelGGL(k_scatter, dim3(nblk), dim3(256), 0, g->stream, a, ge, g->beams,
-                     g->tile_cur, g->pieces, g->cnt);
+                     g->tile_cur, g->blk_hist, g->blk_n, g->pieces, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   const int vec_ok = (g->W % 4 == 0) ? 1 : 0;

@@ -102,6 +102,8 @@ struct dm_grid {
 
   // integrate workspace
   Beam* beams = nullptr; int64_t beams_cap = 0;
+  int2* blk_hist = nullptr;       // [beam blocks][1024] k_beam_prep's (tile, pieces) histogram
+  int32_t* blk_n = nullptr;       // [beam blocks] its entries
   PackedPiece* pieces = nullptr; int64_t segs_cap = 0;  // ray pieces binned by tile
   int32_t* act_raw = nullptr;    // [kShards][act_cap] first-touch lists per shard
   int64_t act_cap = 0;
