@@ -185,37 +185,29 @@ constexpr int kQuarter = 256;  // threads of an apply workgroup (= kChunk)
 static_assert(kChunk < 65536, "packed 16-bit LDS counts");
 static_assert(kChunk == kQuarter, "one piece per thread");
 
-template <int K>
-__device__ inline void block_scan(const int64_t (&v)[K], int64_t (&excl)[K], int64_t (&tot)[K],
-                                  int64_t (*ws)[K]) {
-  const int tid = threadIdx.x, lane = __lane_id(), wid = tid >> 6;
-  int64_t incl[K];
-  for (int q = 0; q < K; ++q) incl[q] = v[q];
+
+constexpr int kPlanThreads = 256;
+
+// Wave-aggregated bump allocation: every active lane gets v lane-exclusive
+// units from *counter; one atomic per wave (returns the wave's base).
+__device__ inline unsigned long long wave_alloc(unsigned long long* counter, unsigned long long v) {
+  const int lane = __lane_id();
+  unsigned long long incl = v;
   for (int d = 1; d < 64; d <<= 1) {
-    for (int q = 0; q < K; ++q) {
-      const int64_t t = __shfl_up(incl[q], d);
-      if (lane >= d) incl[q] += t;
-    }
+    const unsigned long long t = __shfl_up(incl, d);
+    if (lane >= d) incl += t;
   }
-  if (lane == 63) for (int q = 0; q < K; ++q) ws[wid][q] = incl[q];
-  __syncthreads();
-  if (tid == 0) {
-    int64_t run[K];
-    for (int q = 0; q < K; ++q) run[q] = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w)
-      for (int q = 0; q < K; ++q) { const int64_t t = ws[w][q]; ws[w][q] = run[q]; run[q] += t; }
-    for (int q = 0; q < K; ++q) ws[16][q] = run[q];
-  }
-  __syncthreads();
-  for (int q = 0; q < K; ++q) {
-    excl[q] = ws[wid][q] + incl[q] - v[q];
-    tot[q] = ws[16][q];
-  }
+  const unsigned long long total = __shfl(incl, 63);
+  unsigned long long base = 0;
+  if (lane == 63 && total) base = atomicAdd(counter, total);
+  return __shfl(base, 63) + incl - v;
 }
 
-constexpr int kPlanThreads = 1024;
-constexpr int kPlanPer = 4;  // active tiles per thread per round, loads batched in registers
-
+// Work plan for the apply phase, one thread per active tile and no global
+// scan: bin order does not matter, so each tile's bin (its pieces' range in
+// `pieces`) and its work items are bump-allocated with wave-aggregated
+// atomics (wave_alloc).  Writes k_scatter's bin cursor per tile and the
+// items; counters: pieces, heavy + medium items, light items, heavy tiles.
 __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __restrict__ act_raw,
                                                        const unsigned long long* __restrict__ ish,
                                                        int32_t* __restrict__ tile_cur,
@@ -223,11 +215,9 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __
                                                        int4* __restrict__ hitems, int4* __restrict__ litems,
                                                        int32_t* __restrict__ heavy_list,
                                                        unsigned long long* cnt) {
-  __shared__ int64_t ws[17][4];
   __shared__ int32_t soff[kShards + 1];
   const int tid = threadIdx.x, lane = __lane_id();
-  DM_PH_INIT();
-  if (tid < 64) {  // shard offsets: one wave, one load per lane, shuffle scan
+  if (tid < 64) {  // shard offsets of the first-touch lists (every workgroup)
     const int32_t c = tid < kShards ? (int32_t)min((unsigned long long)g.act_cap, ish[tid * kShardWords + SH_ACT]) : 0;
     int32_t incl = c;
     for (int d = 1; d < 64; d <<= 1) {
@@ -238,80 +228,45 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __
     if (tid == kShards - 1) soff[kShards] = incl;
   }
   __syncthreads();
-  DM_PH(dm_phase_acc_integrate, 11);
   const int64_t n = min((int64_t)soff[kShards], (int64_t)g.act_cap);
-  // compact the per-shard first-touch lists: active tile j -> tile.  The
-  // shard of a thread's first j by binary search over the offsets (LDS
-  // reads are dependent: 5 steps, not a 32-step scan), then incrementally.
-  int64_t carry[4] = {0, 0, 0, 0};
-  for (int64_t base = 0; base < n; base += (int64_t)kPlanThreads * kPlanPer) {
-    const int64_t lo = base + (int64_t)tid * kPlanPer;
-    int sh = 0;
-    {
-      int a = 0, b = kShards - 1;  // largest shard with soff[shard] <= lo
+  if (blockIdx.x == 0 && tid == 0) cnt[CNT_ACTIVE] = (unsigned long long)n;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x + (tid & ~63); j0 < n; j0 += stride) {
+    const int64_t j = j0 + lane;
+    int32_t t = -1, c = 0;
+    if (j < n) {
+      int a = 0, b = kShards - 1;  // largest shard with soff[shard] <= j
       while (a < b) {
         const int mid = (a + b + 1) >> 1;
-        if (soff[mid] <= lo) a = mid; else b = mid - 1;
+        if (soff[mid] <= j) a = mid; else b = mid - 1;
       }
-      sh = a;
+      t = act_raw[(int64_t)a * g.act_cap + (j - soff[a])];
+      c = tile_count[t];
     }
-    int32_t t[kPlanPer], c[kPlanPer];
-#pragma unroll
-    for (int q = 0; q < kPlanPer; ++q) {
-      const int64_t j = lo + q;
-      while (sh + 1 < kShards && soff[sh + 1] <= j) ++sh;
-      t[q] = j < n ? act_raw[(int64_t)sh * g.act_cap + (j - soff[sh])] : -1;
+    const bool heavy = c > kMedium;
+    const bool medium = c > kChunk && !heavy;
+    const bool light = t >= 0 && c <= kChunk;
+    const int32_t nh_items = heavy ? (c + kChunk - 1) / kChunk : (medium ? 1 : 0);
+    const unsigned long long p0 = wave_alloc(&cnt[CNT_SEGS], (unsigned long long)c);
+    const unsigned long long hi = wave_alloc(&cnt[CNT_ITEMS], (unsigned long long)nh_items);
+    const unsigned long long li = wave_alloc(&cnt[CNT_LITEMS], light ? 1ull : 0ull);
+    const unsigned long long ho = wave_alloc(&cnt[CNT_HEAVY], heavy ? 1ull : 0ull);
+    if (t < 0) continue;
+    tile_cur[t] = (int32_t)p0;  // k_scatter's cursor: the tile's bin start
+    if (light) {
+      litems[li] = make_int4(t, (int32_t)p0, c, -1);
+    } else if (medium) {  // one item, walked in rounds of kChunk, applied directly
+      hitems[hi] = make_int4(t, (int32_t)p0, c, -1);
+    } else {
+      // a cell's count in this call is at most the tile's piece count: below
+      // 65536 the slab is packed (hits << 16 | misses, one word per cell)
+      const int32_t wide = c >= 65536 ? 1 : 0;
+      heavy_list[ho] = t | (wide << 31);
+      for (int32_t q = 0; q < nh_items; ++q)
+        hitems[hi + q] = make_int4(t, (int32_t)p0 + q * kChunk, min(kChunk, c - q * kChunk),
+                                   (int32_t)(2 * ho + wide));
     }
-#pragma unroll
-    for (int q = 0; q < kPlanPer; ++q) c[q] = t[q] >= 0 ? tile_count[t[q]] : 0;
-    int64_t v[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int q = 0; q < kPlanPer; ++q) {
-      const bool heavy = c[q] > kMedium;
-      const bool medium = c[q] > kChunk && !heavy;
-      v[0] += c[q];
-      v[1] += heavy ? (c[q] + kChunk - 1) / kChunk : (medium ? 1 : 0);
-      v[2] += (t[q] >= 0 && c[q] <= kChunk) ? 1 : 0;
-      v[3] += heavy ? 1 : 0;
-    }
-    int64_t ex[4], tot[4];
-    DM_PH(dm_phase_acc_integrate, 12);
-    block_scan<4>(v, ex, tot, ws);
-    DM_PH(dm_phase_acc_integrate, 13);
-    for (int k = 0; k < 4; ++k) ex[k] += carry[k];
-#pragma unroll
-    for (int q = 0; q < kPlanPer; ++q) {
-      if (t[q] < 0) continue;
-      tile_cur[t[q]] = (int32_t)ex[0];  // k_scatter's cursor: the tile's bin start
-      if (c[q] > kChunk && c[q] <= kMedium) {
-        // medium tile: one item, walked in rounds of kChunk, applied directly
-        hitems[ex[1]++] = make_int4(t[q], (int32_t)ex[0], c[q], -1);
-      } else if (c[q] > kChunk) {
-        // a cell's count in this call is at most the tile's piece count: below
-        // 65536 the slab is packed (hits << 16 | misses, one word per cell)
-        const int32_t wide = c[q] >= 65536 ? 1 : 0;
-        heavy_list[ex[3]] = t[q] | (wide << 31);
-        for (int32_t p0 = 0; p0 < c[q]; p0 += kChunk)
-          hitems[ex[1]++] = make_int4(t[q], (int32_t)ex[0] + p0, min(kChunk, c[q] - p0),
-                                      (int32_t)(2 * ex[3] + wide));
-        ++ex[3];
-      } else {
-        litems[ex[2]++] = make_int4(t[q], (int32_t)ex[0], c[q], -1);
-      }
-      ex[0] += c[q];
-    }
-    for (int k = 0; k < 4; ++k) carry[k] += tot[k];
-    __syncthreads();  // ws is reused by the next round's scan
-    DM_PH(dm_phase_acc_integrate, 14);
   }
-  if (tid == 0) {
-    cnt[CNT_ACTIVE] = (unsigned long long)n;
-    cnt[CNT_SEGS] = (unsigned long long)carry[0];
-    cnt[CNT_ITEMS] = (unsigned long long)carry[1];   // heavy items
-    cnt[CNT_LITEMS] = (unsigned long long)carry[2];  // light items (= light tiles)
-    cnt[CNT_HEAVY] = (unsigned long long)carry[3];   // heavy tiles
-  }
-  DM_PH_FLUSH(dm_phase_acc_integrate);
 }
 
 // A piece as k_tile_accum consumes it: tile-local LDS addresses (pitch
@@ -800,7 +755,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "plan", &t);
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(kPlanThreads), 0, g->stream, ge, g->act_raw, g->ish, g->tile_cur,
+  hipLaunchKernelGGL(k_plan, dim3(grid_for(g->act_cap, kPlanThreads, 256)), dim3(kPlanThreads), 0, g->stream, ge, g->act_raw, g->ish, g->tile_cur,
                      g->tile_count, g->hitems, g->litems, g->heavy_list, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
