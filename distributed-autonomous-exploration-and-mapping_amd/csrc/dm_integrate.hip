@@ -487,17 +487,17 @@ __device__ inline void finish_tile(const Geom& g, int32_t tile, int32_t T, int32
 //    atomics); k_heavy_apply applies the merged slab.
 // The next item's descriptor is loaded while the current one is processed.
 __global__ __launch_bounds__(kQuarter, 6) void k_tile_accum(
-    Geom g, ApplyArgs p, const int4* __restrict__ hitems, const int4* __restrict__ litems,
-    const PackedPiece* __restrict__ pieces, int32_t* tile_count, int32_t* tile_free,
+    Geom g, ApplyArgs p, const int4* __restrict__ list_a, int cnt_a, const int4* __restrict__ list_b,
+    int cnt_b, const PackedPiece* __restrict__ pieces, int32_t* tile_count, int32_t* tile_free,
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
     const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok) {
   __shared__ uint32_t tl[kTileWords];
   __shared__ int32_t s_T, s_free;
   __shared__ uint32_t s_U;
   const int tid = threadIdx.x, lane = lane_id();
-  const int64_t HI = (int64_t)cnt[CNT_ITEMS], LI = (int64_t)cnt[CNT_LITEMS];
+  const int64_t HI = (int64_t)cnt[cnt_a], LI = cnt_b >= 0 ? (int64_t)cnt[cnt_b] : 0;
   const int64_t n_items = HI + LI;
-  auto item_of = [&](int64_t it) { return it < HI ? hitems[it] : litems[it - HI]; };
+  auto item_of = [&](int64_t it) { return it < HI ? list_a[it] : list_b[it - HI]; };
   int4 next = make_int4(0, 0, 0, -1);
   if ((int64_t)blockIdx.x < n_items) next = item_of(blockIdx.x);
   DM_PH_INIT();
@@ -579,62 +579,90 @@ __global__ __launch_bounds__(kQuarter, 6) void k_tile_accum(
 }
 
 // Heavy tiles: apply the merged slab counts, then clear the slab and the
-// tile's piece count for the next call.
+// tile's piece count for the next call.  Four workgroups per heavy tile, one
+// per 16-row quarter (a heavy tile is one of a few dozen: the kernel's time is
+// one workgroup's latency chain, which a quarter cuts to 4 cells per thread).
+// Thread tid takes cell (row 4k + tid / 64, column tid % 64) of its quarter:
+// each wave instruction touches 256 contiguous slab bytes, the full-rate shape
+// for the memory-side atomics (lanes strided over rows run many times slower:
+// MI355X_MICROARCH.md §Global atomics), and 256 contiguous bytes of L.
 __global__ __launch_bounds__(kQuarter) void k_heavy_apply(
     Geom g, ApplyArgs p, const int32_t* __restrict__ heavy_list, int32_t* tile_count, int32_t* tile_free,
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
-    const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok) {
+    const unsigned long long* __restrict__ cnt, unsigned long long* ish) {
   __shared__ int32_t s_T, s_free;
   __shared__ uint32_t s_U;
+  constexpr int kQ = DM_TS * DM_TS / 4;  // cells per quarter
   const int tid = threadIdx.x;
-  const int64_t nh = (int64_t)cnt[CNT_HEAVY];
+  const int64_t nq = 4 * (int64_t)cnt[CNT_HEAVY];
   DM_PH_INIT();
-  for (int64_t h = blockIdx.x; h < nh; h += gridDim.x) {
+  for (int64_t it = blockIdx.x; it < nq; it += gridDim.x) {
+    const int64_t h = it >> 2;
+    const int q = (int)(it & 3);
     const int32_t hl = __builtin_amdgcn_readfirstlane(heavy_list[h]);
     const int32_t tile = hl & 0x7FFFFFFF;
     const bool wide = hl < 0;
-    const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
-    uint32_t* sh = slabs + h * (2 * DM_TS * DM_TS);
-    const int cx = (tid & 15) * 4;
+    const int32_t x = (tile % g.r.TX) * DM_TS + (tid & 63);
+    const int32_t yq = (tile / g.r.TX) * DM_TS + q * (DM_TS / 4) + (tid >> 6);
+    uint32_t* sh = slabs + h * (2 * DM_TS * DM_TS) + q * kQ + tid;
     // read-and-clear with atomics: the slab was only ever written by the
-    // items' device-scope atomics, so its lines live at the memory-side
-    // coherence point; exchanging them there avoids a plain-load round trip
-    // plus a clearing store per word
-    uint4 hv[4], mv[4];
+    // items' device-scope atomics, which execute at the memory side, so the
+    // exchange reads the merged counts there and leaves no stale L2 line
+    uint32_t hc[4], mc[4];
+    float lv[4];
+    int8_t sv[4];
+    // L / state first: their latency then overlaps the exchanges'
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int e0 = ((tid >> 4) + 16 * rr) * DM_TS + cx;
-      uint32_t a[4], m[4];
-      for (int e = 0; e < 4; ++e) a[e] = atomicExch(&sh[e0 + e], 0u);
-      if (wide) {
-        for (int e = 0; e < 4; ++e) m[e] = atomicExch(&sh[DM_TS * DM_TS + e0 + e], 0u);
-      } else {  // packed: split the word
-        for (int e = 0; e < 4; ++e) { m[e] = a[e] & 0xFFFFu; a[e] >>= 16; }
+    for (int k = 0; k < 4; ++k) {
+      const int32_t y = yq + 4 * k;
+      lv[k] = 0.0f;
+      sv[k] = 0;
+      if (y < g.r.R && x < g.r.W) {
+        lv[k] = L[(int64_t)y * g.r.W + x];
+        sv[k] = state[(int64_t)y * g.r.W + x];
       }
-      hv[rr] = make_uint4(a[0], a[1], a[2], a[3]);
-      mv[rr] = make_uint4(m[0], m[1], m[2], m[3]);
     }
-    CellRows<4> cells;
-    cells.prefetch(g, tx0, ty0, tid >> 4, 16, cx, L, state, vec_ok);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hc[k] = atomicExch(sh + k * kQuarter, 0u);
+      if (wide) mc[k] = atomicExch(sh + DM_TS * DM_TS + k * kQuarter, 0u);
+    }
     if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; }
     __syncthreads();
     DM_PH(dm_phase_acc_integrate, 8);
-    DM_PH(dm_phase_acc_integrate, 8);
-    cells.apply(g, p, tx0, ty0, tid >> 4, 16, cx, L, state,
-                [&](int ly, uint32_t* h4, uint32_t* m4) {
-                  const int rr = ly >> 4;
-                  const uint4 a = hv[rr], b = mv[rr];
-                  h4[0] = a.x; h4[1] = a.y; h4[2] = a.z; h4[3] = a.w;
-                  m4[0] = b.x; m4[1] = b.y; m4[2] = b.z; m4[3] = b.w;
-                },
-                &s_T, &s_free, &s_U);
+    int32_t dT = 0, dFree = 0;
+    uint32_t dU = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t hk = hc[k], mk;
+      if (wide) {
+        mk = mc[k];
+      } else {  // packed: split the word
+        mk = hk & 0xFFFFu;
+        hk >>= 16;
+      }
+      const int32_t y = yq + 4 * k;
+      if ((hk | mk) == 0u || y >= g.r.R || x >= g.r.W) continue;
+      const int64_t i = (int64_t)y * g.r.W + x;
+      const float nl = apply_one(p, lv[k], hk, mk);
+      const int8_t ns = state_of(p, nl);
+      L[i] = nl;
+      state[i] = ns;
+      dU += hk + mk;
+      dT += 1;
+      dFree += (ns == 0) - (sv[k] == 0);
+    }
+    if (dT) atomicAdd(&s_T, dT);
+    if (dFree) atomicAdd(&s_free, dFree);
+    if (dU) atomicAdd(&s_U, dU);
     __syncthreads();
     DM_PH(dm_phase_acc_integrate, 9);
-    DM_PH(dm_phase_acc_integrate, 9);
-    if (tid == 0) finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
+    if (tid == 0) {
+      finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
+    }
     __syncthreads();
     DM_PH(dm_phase_acc_integrate, 10);
-    DM_PH_COUNT(dm_phase_acc_integrate, 20, 1);
+    DM_PH_COUNT(dm_phase_acc_integrate, 20, q == 0);
   }
   DM_PH_FLUSH(dm_phase_acc_integrate);
 }
@@ -755,8 +783,9 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "plan", &t);
-  hipLaunchKernelGGL(k_plan, dim3(grid_for(g->act_cap, kPlanThreads, 256)), dim3(kPlanThreads), 0, g->stream, ge, g->act_raw, g->ish, g->tile_cur,
-                     g->tile_count, g->hitems, g->litems, g->heavy_list, g->cnt);
+  hipLaunchKernelGGL(k_plan, dim3(grid_for(g->act_cap, kPlanThreads, 256)), dim3(kPlanThreads), 0, g->stream,
+                     ge, g->act_raw, g->ish, g->tile_cur, g->tile_count, g->hitems, g->litems,
+                     g->heavy_list, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "scatter", &t);
@@ -765,16 +794,18 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   const int vec_ok = (g->W % 4 == 0) ? 1 : 0;
+  // heavy chunks and medium tiles first (the long items), then the light
+  // tiles; k_heavy_apply then applies the heavy tiles' merged slabs
   dm_timer_begin(g, "tile_accum", &t);
   hipLaunchKernelGGL(k_tile_accum, dim3(grid_for(g->hitem_cap + g->act_cap, 1, 2048)), dim3(kQuarter), 0,
-                     g->stream, ge, make_apply(g), g->hitems, g->litems, g->pieces, g->tile_count,
-                     g->tile_free, g->slabs, g->L, g->state, g->cnt, g->ish, vec_ok);
+                     g->stream, ge, make_apply(g), g->hitems, (int)CNT_ITEMS, g->litems, (int)CNT_LITEMS,
+                     g->pieces, g->tile_count, g->tile_free, g->slabs, g->L, g->state, g->cnt, g->ish, vec_ok);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "heavy_apply", &t);
-  hipLaunchKernelGGL(k_heavy_apply, dim3(grid_for(g->heavy_cap, 1, 1024)), dim3(kQuarter), 0, g->stream, ge,
+  hipLaunchKernelGGL(k_heavy_apply, dim3(grid_for(4 * g->heavy_cap, 1, 1024)), dim3(kQuarter), 0, g->stream, ge,
                      make_apply(g), g->heavy_list, g->tile_count, g->tile_free, g->slabs, g->L, g->state,
-                     g->cnt, g->ish, vec_ok);
+                     g->cnt, g->ish);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   return DM_OK;
