@@ -389,6 +389,8 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if ((rc = dev_alloc(&g->m_cnt, 4, "merge counters"))) return fail(rc);
   e = hipHostMalloc((void**)&g->h_mcnt, sizeof(unsigned long long) * 4, hipHostMallocDefault);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipHostMalloc(merge counters)"));
+  e = hipDeviceGetAttribute(&g->n_cu, hipDeviceAttributeMultiprocessorCount, device);
+  if (e != hipSuccess) return fail(dm_hip_check(e, "hipDeviceGetAttribute(multiprocessor count)"));
   e = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate"));
   g->own_stream = true;

@@ -754,8 +754,9 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));
   KernelTimer t;
   const int nft_grid = grid_for(g->NT, 1, 2048);
+  const int ftile_grid = grid_for(g->NT, 1, 8192);
   dm_timer_begin(g, "frontier_tile", &t);
-  hipLaunchKernelGGL(k_frontier_tile, dim3(nft_grid), dim3(kFT), 0, g->stream, fg, g->state,
+  hipLaunchKernelGGL(k_frontier_tile, dim3(ftile_grid), dim3(kFT), 0, g->stream, fg, g->state,
                      g->halo, g->ftiles, list_n, g->border, g->slot_label, g->slot_parent, g->slot_own,
                      g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh);
   dm_timer_end(g, &t);

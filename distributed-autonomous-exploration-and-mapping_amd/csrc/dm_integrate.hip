@@ -330,11 +330,14 @@ struct ApplyArgs {
   float l_occ, l_free, l_min, l_max, occ_t, free_t;
 };
 
+// SPEC a7 as selects (no branches), lowest priority first: L == 0 -> -1,
+// else L >= occ_t -> 100, else L <= free_t -> 0, else -1.
 __device__ inline int8_t state_of(const ApplyArgs& p, float L) {
-  if (L == 0.0f) return -1;
-  if (L >= p.occ_t) return 100;
-  if (L <= p.free_t) return 0;
-  return -1;
+  int32_t r = -1;
+  r = L <= p.free_t ? 0 : r;
+  r = L >= p.occ_t ? 100 : r;
+  r = L == 0.0f ? -1 : r;
+  return (int8_t)r;
 }
 
 // SPEC a6 in this exact op order (no FMA: -ffp-contract=off).
@@ -359,18 +362,19 @@ struct CellRows {
   char4 s[ROWS];
   bool vec;
 
+  // Unconditional loads (cells outside the map, or a ragged column that the
+  // apply reads cell by cell, load the map's first cells instead and are
+  // ignored): a fixed number of loads per thread lets the compiler wait for
+  // the pieces issued before them with vmcnt(N) instead of vmcnt(0).
   __device__ void prefetch(const Geom& g, int32_t tx0, int32_t ty0, int ly0, int dly, int cx,
                            const float* __restrict__ L, const int8_t* __restrict__ state, int vec_ok) {
     vec = vec_ok && tx0 + cx + 4 <= g.r.W;
-    if (!vec) return;
 #pragma unroll
     for (int rr = 0; rr < ROWS; ++rr) {
       const int32_t y = ty0 + ly0 + rr * dly;
-      if (y < g.r.R) {
-        const int64_t base = (int64_t)y * g.r.W + tx0 + cx;
-        l[rr] = *reinterpret_cast<const float4*>(L + base);
-        s[rr] = *reinterpret_cast<const char4*>(state + base);
-      }
+      const int64_t base = (vec && y < g.r.R) ? (int64_t)y * g.r.W + tx0 + cx : 0;
+      l[rr] = *reinterpret_cast<const float4*>(L + base);
+      s[rr] = *reinterpret_cast<const char4*>(state + base);
     }
   }
 
@@ -391,17 +395,20 @@ struct CellRows {
       if (((h4[0] | m4[0]) | (h4[1] | m4[1]) | (h4[2] | m4[2]) | (h4[3] | m4[3])) == 0u) continue;
       const int64_t base = (int64_t)y * g.r.W + tx0 + cx;
       if (vec) {
+        // branch-free per cell: untouched cells keep their values
         float lv[4] = {l[rr].x, l[rr].y, l[rr].z, l[rr].w};
         int8_t sv[4] = {(int8_t)s[rr].x, (int8_t)s[rr].y, (int8_t)s[rr].z, (int8_t)s[rr].w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          if ((h4[e] | m4[e]) == 0u) continue;
-          dU += h4[e] + m4[e];
+          const bool hit = (h4[e] | m4[e]) != 0u;
           const int8_t old = sv[e];
-          lv[e] = apply_one(p, lv[e], h4[e], m4[e]);
-          sv[e] = state_of(p, lv[e]);
-          dT += 1;
-          dFree += (sv[e] == 0) - (old == 0);
+          const float nl = apply_one(p, lv[e], h4[e], m4[e]);
+          const int8_t ns = state_of(p, nl);
+          lv[e] = hit ? nl : lv[e];
+          sv[e] = hit ? ns : old;
+          dU += h4[e] + m4[e];
+          dT += hit ? 1 : 0;
+          dFree += hit ? (int32_t)(ns == 0) - (int32_t)(old == 0) : 0;
         }
         *reinterpret_cast<float4*>(L + base) = make_float4(lv[0], lv[1], lv[2], lv[3]);
         *reinterpret_cast<char4*>(state + base) = make_char4(sv[0], sv[1], sv[2], sv[3]);
@@ -479,14 +486,21 @@ __device__ inline void finish_tile(const Geom& g, int32_t tile, int32_t T, int32
 
 // Per-cell hit/miss counts never touch HBM: a 256-thread workgroup takes one
 // work item (<= kChunk pieces of one tile, one piece per thread), gathers
-// them in a packed LDS count tile (hits << 16 | misses) with wave_pieces,
+// them in a packed LDS count tile (hits << 16 | misses) with walk_piece,
 // and then
-//  * light item (the whole tile): applies the log-odds update to the tile's
-//    cells right away, from L / state loaded before the accumulation;
+//  * light / medium item (the whole tile): applies the log-odds update to the
+//    tile's cells right away, from L / state loaded before the accumulation;
 //  * heavy item: adds its counts to the tile's slab (row-contiguous global
 //    atomics); k_heavy_apply applies the merged slab.
-// The next item's descriptor is loaded while the current one is processed.
-__global__ __launch_bounds__(kQuarter, 6) void k_tile_accum(
+// The next item's pieces are loaded right after this item's apply, its
+// cells (unconditional loads: a fixed count, so the walk waits for the pieces
+// alone with vmcnt(N)) at the top of its iteration, in flight during its
+// walk.  The per-item statistics stay in thread 0's registers (one flush per
+// workgroup) and a light tile's free count is a plain read-modify-write (one
+// workgroup owns the tile), so no memory-side atomic sits in front of the
+// next item's loads in the wave's in-order vmcnt queue.
+constexpr int kAccumPerCu = 6;  // resident k_tile_accum workgroups per CU (4 waves each)
+__global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     Geom g, ApplyArgs p, const int4* __restrict__ list_a, int cnt_a, const int4* __restrict__ list_b,
     int cnt_b, const PackedPiece* __restrict__ pieces, int32_t* tile_count, int32_t* tile_free,
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
@@ -497,34 +511,42 @@ __global__ __launch_bounds__(kQuarter, 6) void k_tile_accum(
   const int tid = threadIdx.x, lane = lane_id();
   const int64_t HI = (int64_t)cnt[cnt_a], LI = cnt_b >= 0 ? (int64_t)cnt[cnt_b] : 0;
   const int64_t n_items = HI + LI;
-  auto item_of = [&](int64_t it) { return it < HI ? list_a[it] : list_b[it - HI]; };
-  int4 next = make_int4(0, 0, 0, -1);
-  if ((int64_t)blockIdx.x < n_items) next = item_of(blockIdx.x);
+  const int64_t G = gridDim.x;
+  if ((int64_t)blockIdx.x >= n_items) return;
+  auto item_of = [&](int64_t it) {
+    return it < n_items ? (it < HI ? list_a[it] : list_b[it - HI]) : make_int4(0, 0, 0, -1);
+  };
+  const int cx = (tid & 15) * 4;
+  __shared__ unsigned long long s_accT, s_accU;  // this workgroup's light-tile totals
+  // the first item's loads
+  int4 info = item_of(blockIdx.x);
+  int4 next = item_of(blockIdx.x + G);
+  PackedPiece mine;
+  CellRows<4> cells;
+  int32_t tfree;
+  auto issue_pieces = [&](const int4& d) {
+    const int32_t c0 = __builtin_amdgcn_readfirstlane(d.y);
+    const int32_t c = __builtin_amdgcn_readfirstlane(d.z);
+    // lanes past the item's pieces re-read its last one (past the list's end:
+    // piece 0); unconditional, so the loop carries no phi of the old pieces
+    mine = pieces[c0 + min(tid, max(c - 1, 0))];
+  };
+  issue_pieces(info);
+  for (int e = tid; e < kTileWords; e += kQuarter) tl[e] = 0u;
+  if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; s_accT = 0ull; s_accU = 0ull; }
+  __syncthreads();
   DM_PH_INIT();
-  for (int64_t it = blockIdx.x; it < n_items; it += gridDim.x) {
-    const int4 info = next;
-    if (it + gridDim.x < n_items) next = item_of(it + gridDim.x);
+  for (int64_t it = blockIdx.x; it < n_items; it += G) {
     // the descriptor is workgroup-uniform: scalar registers, scalar branches
     const int32_t tile = __builtin_amdgcn_readfirstlane(info.x);
     const int32_t c0 = __builtin_amdgcn_readfirstlane(info.y);
     const int32_t c = __builtin_amdgcn_readfirstlane(info.z);
     const int32_t heavy = __builtin_amdgcn_readfirstlane(info.w);
     const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
-    PackedPiece mine = no_piece();
-    if (tid < c) mine = pieces[c0 + tid];  // first round (light / medium) or the heavy chunk
-    CellRows<4> cells;
-    const int cx = (tid & 15) * 4;
-    if (heavy < 0) cells.prefetch(g, tx0, ty0, tid >> 4, 16, cx, L, state, vec_ok);
-    for (int e = tid; e < kTileWords; e += kQuarter) tl[e] = 0u;
-    if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; }
-    __syncthreads();
     DM_PH(dm_phase_acc_integrate, 0);
     if (heavy >= 0) {
-      // heavy (a sensor's tile): the pieces all start at the sensor's cell,
-      // so a plain per-thread walk would pile a wave's atomics onto one LDS
-      // word.  Each thread walks its piece from a staggered start step
-      // (lane mod length) and wraps around: at any step the wave's lanes
-      // sit at different distances from the sensor, on different cells.
+      // heavy (a sensor's tile): the pieces all start at the sensor's cell;
+      // walk_piece's staggered start keeps a wave's lanes on different cells
       walk_piece(tl, mine, tid < c, lane);
       __syncthreads();
       DM_PH(dm_phase_acc_integrate, 1);
@@ -544,36 +566,52 @@ __global__ __launch_bounds__(kQuarter, 6) void k_tile_accum(
           if (v) atomicAdd(&sh[e], v);
         }
       }
-      __syncthreads();
       DM_PH(dm_phase_acc_integrate, 2);
-      continue;
-    }
-    // light / medium: one piece per thread per round, walked cell by cell
-    // (PieceCursor: no division per cell); the wave's trip count is its
-    // longest piece
-    for (int32_t r0 = 0; r0 < c; r0 += kChunk) {
-      if (r0 > 0) {
-        mine = no_piece();
-        if (r0 + tid < c) mine = pieces[c0 + r0 + tid];
+    } else {
+      // light / medium: one piece per thread per round (medium tiles walk
+      // their later rounds with in-loop loads); the cells' loads fly during
+      // the walk
+      tfree = tile_free[tile];
+      cells.prefetch(g, tx0, ty0, tid >> 4, 16, cx, L, state, vec_ok);
+      walk_piece(tl, mine, tid < c, lane);
+      for (int32_t r0 = kChunk; r0 < c; r0 += kChunk) {
+        const PackedPiece more = r0 + tid < c ? pieces[c0 + r0 + tid] : no_piece();
+        walk_piece(tl, more, r0 + tid < c, lane);
       }
-      walk_piece(tl, mine, r0 + tid < c, lane);
+      __syncthreads();
+      DM_PH(dm_phase_acc_integrate, 3);
+      DM_PH_COUNT(dm_phase_acc_integrate, 16, 1);
+      DM_PH_COUNT(dm_phase_acc_integrate, 18, c);
+      cells.apply(g, p, tx0, ty0, tid >> 4, 16, cx, L, state,
+                  [&](int ly, uint32_t* h4, uint32_t* m4) {
+                    for (int e = 0; e < 4; ++e) {
+                      const uint32_t v = tl[ly * kLdsPitch + cx + e];
+                      h4[e] = v >> 16;
+                      m4[e] = v & 0xFFFFu;
+                    }
+                  },
+                  &s_T, &s_free, &s_U);
+      DM_PH(dm_phase_acc_integrate, 4);
     }
     __syncthreads();
-    DM_PH(dm_phase_acc_integrate, 3);
-    DM_PH_COUNT(dm_phase_acc_integrate, 16, 1);
-    DM_PH_COUNT(dm_phase_acc_integrate, 18, c);
-    cells.apply(g, p, tx0, ty0, tid >> 4, 16, cx, L, state,
-                [&](int ly, uint32_t* h4, uint32_t* m4) {
-                  for (int e = 0; e < 4; ++e) {
-                    const uint32_t v = tl[ly * kLdsPitch + cx + e];
-                    h4[e] = v >> 16;
-                    m4[e] = v & 0xFFFFu;
-                  }
-                },
-                &s_T, &s_free, &s_U);
+    if (tid == 0 && heavy < 0) {
+      s_accT += (unsigned long long)s_T;
+      s_accU += (unsigned long long)s_U;
+      if (s_free) tile_free[tile] = tfree + s_free;
+      tile_count[tile] = 0;  // ready for the next call
+    }
+    // the next item: its pieces go out now, ahead of its walk
+    info = next;
+    next = item_of(it + 2 * G);
+    issue_pieces(info);
+    for (int e = tid; e < kTileWords; e += kQuarter) tl[e] = 0u;
+    if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; }
     __syncthreads();
-    DM_PH(dm_phase_acc_integrate, 4);
-    if (tid == 0) finish_tile(g, tile, s_T, s_free, s_U, false, tile_count, tile_free, ish);
+  }
+  if (tid == 0) {
+    unsigned long long* sh = ish + (blockIdx.x % kShards) * kShardWords;
+    if (s_accT) atomicAdd(&sh[SH_T], s_accT);
+    if (s_accU) atomicAdd(&sh[SH_U], s_accU);
   }
   DM_PH_FLUSH(dm_phase_acc_integrate);
 }
@@ -797,7 +835,8 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   // heavy chunks and medium tiles first (the long items), then the light
   // tiles; k_heavy_apply then applies the heavy tiles' merged slabs
   dm_timer_begin(g, "tile_accum", &t);
-  hipLaunchKernelGGL(k_tile_accum, dim3(grid_for(g->hitem_cap + g->act_cap, 1, 2048)), dim3(kQuarter), 0,
+  hipLaunchKernelGGL(k_tile_accum, dim3(grid_for(g->hitem_cap + g->act_cap, 1, 16384)),
+                     dim3(kQuarter), 0,
                      g->stream, ge, make_apply(g), g->hitems, (int)CNT_ITEMS, g->litems, (int)CNT_LITEMS,
                      g->pieces, g->tile_count, g->tile_free, g->slabs, g->L, g->state, g->cnt, g->ish, vec_ok);
   dm_timer_end(g, &t);

@@ -83,6 +83,7 @@ struct KernelTimer {
 struct dm_grid {
   dm_params p;
   int device = 0;
+  int n_cu = 256;  // compute units of the device: sizes the resident (one-pass) grids
   hipStream_t stream = nullptr;
   bool own_stream = false;
   int64_t W = 0, H = 0, R = 0, row0 = 0;
