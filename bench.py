@@ -5,7 +5,12 @@ Workload (per GPU): BASELINE config C3 — a 16384 x 16384 grid at 5 cm,
 64 robots random-walking in a seeded synthetic world, 64-scan x 4096-beam
 LD06-format batches.  One step = integrate one 64-scan batch (inputs already
 resident in HBM, dm_integrate_device) + full frontier extraction
-(mask + CCL + clusters, clusters copied to the host, dm_frontiers).
+(mask + CCL + clusters, clusters copied to the host).  Steps are pipelined
+by default: step k's frontier pass (dm_frontiers_begin) is collected
+(dm_frontiers_end) after step k+1's integrate call was enqueued, and with
+dm_set_overlap step k+1's ray front-end (beam prep, tile planning, piece
+scatter) runs beside it; the map update of step k+1 still waits for step k's
+frontier pass.  --no-overlap runs the steps back to back.
 
 N GPUs (weak scaling): rank r owns a 16384-row band of a 16384 x 16384*N map
 with its own 64 robots anywhere in the band (plus the neighbours' scans that
@@ -45,6 +50,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="budget for the CPU-oracle baseline sample (0 disables)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="run the steps back to back without overlapping step k+1's integrate "
+                         "front-end with step k's frontier pass")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1")
     ap.add_argument("--device-override", type=int, default=None,
                     help="put every rank on this GPU (rehearsal with --backend gloo)")
@@ -142,8 +150,34 @@ def main():
         integrate(k)
         return mapper.frontiers()
 
-    for k in range(args.warmup):
-        step(k)
+    # Pipelined steps (default): step k's frontier pass is started right
+    # after its integrate call and collected after step k+1's integrate call
+    # was enqueued, so step k+1's ray front-end (beam prep, tile planning,
+    # piece scatter: poses/ranges only) runs beside step k's frontier pass
+    # (dm_set_overlap).  Every frontier pass still sees exactly the map after
+    # its own batch, every batch is fully integrated: the work per step is
+    # unchanged, only independent kernels overlap.
+    pipelined = not args.no_overlap
+
+    def run_steps(k0, n):
+        if n <= 0:
+            return None
+        if not pipelined:
+            fr = None
+            for k in range(n):
+                fr = step(k0 + k)
+            return fr
+        integrate(k0)
+        mapper.frontiers_begin()
+        for k in range(1, n):
+            integrate(k0 + k)
+            mapper.frontiers_end()
+            mapper.frontiers_begin()
+        return mapper.frontiers_end()
+
+    if pipelined:
+        mapper.set_overlap(True)
+    run_steps(0, args.warmup)
 
     def barrier():
         if world_size > 1:
@@ -152,10 +186,8 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    n_clusters = 0
-    for k in range(args.steps):
-        fr = step(args.warmup + k)
-        n_clusters = len(fr)
+    fr = run_steps(args.warmup, args.steps)
+    band.synchronize()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -265,6 +297,8 @@ def main():
             "exchange": ("device: RCCL all-gather of halo rows + export records, dm_merge_bands"
                          if world_size > 1 else None),
             "exchange_fallbacks": getattr(mapper, "fallbacks", 0),
+            "pipelined": ("step k+1's integrate front-end overlaps step k's frontier pass "
+                          "(dm_set_overlap + dm_frontiers_begin/_end)") if pipelined else None,
             "cpu_baseline": cpu,
             "gen_seconds": t_gen,
         }

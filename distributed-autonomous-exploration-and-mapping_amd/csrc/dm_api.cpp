@@ -137,6 +137,7 @@ int ensure_trig(dm_grid* g, int32_t N, float amin, float inc) {
   if (N == g->trig_n && amin == g->trig_amin && inc == g->trig_inc) return DM_OK;
   // the table may still be read by an in-flight call
   DM_HIP(hipStreamSynchronize(g->stream));
+  if (g->fe_stream) DM_HIP(hipStreamSynchronize(g->fe_stream));
   std::vector<double> t(2 * (size_t)std::max(N, 1));
   for (int32_t i = 0; i < N; ++i) {
     const double phi = (double)amin + (double)i * (double)inc;
@@ -263,11 +264,11 @@ int finish_counts(dm_grid* g, uint64_t* U, uint64_t* T) {
                         hipMemcpyDeviceToHost, g->stream));
   DM_HIP(dm_copy_shards(g));
   DM_HIP(hipStreamSynchronize(g->stream));
-  if (g->h_cnt[CNT_OVERFLOW] & 11ull) {
+  if (g->h_cnt[CNT_IOVERFLOW]) {
     // cannot happen with the bounds in grow_integrate; keep the map consistent anyway
     (void)hipMemset(g->tile_count, 0, sizeof(int32_t) * (size_t)g->NT);
     return dm_set_error(DM_ERR_CAPACITY, "integrate workspace overflow (flags %llu)",
-                        (unsigned long long)g->h_cnt[CNT_OVERFLOW]);
+                        (unsigned long long)g->h_cnt[CNT_IOVERFLOW]);
   }
   if (U) *U = dm_shard_sum(g->h_sh, SH_U);
   if (T) *T = dm_shard_sum(g->h_sh, SH_T);
@@ -291,17 +292,18 @@ int dm_hip_check(hipError_t e, const char* what) {
                       hipGetErrorString(e), (int)e);
 }
 
-void dm_timer_begin(dm_grid* g, const char* name, KernelTimer* t) {
+void dm_timer_begin(dm_grid* g, const char* name, KernelTimer* t, hipStream_t s) {
   if (!g->profile) return;
   t->name = name;
+  t->stream = s ? s : g->stream;
   (void)hipEventCreate(&t->start);
   (void)hipEventCreate(&t->stop);
-  (void)hipEventRecord(t->start, g->stream);
+  (void)hipEventRecord(t->start, t->stream);
 }
 
 void dm_timer_end(dm_grid* g, KernelTimer* t) {
   if (!g->profile) return;
-  (void)hipEventRecord(t->stop, g->stream);
+  (void)hipEventRecord(t->stop, t->stream);
   g->pending.push_back(*t);
   if (g->pending.size() > 4096) {
     int32_t n = 0;
@@ -394,6 +396,12 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   e = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate"));
   g->own_stream = true;
+  e = hipStreamCreateWithFlags(&g->fe_stream, hipStreamNonBlocking);
+  if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(front-end)"));
+  for (hipEvent_t* ev : {&g->ev_fe, &g->ev_tiles, &g->ev_frontier}) {
+    e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
+  }
   if ((rc = dm_reset(g))) return fail(rc);
   *out = g;
   return DM_OK;
@@ -403,7 +411,11 @@ int dm_destroy(dm_grid* g) {
   if (!g) return DM_OK;
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
+  if (g->fe_stream) (void)hipStreamSynchronize(g->fe_stream);
   for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
+  for (hipEvent_t ev : {g->ev_fe, g->ev_tiles, g->ev_frontier})
+    if (ev) (void)hipEventDestroy(ev);
+  if (g->fe_stream) (void)hipStreamDestroy(g->fe_stream);
   dev_free(g->L); dev_free(g->state); dev_free(g->tile_count); dev_free(g->tile_cur);
   dev_free(g->tile_free); dev_free(g->cnt); dev_free(g->beams); dev_free(g->blk_hist); dev_free(g->blk_n); dev_free(g->pieces);
   dev_free(g->trig);
@@ -472,7 +484,8 @@ int dm_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N, const fl
     g->h_pose_cap = (int64_t)S * 4;
   }
   // the pinned pose staging buffer may still feed an in-flight copy
-  DM_HIP(hipStreamSynchronize(g->stream));
+  hipStream_t fs = g->overlap ? g->fe_stream : g->stream;
+  DM_HIP(hipStreamSynchronize(fs));
   for (int32_t s = 0; s < S; ++s) {
     const double x = poses[3 * s], y = poses[3 * s + 1], yaw = poses[3 * s + 2];
     g->h_pose4[4 * s + 0] = x;
@@ -480,16 +493,17 @@ int dm_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N, const fl
     g->h_pose4[4 * s + 2] = cos(yaw);  // C library, as the oracle
     g->h_pose4[4 * s + 3] = sin(yaw);
   }
+  if (g->overlap) DM_HIP(hipStreamWaitEvent(fs, g->ev_tiles, 0));  // pose4 / ranges of the last call read
   if (S > 0)
     DM_HIP(hipMemcpyAsync(g->pose4, g->h_pose4, sizeof(double) * 4 * (size_t)S,
-                          hipMemcpyHostToDevice, g->stream));
+                          hipMemcpyHostToDevice, fs));
   if (nb > 0)
-    DM_HIP(hipMemcpyAsync(g->ranges, ranges, sizeof(float) * (size_t)nb, hipMemcpyHostToDevice,
-                          g->stream));
+    DM_HIP(hipMemcpyAsync(g->ranges, ranges, sizeof(float) * (size_t)nb, hipMemcpyHostToDevice, fs));
   if ((rc = dm_launch_integrate(g, S, g->pose4, N, g->ranges, g->trig))) return rc;
   g->last_S = S;
   g->last_N = N;
   g->frontier_valid = false;
+  ++g->integrate_seq;
   return finish_counts(g, out_updates, out_touched);
 }
 
@@ -504,6 +518,7 @@ int dm_integrate_device(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   g->last_S = S;
   g->last_N = N;
   g->frontier_valid = false;
+  ++g->integrate_seq;
   return DM_OK;
 }
 
@@ -561,6 +576,7 @@ int dm_set_logodds(dm_grid* g, const float* in) {
   if ((rc = dm_launch_state_from_logodds(g))) return rc;
   DM_HIP(hipStreamSynchronize(g->stream));
   g->frontier_valid = false;
+  ++g->integrate_seq;
   return DM_OK;
 }
 
@@ -580,6 +596,7 @@ int dm_set_state(dm_grid* g, const int8_t* in) {
   (void)hipFree(d);
   if (e != hipSuccess) return dm_hip_check(e, "dm_set_state");
   g->frontier_valid = false;
+  ++g->integrate_seq;
   return rc;
 }
 
@@ -594,6 +611,8 @@ int dm_frontiers(dm_grid* g, uint8_t* mask, int64_t* labels, dm_cluster* out, in
     if ((rc = dev_alloc(&g->cell_slot, cells, "dense cell slots"))) return rc;
     if ((rc = dev_alloc(&g->labels, cells, "dense labels"))) return rc;
   }
+  if (g->fr_pending)  // an unfinished asynchronous pass shares the readback buffer
+    return dm_set_error(DM_ERR_INVALID_ARG, "a frontier / merge pass is in flight: end it first");
   int64_t n = 0, copied = 0;
   for (int attempt = 0; attempt < 8; ++attempt) {
     rc = dm_launch_frontiers(g, mask != nullptr, labels != nullptr, &n, &copied);
@@ -637,21 +656,35 @@ int dm_frontiers_export_device(dm_grid* g, void* d_export, int64_t rec_cap) {
   return DM_OK;
 }
 
-int dm_merge_bands(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap, int64_t min_size,
-                   dm_cluster* out, int64_t cap, int64_t* n_out) {
+int dm_merge_bands_begin(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap,
+                         int64_t min_size) {
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
+  if (g->fr_pending)
+    return dm_set_error(DM_ERR_INVALID_ARG, "a frontier / merge pass is in flight: end it first");
   if (!d_gathered || nranks < 1 || rec_cap < 1)
     return dm_set_error(DM_ERR_INVALID_ARG, "need d_gathered, nranks >= 1, rec_cap >= 1");
-  if (cap < 0 || (cap > 0 && !out)) return dm_set_error(DM_ERR_INVALID_ARG, "bad cluster buffer");
   const int64_t n = (int64_t)nranks * rec_cap;
   if (n >= (1ll << 31)) return dm_set_error(DM_ERR_SHAPE, "nranks * rec_cap must be < 2^31");
   if ((rc = grow_merge(g, n))) return rc;
   if ((rc = dm_launch_merge(g, d_gathered, nranks, rec_cap, min_size))) return rc;
+  DM_HIP(hipEventRecord(g->ev_frontier, g->stream));
+  g->fr_pending = 2;
+  g->fr_merge_n = n;
+  return DM_OK;
+}
+
+int dm_merge_bands_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (g->fr_pending != 2) return dm_set_error(DM_ERR_INVALID_ARG, "no dm_merge_bands_begin pass in flight");
+  if (cap < 0 || (cap > 0 && !out)) return dm_set_error(DM_ERR_INVALID_ARG, "bad cluster buffer");
+  DM_HIP(hipEventSynchronize(g->ev_frontier));
+  g->fr_pending = 0;
   // the merge's sort kernel wrote the merge counters and the first h_out_cap
   // records into the mapped host readback buffer: no copy command
+  const int64_t n = g->fr_merge_n;
   const int64_t hint = std::min<int64_t>(g->h_out_cap, n);
-  DM_HIP(hipStreamSynchronize(g->stream));
   memcpy(g->h_mcnt, dm_rb_header(g->h_out), sizeof(unsigned long long) * 4);
   if (g->h_mcnt[1]) {
     if (n_out) *n_out = (int64_t)g->h_mcnt[3];
@@ -661,12 +694,74 @@ int dm_merge_bands(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t r
                         (unsigned long long)g->h_mcnt[1], (unsigned long long)g->h_mcnt[3]);
   }
   const int64_t K = (int64_t)g->h_mcnt[0];
-  const int64_t nw = std::min<int64_t>(K, cap);
-  if ((rc = copy_clusters(g, g->h_mcnt[2] != 0, K, nw, hint, g->m_out, g->m_clu, out))) return rc;
-  if (K + K / 4 + 64 > g->h_out_cap && (rc = grow_host_out(g, K + K / 4 + 64))) return rc;
   if (n_out) *n_out = K;
-  if (K > cap) return dm_set_error(DM_ERR_CAPACITY, "%lld clusters, capacity %lld", (long long)K,
-                                   (long long)cap);
+  if (K > cap) {  // the result stays pending: call again with cap >= K
+    g->fr_pending = 2;
+    return dm_set_error(DM_ERR_CAPACITY, "%lld clusters, capacity %lld", (long long)K, (long long)cap);
+  }
+  if ((rc = copy_clusters(g, g->h_mcnt[2] != 0, K, K, hint, g->m_out, g->m_clu, out))) return rc;
+  if (K + K / 4 + 64 > g->h_out_cap && (rc = grow_host_out(g, K + K / 4 + 64))) return rc;
+  return DM_OK;
+}
+
+int dm_merge_bands(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap, int64_t min_size,
+                   dm_cluster* out, int64_t cap, int64_t* n_out) {
+  if (cap < 0 || (cap > 0 && !out)) return dm_set_error(DM_ERR_INVALID_ARG, "bad cluster buffer");
+  int rc = dm_merge_bands_begin(g, d_gathered, nranks, rec_cap, min_size);
+  if (rc) return rc;
+  rc = dm_merge_bands_end(g, out, cap, n_out);
+  g->fr_pending = 0;  // synchronous form: a capacity error ends the pass (rerun with more room)
+  return rc;
+}
+
+int dm_frontiers_begin(dm_grid* g) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (g->fr_pending)
+    return dm_set_error(DM_ERR_INVALID_ARG, "a frontier / merge pass is in flight: end it first");
+  if ((rc = dm_enqueue_frontiers(g, false, false))) return rc;
+  DM_HIP(hipEventRecord(g->ev_frontier, g->stream));
+  g->fr_pending = 1;
+  g->fr_seq = g->integrate_seq;
+  return DM_OK;
+}
+
+int dm_frontiers_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (g->fr_pending != 1) return dm_set_error(DM_ERR_INVALID_ARG, "no dm_frontiers_begin pass in flight");
+  if (cap < 0 || (cap > 0 && !out)) return dm_set_error(DM_ERR_INVALID_ARG, "bad cluster buffer");
+  DM_HIP(hipEventSynchronize(g->ev_frontier));
+  g->fr_pending = 0;
+  int64_t n = 0, copied = 0;
+  rc = dm_frontiers_readback(g, &n, &copied);
+  if (rc == DM_ERR_CAPACITY) {
+    if ((rc = grow_slots(g, n + n / 2 + 1024))) return rc;
+    if (n_out) *n_out = 0;
+    return dm_set_error(DM_ERR_INCOMPLETE, "frontier slot arrays overflowed (grown now): this pass "
+                                           "has no result, run dm_frontiers");
+  }
+  if (rc) return rc;
+  // the slot data (dm_get_edge_labels) describes the map only if no
+  // integrate call came in between
+  g->frontier_valid = g->fr_seq == g->integrate_seq;
+  if (n_out) *n_out = n;
+  if (n > cap) {  // the result stays pending: call again with cap >= n
+    g->fr_pending = 1;
+    return dm_set_error(DM_ERR_CAPACITY, "%lld clusters, capacity %lld", (long long)n, (long long)cap);
+  }
+  if ((rc = copy_clusters(g, g->h_cnt[CNT_SORTED] != 0, n, n, copied, g->out_clu, g->clusters, out)))
+    return rc;
+  if (n + n / 4 + 64 > g->h_out_cap && (rc = grow_host_out(g, n + n / 4 + 64))) return rc;
+  return DM_OK;
+}
+
+int dm_set_overlap(dm_grid* g, int32_t on) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  DM_HIP(hipStreamSynchronize(g->stream));
+  DM_HIP(hipStreamSynchronize(g->fe_stream));
+  g->overlap = on != 0;
   return DM_OK;
 }
 
@@ -679,6 +774,7 @@ int dm_set_halo(dm_grid* g, const int8_t* before, const int8_t* after) {
   g->has_halo[0] = before != nullptr;
   g->has_halo[1] = after != nullptr;
   g->frontier_valid = false;
+  ++g->integrate_seq;
   return DM_OK;
 }
 
@@ -691,6 +787,7 @@ int dm_set_halo_device(dm_grid* g, const int8_t* before, const int8_t* after) {
   g->has_halo[0] = before != nullptr;
   g->has_halo[1] = after != nullptr;
   g->frontier_valid = false;
+  ++g->integrate_seq;
   return DM_OK;
 }
 
@@ -828,6 +925,7 @@ int dm_load(dm_grid* g, const char* path) {
 int dm_set_stream(dm_grid* g, void* stream) {
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
+  DM_HIP(hipStreamSynchronize(g->fe_stream));
   DM_HIP(hipStreamSynchronize(g->stream));
   if (stream) {
     if (g->own_stream && g->stream) (void)hipStreamDestroy(g->stream);
@@ -843,6 +941,7 @@ int dm_set_stream(dm_grid* g, void* stream) {
 int dm_synchronize(dm_grid* g) {
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
+  DM_HIP(hipStreamSynchronize(g->fe_stream));
   DM_HIP(hipStreamSynchronize(g->stream));
   return DM_OK;
 }

@@ -791,22 +791,15 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   return DM_OK;
 }
 
-// Runs the frontier pipeline and copies the counters plus a speculative first
-// chunk of the sorted cluster records into g->h_out with ONE synchronisation.
-// Returns DM_ERR_CAPACITY (with *n_clusters = slots needed) when the slot
-// arrays overflowed; the caller grows them and reruns.
-int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters,
-                        int64_t* copied) {
-  int rc = dm_enqueue_frontiers(g, want_mask, want_labels);
-  if (rc) return rc;
-  // no copy command: k_rank_sort wrote the readback header (counters + the
-  // fullest slot shard) and the first h_out_cap sorted records straight into
-  // the mapped host buffer
-  const int64_t hint = std::min<int64_t>(g->h_out_cap, g->slot_cap);
-  DM_HIP(hipStreamSynchronize(g->stream));
+// After a frontier pass completed: the counters plus a speculative first
+// chunk of the sorted cluster records are in g->h_out (k_rank_sort wrote the
+// readback header and the first h_out_cap records straight into the mapped
+// host buffer: no copy command).  Returns DM_ERR_CAPACITY (with
+// *n_clusters = slots needed) when the slot arrays overflowed.
+int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied) {
   const unsigned long long* hdr = dm_rb_header(g->h_out);
   memcpy(g->h_cnt, hdr, sizeof(unsigned long long) * CNT_N);
-  *copied = hint;
+  *copied = std::min<int64_t>(g->h_out_cap, g->slot_cap);
   const unsigned long long most = hdr[CNT_N];
   if ((int64_t)most > g->slot_cap / kShards || (g->h_cnt[CNT_OVERFLOW] & 4ull)) {
     *n_clusters = (int64_t)most * kShards;  // slot capacity that fits the fullest shard
@@ -814,4 +807,13 @@ int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n
   }
   *n_clusters = (int64_t)g->h_cnt[CNT_CLUSTERS];
   return DM_OK;
+}
+
+// Runs the frontier pipeline with ONE synchronisation (dm_frontiers_readback).
+int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters,
+                        int64_t* copied) {
+  int rc = dm_enqueue_frontiers(g, want_mask, want_labels);
+  if (rc) return rc;
+  DM_HIP(hipStreamSynchronize(g->stream));
+  return dm_frontiers_readback(g, n_clusters, copied);
 }

@@ -111,7 +111,7 @@ __device__ inline void first_touch(const Geom& g, int32_t tile, int32_t old, int
   const int sh = blockIdx.x % kShards;
   const unsigned long long l = atomicAdd(&ish[sh * kShardWords + SH_ACT], 1ull);
   if (l < (unsigned long long)g.act_cap) act_raw[(int64_t)sh * g.act_cap + (int64_t)l] = tile;
-  else atomicOr(&cnt[CNT_OVERFLOW], 1ull);
+  else atomicOr(&cnt[CNT_IOVERFLOW], 1ull);
 }
 
 __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const double* __restrict__ pose4,
@@ -278,7 +278,7 @@ __device__ inline void put_piece(const Geom& g, PackedPiece* pieces, int64_t idx
     const int32_t ty0 = (tile / g.r.TX) * DM_TS;
     pieces[idx] = dm_pack_piece(dm_tile_piece(bm, k0, k1, g.r.row0, tx0, ty0, kLdsPitch));
   } else {
-    atomicOr(&cnt[CNT_OVERFLOW], 2ull);
+    atomicOr(&cnt[CNT_IOVERFLOW], 2ull);
   }
 }
 
@@ -710,7 +710,8 @@ __global__ __launch_bounds__(kQuarter) void k_heavy_apply(
 // Per-call reset of the device counters and integrate shards in one launch.
 __global__ __launch_bounds__(256) void k_integrate_reset(unsigned long long* cnt, unsigned long long* ish) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < CNT_N) cnt[i] = 0ull;
+  constexpr int nI = (int)(sizeof(kIntegrateCounters) / sizeof(kIntegrateCounters[0]));
+  if (i < nI) cnt[kIntegrateCounters[i]] = 0ull;
   if (i < kShards * kShardWords) ish[i] = 0ull;
 }
 
@@ -800,9 +801,24 @@ DM_PH_READER(integrate)
 int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                         const float* d_ranges, const double* d_trig) {
   const int64_t nb = (int64_t)S * N;
-  hipLaunchKernelGGL(k_integrate_reset, dim3(2), dim3(256), 0, g->stream, g->cnt, g->ish);
+  // front-end stream: with overlap, its own stream after the previous call's
+  // accumulation (ev_tiles: the tile workspace is free again), so it runs
+  // beside a frontier pass still in flight on g->stream
+  hipStream_t fs = g->stream;
+  if (g->overlap) {
+    fs = g->fe_stream;
+    DM_HIP(hipStreamWaitEvent(fs, g->ev_tiles, 0));
+  }
+  hipLaunchKernelGGL(k_integrate_reset, dim3(2), dim3(256), 0, fs, g->cnt, g->ish);
   DM_HIP(hipGetLastError());
-  if (nb == 0) return DM_OK;
+  if (nb == 0) {
+    if (g->overlap) {  // keep the stream order of the calls
+      DM_HIP(hipEventRecord(g->ev_fe, fs));
+      DM_HIP(hipStreamWaitEvent(g->stream, g->ev_fe, 0));
+      DM_HIP(hipEventRecord(g->ev_tiles, g->stream));
+    }
+    return DM_OK;
+  }
   RayArgs a;
   a.S = S;
   a.N = N;
@@ -815,22 +831,26 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   ge.nb = nb;
   const int nblk = (int)((nb + 255) / 256);
   KernelTimer t;
-  dm_timer_begin(g, "beam_prep", &t);
-  hipLaunchKernelGGL(k_beam_prep, dim3(nblk), dim3(256), 0, g->stream, a, ge, d_pose4, d_ranges,
+  dm_timer_begin(g, "beam_prep", &t, fs);
+  hipLaunchKernelGGL(k_beam_prep, dim3(nblk), dim3(256), 0, fs, a, ge, d_pose4, d_ranges,
                      d_trig, g->beams, g->tile_count, g->act_raw, g->ish, g->blk_hist, g->blk_n, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
-  dm_timer_begin(g, "plan", &t);
-  hipLaunchKernelGGL(k_plan, dim3(grid_for(g->act_cap, kPlanThreads, 256)), dim3(kPlanThreads), 0, g->stream,
+  dm_timer_begin(g, "plan", &t, fs);
+  hipLaunchKernelGGL(k_plan, dim3(grid_for(g->act_cap, kPlanThreads, 256)), dim3(kPlanThreads), 0, fs,
                      ge, g->act_raw, g->ish, g->tile_cur, g->tile_count, g->hitems, g->litems,
                      g->heavy_list, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
-  dm_timer_begin(g, "scatter", &t);
-  hipLaunchKernelGGL(k_scatter, dim3(nblk), dim3(256), 0, g->stream, a, ge, g->beams,
+  dm_timer_begin(g, "scatter", &t, fs);
+  hipLaunchKernelGGL(k_scatter, dim3(nblk), dim3(256), 0, fs, a, ge, g->beams,
                      g->tile_cur, g->blk_hist, g->blk_n, g->pieces, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
+  if (g->overlap) {
+    DM_HIP(hipEventRecord(g->ev_fe, fs));
+    DM_HIP(hipStreamWaitEvent(g->stream, g->ev_fe, 0));
+  }
   const int vec_ok = (g->W % 4 == 0) ? 1 : 0;
   // heavy chunks and medium tiles first (the long items), then the light
   // tiles; k_heavy_apply then applies the heavy tiles' merged slabs
@@ -847,6 +867,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                      g->cnt, g->ish);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
+  if (g->overlap) DM_HIP(hipEventRecord(g->ev_tiles, g->stream));
   return DM_OK;
 }
 

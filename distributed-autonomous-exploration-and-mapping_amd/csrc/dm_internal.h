@@ -40,8 +40,14 @@ enum {
   CNT_FL0 = 12,     // frontier tile-list length, even calls (zeroed by the odd calls)
   CNT_FL1 = 13,     // frontier tile-list length, odd calls (zeroed by the even calls)
   CNT_LITEMS = 14,  // light work items (= light tiles)
-  CNT_N = 15
+  CNT_IOVERFLOW = 15,  // integrate capacity overflow flags (1 first-touch list, 2 pieces)
+  CNT_N = 16
 };
+// Integrate counters, zeroed by each integrate call; the others belong to the
+// frontier pass, which may still be running when the next call's front-end
+// starts (dm_set_overlap), so the integrate reset never touches them.
+constexpr int kIntegrateCounters[] = {CNT_ACTIVE, CNT_U, CNT_T, CNT_SEGS, CNT_ITEMS,
+                                      CNT_HEAVY, CNT_TH, CNT_LITEMS, CNT_IOVERFLOW};
 
 // Sharded counters: same-address device atomics serialise at the memory side
 // (~12 ns each, MI355X_MICROARCH.md price list "fanin"), so per-workgroup
@@ -78,6 +84,7 @@ inline unsigned long long dm_shard_sum(const unsigned long long* sh, int field) 
 struct KernelTimer {
   std::string name;
   hipEvent_t start, stop;
+  hipStream_t stream = nullptr;
 };
 
 struct dm_grid {
@@ -86,6 +93,18 @@ struct dm_grid {
   int n_cu = 256;  // compute units of the device: sizes the resident (one-pass) grids
   hipStream_t stream = nullptr;
   bool own_stream = false;
+  // dm_set_overlap: the integrate front-end (reset, beam_prep, plan, scatter)
+  // runs on fe_stream and waits only for the previous call's accumulation
+  // (ev_tiles), so it overlaps a frontier pass still running on `stream`;
+  // the accumulation waits for it (ev_fe).  ev_frontier marks the end of an
+  // asynchronous frontier / band-merge pass (dm_frontiers_begin,
+  // dm_merge_bands_begin); fr_pending says which one is in flight.
+  bool overlap = false;
+  hipStream_t fe_stream = nullptr;
+  hipEvent_t ev_fe = nullptr, ev_tiles = nullptr, ev_frontier = nullptr;
+  int fr_pending = 0;  // 0 none, 1 band frontiers, 2 band merge
+  uint64_t integrate_seq = 0, fr_seq = 0;  // map changes so far / at the pending pass's start
+  int64_t fr_merge_n = 0;  // nranks * rec_cap of the pending merge
   int64_t W = 0, H = 0, R = 0, row0 = 0;
   int64_t TX = 0, TY = 0, NT = 0;
   int32_t nmax = 0;  // max ray length (cells) bound
@@ -173,6 +192,7 @@ int dm_launch_map_image(dm_grid* g, uint8_t* d_img);
 int dm_launch_set_state(dm_grid* g, const int8_t* d_state_in);
 int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels);
 int dm_launch_edge_labels(dm_grid* g);
+int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied);
 int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters,
                         int64_t* copied);
 int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const unsigned long long* d_count,
@@ -191,7 +211,7 @@ int dm_launch_ld06(dm_grid* g, int32_t S, const dm_ld06_point* d_pts, const int6
 // error plumbing (dm_api.cpp)
 int dm_set_error(int code, const char* fmt, ...);
 int dm_hip_check(hipError_t e, const char* what);
-void dm_timer_begin(dm_grid* g, const char* name, KernelTimer* t);
+void dm_timer_begin(dm_grid* g, const char* name, KernelTimer* t, hipStream_t s = nullptr);
 void dm_timer_end(dm_grid* g, KernelTimer* t);
 
 #define DM_HIP(call)                                         \

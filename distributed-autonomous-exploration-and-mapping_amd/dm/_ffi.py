@@ -154,6 +154,11 @@ SIGNATURES = {
     "dm_export_bytes": [_vp, _i64, ctypes.POINTER(_i64)],
     "dm_frontiers_export_device": [_vp, _vp, _i64],
     "dm_merge_bands": [_vp, _vp, _i32, _i64, _i64, _vp, _i64, ctypes.POINTER(_i64)],
+    "dm_merge_bands_begin": [_vp, _vp, _i32, _i64, _i64],
+    "dm_merge_bands_end": [_vp, _vp, _i64, ctypes.POINTER(_i64)],
+    "dm_frontiers_begin": [_vp],
+    "dm_frontiers_end": [_vp, _vp, _i64, ctypes.POINTER(_i64)],
+    "dm_set_overlap": [_vp, _i32],
 }
 # functions returning const char*
 STRING_FUNCS = ("dm_last_error", "dm_version")

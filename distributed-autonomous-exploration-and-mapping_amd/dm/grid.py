@@ -234,6 +234,35 @@ class OccupancyMapper:
             clusters = buf[: int(n.value)]
         return Frontiers(clusters=clusters, mask=mask, labels=labels)
 
+    def frontiers_begin(self):
+        """Enqueue a clusters-only frontier pass and return at once
+        (dm_frontiers_begin); collect it with frontiers_end()."""
+        with self._lock:
+            check(self._lib.dm_frontiers_begin(self._handle()))
+
+    def frontiers_end(self) -> Frontiers | None:
+        """Clusters of the pass started by frontiers_begin(), as frontiers()
+        would have returned them on the map at that time; None if the pass
+        overflowed the library's slot arrays (grown now: call frontiers())."""
+        n = ctypes.c_int64(0)
+        with self._lock:
+            while True:
+                buf = np.empty(self._cap, dtype=np.dtype(CLUSTER_DTYPE))
+                rc = self._lib.dm_frontiers_end(self._handle(), _vp(buf), buf.shape[0], ctypes.byref(n))
+                if rc == _ffi.DM_ERR_CAPACITY and n.value > buf.shape[0]:
+                    self._cap = int(n.value) * 2  # the pass stays pending: read it again
+                    continue
+                if rc == _ffi.DM_ERR_INCOMPLETE:
+                    return None
+                check(rc)
+                return Frontiers(clusters=buf[: int(n.value)])
+
+    def set_overlap(self, on: bool = True):
+        """dm_set_overlap: run the integrate front-end beside an in-flight
+        frontier pass (results unchanged)."""
+        with self._lock:
+            check(self._lib.dm_set_overlap(self._handle(), 1 if on else 0))
+
     # -- sharding support -------------------------------------------------
     def set_halo(self, before=None, after=None):
         b = None if before is None else np.ascontiguousarray(before, np.int8)
@@ -297,6 +326,30 @@ class OccupancyMapper:
                 if rc == _ffi.DM_ERR_CAPACITY and n.value > buf.shape[0]:
                     self._mbuf = np.empty(int(n.value) * 2, dtype=np.dtype(CLUSTER_DTYPE))
                     continue
+                check(rc)
+                return buf[: int(n.value)].copy(), None
+
+    def merge_bands_begin(self, d_gathered_ptr: int, nranks: int, rec_cap: int, min_size: int):
+        """Enqueue the device merge of gathered export records and return
+        (dm_merge_bands_begin); collect it with merge_bands_end()."""
+        with self._lock:
+            check(self._lib.dm_merge_bands_begin(self._handle(), ctypes.c_void_p(d_gathered_ptr), int(nranks),
+                                                 int(rec_cap), int(min_size)))
+
+    def merge_bands_end(self):
+        """merge_bands()'s result for the pass started by merge_bands_begin()."""
+        n = ctypes.c_int64(0)
+        with self._lock:
+            while True:
+                buf = self._mbuf if getattr(self, "_mbuf", None) is not None else \
+                    np.empty(1 << 14, dtype=np.dtype(CLUSTER_DTYPE))
+                rc = self._lib.dm_merge_bands_end(self._handle(), _vp(buf), buf.shape[0], ctypes.byref(n))
+                self._mbuf = buf
+                if rc == _ffi.DM_ERR_INCOMPLETE:
+                    return None, int(n.value)
+                if rc == _ffi.DM_ERR_CAPACITY and n.value > buf.shape[0]:
+                    self._mbuf = np.empty(int(n.value) * 2, dtype=np.dtype(CLUSTER_DTYPE))
+                    continue  # the pass stays pending: read it again
                 check(rc)
                 return buf[: int(n.value)].copy(), None
 

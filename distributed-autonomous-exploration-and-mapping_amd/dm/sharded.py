@@ -158,6 +158,7 @@ class ShardedMapper:
         self.W = int(params.width)
         self._device = None
         self._dev_path = False
+        self._pending = None  # frontiers_begin() pass in flight
         if world_size > 1:
             import torch.distributed as dist
 
@@ -240,7 +241,9 @@ class ShardedMapper:
             self._dist.all_gather_into_tensor(o, t.cpu(), group=self.group)
             out.copy_(o)
 
-    def _frontiers_device(self):
+    def _device_enqueue(self):
+        """Halo all-gather, band frontiers + export record, record all-gather
+        and the device merge, all enqueued on self.stream (no host wait)."""
         torch = self._torch
         W, P, r = self.W, self.world_size, self.rank
         with torch.cuda.stream(self.stream):
@@ -256,7 +259,10 @@ class ShardedMapper:
             gexp = self._buf("gexp", P * nb, torch.uint8)
             self.band.frontiers_export_device(exp.data_ptr(), self.rec_cap)
             self._gather_dev(exp, gexp)
-            clusters, max_k = self.band.merge_bands(gexp.data_ptr(), P, self.rec_cap, self.min_size)
+            self.band.merge_bands_begin(gexp.data_ptr(), P, self.rec_cap, self.min_size)
+
+    def _device_finish(self) -> Frontiers:
+        clusters, max_k = self.band.merge_bands_end()
         if clusters is not None:
             return Frontiers(clusters=clusters)
         # a band's record was incomplete; every rank merged the same gathered
@@ -266,12 +272,51 @@ class ShardedMapper:
             self.rec_cap *= 2
         return self._frontiers_host(False, False)
 
+    def _frontiers_device(self):
+        self._device_enqueue()
+        return self._device_finish()
+
     def frontiers(self, want_mask=False, want_labels=False) -> Frontiers:
+        if self._pending is not None:
+            raise RuntimeError("a frontiers_begin() pass is in flight: call frontiers_end() first")
         if self.world_size == 1:
             return self.band.frontiers(want_mask=want_mask, want_labels=want_labels)
         if self._dev_path and not (want_mask or want_labels):
             return self._frontiers_device()
         return self._frontiers_host(want_mask, want_labels)
+
+    # -- pipelined frontier passes -----------------------------------------
+    def set_overlap(self, on: bool = True):
+        """Let the next integrate calls' ray front-end run beside an in-flight
+        frontier pass (dm_set_overlap; results unchanged)."""
+        if hasattr(self.band, "set_overlap"):
+            self.band.set_overlap(on)
+
+    def frontiers_begin(self):
+        """Start a clusters-only frontier pass over the map as it is now and
+        return; frontiers_end() returns its clusters (the same as frontiers()
+        would have), and integrate calls may be made in between."""
+        if self._pending is not None:
+            raise RuntimeError("a frontiers_begin() pass is already in flight")
+        if self.world_size == 1 and hasattr(self.band, "frontiers_begin"):
+            self.band.frontiers_begin()
+            self._pending = ("band", None)
+        elif self.world_size > 1 and self._dev_path:
+            self._device_enqueue()
+            self._pending = ("merge", None)
+        else:  # host exchange (or a non-libdm band): computed now
+            self._pending = ("done", self.frontiers())
+
+    def frontiers_end(self) -> Frontiers:
+        kind, res = self._pending
+        self._pending = None
+        if kind == "band":
+            fr = self.band.frontiers_end()
+            # slot overflow (workspace grown): rerun on the map as it is now
+            return fr if fr is not None else self.band.frontiers()
+        if kind == "merge":
+            return self._device_finish()
+        return res
 
     def _frontiers_host(self, want_mask, want_labels) -> Frontiers:
         if self._dev_path:

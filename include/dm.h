@@ -154,6 +154,33 @@ int dm_set_state(dm_grid* g, const int8_t* in);
 int dm_frontiers(dm_grid* g, uint8_t* mask, int64_t* labels, dm_cluster* out,
                  int64_t cap, int64_t* n_out);
 
+/* Pipelined frontier passes.  dm_frontiers_begin enqueues a clusters-only
+ * frontier pass (the same pipeline as dm_frontiers with mask = labels = NULL)
+ * on the handle's stream and returns; dm_frontiers_end waits for THAT pass
+ * (an event, not the stream: integrate calls made in between keep running)
+ * and returns its clusters exactly as dm_frontiers would have on the map as
+ * it was at dm_frontiers_begin.  One pass may be in flight per handle; on
+ * DM_ERR_CAPACITY (*n_out = clusters) the pass stays pending, so call _end
+ * again with cap >= *n_out.  If
+ * the pass overflowed the slot arrays they are grown and DM_ERR_INCOMPLETE
+ * is returned with *n_out = 0: that pass has no result (run dm_frontiers).
+ * The reference (main.py:123-188) has no frontier step; this is the
+ * planner-facing form of SURVEY.md §8 a8-a10 used by a ROS node that keeps
+ * integrating scans while the last frontier request completes. */
+int dm_frontiers_begin(dm_grid* g);
+int dm_frontiers_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out);
+
+/* Overlap mode (default off).  When on, the integrate front-end of
+ * dm_integrate / dm_integrate_device (beam preparation, tile planning, piece
+ * scatter: everything that reads poses / ranges and not the map) runs on an
+ * internal stream that waits only for the previous integrate call's map
+ * update, so it overlaps a frontier pass still in flight on the handle's
+ * stream; the map update itself stays in the handle's stream order, after
+ * every earlier call.  Results are identical with overlap on or off.  With
+ * overlap on, the device inputs of dm_integrate_device must be complete when
+ * the call is made (e.g. produced by work the host already synchronised). */
+int dm_set_overlap(dm_grid* g, int32_t on);
+
 /* Sharding support (row bands).  Halo rows are the global
  * rows band_row0-1 (top, "above" = lower row index) and band_row0+band_rows
  * (bottom); NULL = no neighbour there.  Host and device variants. */
@@ -193,6 +220,14 @@ int dm_frontiers_export_device(dm_grid* g, void* d_export, int64_t rec_cap);
  * incomplete, DM_ERR_CAPACITY (*n_out = clusters) when cap is too small. */
 int dm_merge_bands(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap,
                    int64_t min_size, dm_cluster* out, int64_t cap, int64_t* n_out);
+/* dm_merge_bands split like dm_frontiers_begin / _end: _begin enqueues the
+ * merge and returns, _end waits for it (event) and returns its result with
+ * dm_merge_bands' error behaviour, except that on DM_ERR_CAPACITY the pass
+ * stays pending (call _end again with cap >= *n_out).  d_gathered must stay
+ * valid until _end. */
+int dm_merge_bands_begin(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap,
+                         int64_t min_size);
+int dm_merge_bands_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out);
 
 /* LD06 driver point (ldlidar::PointData fields the LaserScan conversion uses). */
 typedef struct dm_ld06_point {

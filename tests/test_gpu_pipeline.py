@@ -1,0 +1,149 @@
+"""GPU: pipelined frontier passes and the overlapped integrate front-end
+(dm_frontiers_begin / _end, dm_merge_bands_begin / _end, dm_set_overlap).
+
+Every pass collected with frontiers_end() must equal the CPU oracle's
+frontiers on the map as it was after that pass's own batch, although the next
+batch's integrate call (front-end on the overlap stream) was enqueued before
+the pass was collected; the final map must equal the oracle's bit for bit."""
+import numpy as np
+import pytest
+
+import cases
+import dm
+from test_gpu_parity import assert_map_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def _device_batches(batches):
+    import torch
+    from dm import synth
+
+    out = [(torch.from_numpy(synth.pose4(p)).cuda(), torch.from_numpy(np.ascontiguousarray(r)).cuda())
+           for p, r in batches]
+    torch.cuda.synchronize()  # overlap mode: device inputs complete at call time
+    return out
+
+
+def _oracle_steps(oracle_lib, p, batches, amin, inc):
+    om = oracle_lib.OracleMap(p)
+    clusters = []
+    for poses, ranges in batches:
+        om.integrate(poses, ranges, amin, inc)
+        clusters.append(om.frontiers(want_mask=False, want_labels=False)[2])
+    return om, clusters
+
+
+@pytest.mark.parametrize("W,H,S,N,nb,seed", [(2048, 2048, 8, 1024, 6, 41), (640, 480, 3, 720, 5, 42),
+                                             (1000, 700, 16, 2048, 4, 43)])
+def test_pipelined_steps_match_oracle(oracle_lib, W, H, S, N, nb, seed):
+    p, batches, amin, inc = cases.world_case(seed, W, H, 0.05, S, N, nb, region_frac=0.6)
+    om, expect = _oracle_steps(oracle_lib, p, batches, amin, inc)
+    dev = _device_batches(batches)
+    with dm.OccupancyMapper(p) as m:
+        m.set_overlap(True)
+        got = []
+        for k, (pose4, rng) in enumerate(dev):
+            m.integrate_device(pose4.data_ptr(), pose4.shape[0], rng.data_ptr(), N, amin, inc)
+            if k > 0:
+                got.append(m.frontiers_end())
+            m.frontiers_begin()
+        got.append(m.frontiers_end())
+        for k, fr in enumerate(got):
+            assert fr is not None
+            np.testing.assert_array_equal(fr.clusters, expect[k])
+        assert_map_equal(m, om)
+        m.set_overlap(False)
+        np.testing.assert_array_equal(m.frontiers().clusters, expect[-1])
+
+
+def test_overlap_host_integrate_and_sync_frontiers(oracle_lib):
+    """Overlap mode with the host-input entry point (uploads on the front-end
+    stream) and synchronous frontiers between calls."""
+    p, batches, amin, inc = cases.world_case(44, 900, 900, 0.05, 4, 900, 5, region_frac=0.7)
+    om, expect = _oracle_steps(oracle_lib, p, batches, amin, inc)
+    with dm.OccupancyMapper(p) as m:
+        m.set_overlap(True)
+        for k, (poses, ranges) in enumerate(batches):
+            m.integrate(poses, ranges, amin, inc)
+            np.testing.assert_array_equal(m.frontiers().clusters, expect[k])
+        assert_map_equal(m, om)
+
+
+def test_frontiers_end_protocol():
+    import ctypes
+
+    from dm import _ffi
+
+    p, batches, amin, inc = cases.world_case(45, 512, 512, 0.05, 4, 720, 2, region_frac=0.7)
+    with dm.OccupancyMapper(p) as m:
+        for poses, ranges in batches:
+            m.integrate(poses, ranges, amin, inc)
+        ref = m.frontiers().clusters
+        assert len(ref) > 2
+        lib, h = m._lib, m._handle()
+        n = ctypes.c_int64(-1)
+        # end without begin, begin twice, synchronous pass while one is pending
+        assert lib.dm_frontiers_end(h, None, 0, ctypes.byref(n)) == _ffi.DM_ERR_INVALID_ARG
+        assert lib.dm_frontiers_begin(h) == 0
+        assert lib.dm_frontiers_begin(h) == _ffi.DM_ERR_INVALID_ARG
+        with pytest.raises(dm.DmError):
+            m.frontiers()
+        # too small a buffer: DM_ERR_CAPACITY with the count, the pass stays pending
+        assert lib.dm_frontiers_end(h, None, 0, ctypes.byref(n)) == _ffi.DM_ERR_CAPACITY
+        assert n.value == len(ref)
+        buf = np.empty(len(ref), dtype=np.dtype(dm.CLUSTER_DTYPE))
+        assert lib.dm_frontiers_end(h, buf.ctypes.data_as(ctypes.c_void_p), len(ref), ctypes.byref(n)) == 0
+        np.testing.assert_array_equal(buf, ref)
+        # the pass is over now
+        assert lib.dm_frontiers_end(h, None, 0, ctypes.byref(n)) == _ffi.DM_ERR_INVALID_ARG
+        # the Python wrapper grows its buffer itself
+        m._cap = 1
+        m.frontiers_begin()
+        np.testing.assert_array_equal(m.frontiers_end().clusters, ref)
+
+
+def test_sharded_single_band_pipelined(oracle_lib):
+    from dm.sharded import ShardedMapper
+
+    p, batches, amin, inc = cases.world_case(46, 700, 600, 0.05, 4, 900, 4, region_frac=0.7)
+    om, expect = _oracle_steps(oracle_lib, p, batches, amin, inc)
+    sm = ShardedMapper(p)
+    try:
+        sm.set_overlap(True)
+        got = []
+        for k, (poses, ranges) in enumerate(batches):
+            sm.integrate(poses, ranges, amin, inc)
+            if k > 0:
+                got.append(sm.frontiers_end())
+            sm.frontiers_begin()
+        got.append(sm.frontiers_end())
+        for k, fr in enumerate(got):
+            np.testing.assert_array_equal(fr.clusters, expect[k])
+    finally:
+        sm.close()
+
+
+@pytest.mark.parametrize("P,W,H,seed", [(2, 300, 640, 3), (4, 1000, 1024, 7)])
+def test_merge_bands_begin_end_matches_sync(P, W, H, seed):
+    from test_gpu_merge import _bands, _export_all, _set_halos
+
+    p, batches, amin, inc = cases.world_case(seed, W, H, 0.05, 6, 900, 2, region_frac=0.8)
+    bands = _bands(p, P)
+    try:
+        for poses, ranges in batches:
+            for b in bands:
+                b.integrate(poses, ranges, amin, inc)
+        _set_halos(bands)
+        rec_cap = 4096
+        g, nb = _export_all(bands, rec_cap)
+        sync, k = bands[0].merge_bands(g.data_ptr(), P, rec_cap, 1)
+        assert k is None and len(sync) > 0
+        bands[1].merge_bands_begin(g.data_ptr(), P, rec_cap, 1)
+        bands[1]._mbuf = np.empty(1, dtype=np.dtype(dm.CLUSTER_DTYPE))  # forces the pending re-read
+        got, k = bands[1].merge_bands_end()
+        assert k is None
+        np.testing.assert_array_equal(got, sync)
+    finally:
+        for b in bands:
+            b.close()
