@@ -178,7 +178,7 @@ __device__ inline void tile_issue(const FGeom& g, const int8_t* __restrict__ sta
 //     first run, whose first cell is the component's min linear index);
 //  4. per-component sums from run lengths, one slot per component, border
 //     slot ids for k_frontier_merge.
-__global__ __launch_bounds__(kFT) void k_frontier_tile(
+__global__ __launch_bounds__(kFT, 5) void k_frontier_tile(
     FGeom g, const int8_t* __restrict__ state, const int8_t* __restrict__ halo,
     const int32_t* __restrict__ ftiles, const unsigned long long* __restrict__ list_n,
     int32_t* __restrict__ border,
@@ -197,25 +197,19 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
   __shared__ uint8_t r_s[kMaxRuns], r_e[kMaxRuns], r_y[kMaxRuns];
   __shared__ int16_t r_rid[kMaxRuns];
   __shared__ int16_t c_run[kMaxRoots];
-  __shared__ uint32_t ssz[kMaxRoots], ssx[kMaxRoots], ssy[kMaxRoots];
+  // per-component size << 18 | sum of x (size <= 4096 < 2^13, sum of x <=
+  // 4096 * 63 < 2^18: one 32-bit LDS add per run for both) and sum of y
+  __shared__ uint32_t szx[kMaxRoots], ssy[kMaxRoots];
   __shared__ int32_t nroots;
   __shared__ long long sbase;
   const int tid = threadIdx.x, lane = __lane_id();
   const int64_t nft = (int64_t)*list_n;
-  // software pipeline: the next tile's loads (and the one after's index) are
-  // issued before the current tile is labelled
   const int64_t G = gridDim.x;
-  int32_t tile_n = (int64_t)blockIdx.x < nft ? ftiles[blockIdx.x] : -1;
-  int32_t tile_nn = (int64_t)blockIdx.x + G < nft ? ftiles[blockIdx.x + G] : -1;
-  TileLoads ld_n;
-  if (tile_n >= 0) tile_issue(g, state, halo, tile_n, tid, ld_n);
   DM_PH_INIT();
-  for (int64_t jj = blockIdx.x; jj < nft; jj += G) {
-    const int32_t tile = tile_n;
-    const TileLoads cur = ld_n;
-    tile_n = tile_nn;
-    if (tile_n >= 0) tile_issue(g, state, halo, tile_n, tid, ld_n);
-    tile_nn = jj + 2 * G < nft ? ftiles[jj + 2 * G] : -1;
+  for (int64_t jj = blockIdx.x; jj < nft; jj += G) {  // one tile per workgroup at C3
+    const int32_t tile = ftiles[jj];
+    TileLoads cur;
+    tile_issue(g, state, halo, tile, tid, cur);
     const int64_t j = tile;  // border records are indexed by tile
     DM_PH_COUNT(dm_phase_acc_frontier, 16, 1);
     const int32_t tx0 = (tile % g.TX) * DM_TS;
@@ -324,7 +318,7 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
       }
     }
     if (tid == 0) nroots = 0;
-    for (int r = tid; r < kMaxRoots; r += kFT) { ssz[r] = 0; ssx[r] = 0; ssy[r] = 0; }
+    for (int r = tid; r < kMaxRoots; r += kFT) { szx[r] = 0; ssy[r] = 0; }
     __syncthreads();
     const int nruns = s_rbase[DM_TS];
     DM_PH(dm_phase_acc_frontier, 2);
@@ -349,20 +343,16 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
     }
     __syncthreads();
     DM_PH(dm_phase_acc_frontier, 3);
-    {  // roots first, writes after a barrier: a final root written early
-       // could be overwritten by another thread's path-halving store
-      int32_t root[kMaxRuns / kFT];
-#pragma unroll
-      for (int q = 0; q < kMaxRuns / kFT; ++q) {
-        const int r = tid + q * kFT;
-        root[q] = r < nruns ? lds_find(r_par, r) : 0;
+    // compress: every run points at its root.  The finds here only read
+    // (no halving), so the only stores are final roots: a find passing
+    // through a run already compressed just takes the shortcut.
+    for (int r = tid; r < nruns; r += kFT) {
+      int32_t x = r, p = r_par[r];
+      while (p != x) {
+        x = p;
+        p = ((volatile int32_t*)r_par)[x];
       }
-      __syncthreads();
-#pragma unroll
-      for (int q = 0; q < kMaxRuns / kFT; ++q) {
-        const int r = tid + q * kFT;
-        if (r < nruns) r_par[r] = root[q];
-      }
+      r_par[r] = x;
     }
     __syncthreads();
     DM_PH(dm_phase_acc_frontier, 4);
@@ -383,8 +373,7 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
     for (int r = tid; r < nruns; r += kFT) {
       const int c = r_rid[r_par[r]];
       const uint32_t s0 = r_s[r], e0 = r_e[r], len = e0 - s0 + 1;
-      atomicAdd(&ssz[c], len);
-      atomicAdd(&ssx[c], (s0 + e0) * len / 2);
+      atomicAdd(&szx[c], (len << 18) + (s0 + e0) * len / 2);
       atomicAdd(&ssy[c], (uint32_t)r_y[r] * len);
     }
     __syncthreads();
@@ -398,10 +387,11 @@ __global__ __launch_bounds__(kFT) void k_frontier_tile(
       const int r = c_run[c];
       const long long gy = (long long)g.row0 + ty0 + r_y[r];
       const long long gx = (long long)tx0 + r_s[r];
-      const long long sz = ssz[c];
+      const uint32_t zx = szx[c];
+      const long long sz = zx >> 18;
       slot_label[slot] = gy * g.W + gx;
       slot_parent[slot] = (int32_t)slot;
-      const long long sx = sz * tx0 + ssx[c];
+      const long long sx = sz * tx0 + (zx & 0x3FFFFu);
       const long long sy = sz * ((long long)g.row0 + ty0) + ssy[c];
       slot_own[3 * slot + 0] = sz; slot_own[3 * slot + 1] = sx; slot_own[3 * slot + 2] = sy;
       slot_acc[3 * slot + 0] = sz; slot_acc[3 * slot + 1] = sx; slot_acc[3 * slot + 2] = sy;
@@ -754,6 +744,7 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));
   KernelTimer t;
   const int nft_grid = grid_for(g->NT, 1, 2048);
+  // k_frontier_tile: one listed tile per workgroup (the dispatcher balances)
   const int ftile_grid = grid_for(g->NT, 1, 8192);
   dm_timer_begin(g, "frontier_tile", &t);
   hipLaunchKernelGGL(k_frontier_tile, dim3(ftile_grid), dim3(kFT), 0, g->stream, fg, g->state,

@@ -1,0 +1,62 @@
+"""Host-side timing of the pipelined bench loop (C3, one GPU): per step, the
+wall time spent in the integrate call, in frontiers_end (waiting for the
+previous pass + copying its clusters) and in frontiers_begin (enqueueing the
+pass).  Diagnostic only."""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "distributed-autonomous-exploration-and-mapping_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import dm  # noqa: E402
+from dm import synth  # noqa: E402
+
+
+def main():
+    G, res, S, N = 16384, 0.05, 64, 4096
+    half = G * res / 2
+    world = synth.make_world(0, -half, -half, half, half)
+    st = synth.ScanStream(world, S, N, 500, region=(-half + 1, -half + 1, half - 1, half - 1))
+    pool = [st.next_batch() for _ in range(4)]
+    dev = torch.device("cuda", 0)
+    dpool = [(torch.from_numpy(synth.pose4(p)).to(dev), torch.from_numpy(r).to(dev)) for p, r in pool]
+    torch.cuda.synchronize()
+    amin, inc = float(synth.LD06_ANGLE_MIN), float(synth.ld06_angle_increment(N))
+    m = dm.OccupancyMapper(dm.default_params(G, G, resolution=res))
+    m.set_overlap(True)
+
+    def integrate(k):
+        p4, r = dpool[k % len(dpool)]
+        m.integrate_device(p4.data_ptr(), S, r.data_ptr(), N, amin, inc)
+
+    for rep in range(2):
+        ti, te, tb = [], [], []
+        t0 = time.perf_counter()
+        integrate(0)
+        m.frontiers_begin()
+        steps = 30
+        for k in range(1, steps):
+            a = time.perf_counter()
+            integrate(k)
+            b = time.perf_counter()
+            m.frontiers_end()
+            c = time.perf_counter()
+            m.frontiers_begin()
+            d = time.perf_counter()
+            ti.append(b - a)
+            te.append(c - b)
+            tb.append(d - c)
+        m.frontiers_end()
+        el = time.perf_counter() - t0
+        f = lambda v: 1e6 * float(np.median(v))
+        print(f"rep {rep}: {1e6 * el / steps:.1f} us/step; integrate call {f(ti):.1f}, "
+              f"frontiers_end {f(te):.1f}, frontiers_begin {f(tb):.1f} us (medians)", flush=True)
+    m.close()
+
+
+if __name__ == "__main__":
+    main()
