@@ -398,10 +398,15 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   g->own_stream = true;
   e = hipStreamCreateWithFlags(&g->fe_stream, hipStreamNonBlocking);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(front-end)"));
-  for (hipEvent_t* ev : {&g->ev_fe, &g->ev_tiles, &g->ev_frontier}) {
-    e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+  // ev_fe / ev_tiles only order the two streams on the device: no system-
+  // scope fence (no host-visible cache writeback at every step).  The host
+  // waits on ev_frontier and then reads mapped host memory: default fences.
+  for (hipEvent_t* ev : {&g->ev_fe, &g->ev_tiles}) {
+    e = hipEventCreateWithFlags(ev, hipEventDisableTiming | hipEventDisableSystemFence);
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
   }
+  e = hipEventCreateWithFlags(&g->ev_frontier, hipEventDisableTiming);
+  if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
   if ((rc = dm_reset(g))) return fail(rc);
   *out = g;
   return DM_OK;
@@ -493,7 +498,10 @@ int dm_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N, const fl
     g->h_pose4[4 * s + 2] = cos(yaw);  // C library, as the oracle
     g->h_pose4[4 * s + 3] = sin(yaw);
   }
-  if (g->overlap) DM_HIP(hipStreamWaitEvent(fs, g->ev_tiles, 0));  // pose4 / ranges of the last call read
+  if (g->overlap) {  // pose4 / ranges of the last call read
+    DM_HIP(dm_mark_tiles(g));
+    DM_HIP(hipStreamWaitEvent(fs, g->ev_tiles, 0));
+  }
   if (S > 0)
     DM_HIP(hipMemcpyAsync(g->pose4, g->h_pose4, sizeof(double) * 4 * (size_t)S,
                           hipMemcpyHostToDevice, fs));
@@ -762,6 +770,7 @@ int dm_set_overlap(dm_grid* g, int32_t on) {
   DM_HIP(hipStreamSynchronize(g->stream));
   DM_HIP(hipStreamSynchronize(g->fe_stream));
   g->overlap = on != 0;
+  g->tiles_mark_pending = false;
   return DM_OK;
 }
 

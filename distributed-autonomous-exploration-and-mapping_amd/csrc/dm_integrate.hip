@@ -807,6 +807,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   hipStream_t fs = g->stream;
   if (g->overlap) {
     fs = g->fe_stream;
+    DM_HIP(dm_mark_tiles(g));
     DM_HIP(hipStreamWaitEvent(fs, g->ev_tiles, 0));
   }
   hipLaunchKernelGGL(k_integrate_reset, dim3(2), dim3(256), 0, fs, g->cnt, g->ish);
@@ -815,7 +816,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
     if (g->overlap) {  // keep the stream order of the calls
       DM_HIP(hipEventRecord(g->ev_fe, fs));
       DM_HIP(hipStreamWaitEvent(g->stream, g->ev_fe, 0));
-      DM_HIP(hipEventRecord(g->ev_tiles, g->stream));
+      g->tiles_mark_pending = true;
     }
     return DM_OK;
   }
@@ -867,7 +868,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                      g->cnt, g->ish);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
-  if (g->overlap) DM_HIP(hipEventRecord(g->ev_tiles, g->stream));
+  if (g->overlap) g->tiles_mark_pending = true;
   return DM_OK;
 }
 

@@ -102,6 +102,10 @@ struct dm_grid {
   bool overlap = false;
   hipStream_t fe_stream = nullptr;
   hipEvent_t ev_fe = nullptr, ev_tiles = nullptr, ev_frontier = nullptr;
+  // ev_tiles is recorded lazily: after the next frontier pass's first
+  // kernel (an event marker right behind the write-heavy map update costs
+  // the stream several microseconds), or at the next integrate call
+  bool tiles_mark_pending = false;
   int fr_pending = 0;  // 0 none, 1 band frontiers, 2 band merge
   uint64_t integrate_seq = 0, fr_seq = 0;  // map changes so far / at the pending pass's start
   int64_t fr_merge_n = 0;  // nranks * rec_cap of the pending merge
@@ -182,6 +186,14 @@ struct dm_grid {
   std::vector<KernelTimer> pending;
   std::vector<dm_kernel_stat> stats;
 };
+
+// Record ev_tiles (the tile workspace of the last integrate call is free
+// once the work enqueued so far on g->stream is done) if it is still owed.
+inline hipError_t dm_mark_tiles(dm_grid* g) {
+  if (!g->overlap || !g->tiles_mark_pending) return hipSuccess;
+  g->tiles_mark_pending = false;
+  return hipEventRecord(g->ev_tiles, g->stream);
+}
 
 // ---- launchers (dm_integrate.hip / dm_frontier.hip) -----------------------
 int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,

@@ -24,3 +24,24 @@ for k in range(first, min(first + 2, len(accum) - 1)):
     print(f"-- step from k_tile_accum #{k}")
     for s, e, name in rows[accum[k] - 6:accum[k + 1] + 1]:
         print(f"  {name:26s} {(s - t0) / 1e3:8.1f} {(e - t0) / 1e3:8.1f}  ({(e - s) / 1e3:5.1f})")
+
+# main-stream gaps per step (pipelined region): rank_sort end -> next
+# k_tile_accum start, heavy_apply end -> frontier_prep start, prep end -> tile start
+def gaps(a, b):
+    out = []
+    ends = [r for r in rows if r[2] == a]
+    starts = [r for r in rows if r[2] == b]
+    j = 0
+    for s, e, _ in ends:
+        while j < len(starts) and starts[j][0] < e:
+            j += 1
+        if j < len(starts):
+            out.append((starts[j][0] - e) / 1e3)
+    return out
+
+
+for a, b in (("k_rank_sort", "k_tile_accum"), ("k_heavy_apply", "k_frontier_prep"),
+             ("k_frontier_prep", "k_frontier_tile"), ("k_scatter", "k_tile_accum")):
+    g = gaps(a, b)[5:30]
+    if g:
+        print(f"gap {a} -> {b}: median {statistics.median(g):.1f} us, min {min(g):.1f}")
