@@ -161,11 +161,13 @@ int grow_slots(dm_grid* g, int64_t need) {
   if (!rc) rc = dev_alloc(&g->slot_own, 3 * cap, "slot sums");
   if (!rc) rc = dev_alloc(&g->slot_acc, 3 * cap, "slot totals");
   if (!rc) rc = dev_alloc(&g->clusters, 4 * cap, "clusters");
-  if (!rc) {
-    dm_cluster* base = g->out_clu ? g->out_clu - kRbRecords : nullptr;
+  for (int sl = 0; sl <= dm_grid::kRbSlots && !rc; ++sl) {  // one per readback slot
+    dm_cluster* base = g->rb[sl].out_clu ? g->rb[sl].out_clu - kRbRecords : nullptr;
     rc = dev_alloc(&base, cap + kRbRecords, "sorted clusters");
-    g->out_clu = base ? base + kRbRecords : nullptr;
+    g->rb[sl].out_clu = base ? base + kRbRecords : nullptr;
   }
+  ++g->rb_gen;
+  g->out_clu = g->rb[g->rb_head].out_clu;
   if (!rc) rc = dev_alloc(&g->slot_k, cap, "slot cluster index");
   if (!rc) rc = dev_alloc(&g->rank_of, cap, "cluster sorted position");
   if (rc) return rc;
@@ -173,13 +175,14 @@ int grow_slots(dm_grid* g, int64_t need) {
   return DM_OK;
 }
 
-int grow_host_out(dm_grid* g, int64_t need) {
-  if (need <= g->h_out_cap) return DM_OK;
-  int64_t cap = std::max<int64_t>(need, 2 * g->h_out_cap);
-  if (g->stream) DM_HIP(hipStreamSynchronize(g->stream));
-  if (g->h_out) (void)hipHostFree(g->h_out - kRbRecords);
-  g->h_out = nullptr;
-  g->h_out_cap = 0;
+// Grow readback slot `slot`'s mapped buffer (no pass of that slot in flight).
+int grow_host_out(dm_grid* g, int slot, int64_t need) {
+  dm_grid::RbSlot& r = g->rb[slot];
+  if (need <= r.h_out_cap) return DM_OK;
+  int64_t cap = std::max<int64_t>(need, 2 * r.h_out_cap);
+  if (r.h_out) (void)hipHostFree(r.h_out - kRbRecords);
+  r.h_out = nullptr;
+  r.h_out_cap = 0;
   // mapped + coherent: k_rank_sort writes the readback header and the first
   // records straight into it over PCIe (no D2H copy command per call)
   dm_cluster* base = nullptr;
@@ -191,9 +194,9 @@ int grow_host_out(dm_grid* g, int64_t need) {
     (void)hipHostFree(base);
     return dm_hip_check(e, "hipHostGetDevicePointer(cluster readback)");
   }
-  g->h_out = base + kRbRecords;
-  g->h_out_dev = dbase + kRbRecords;
-  g->h_out_cap = cap;
+  r.h_out = base + kRbRecords;
+  r.h_out_dev = dbase + kRbRecords;
+  r.h_out_cap = cap;
   return DM_OK;
 }
 
@@ -234,7 +237,9 @@ int grow_merge(dm_grid* g, int64_t n) {
   if (!rc) rc = dev_alloc(&g->m_label, n, "merge labels");
   if (!rc) rc = dev_alloc(&g->m_acc, 3 * n, "merge sums");
   if (!rc) rc = dev_alloc(&g->m_clu, 4 * n, "merged clusters");
-  if (!rc) rc = dev_alloc(&g->m_out, n, "merged clusters (sorted)");
+  for (int sl = 0; sl <= dm_grid::kRbSlots && !rc; ++sl)
+    rc = dev_alloc(&g->rb[sl].m_out, n, "merged clusters (sorted)");
+  ++g->rb_gen;
   if (rc) { g->m_cap = 0; return rc; }
   g->m_cap = n;
   return DM_OK;
@@ -382,7 +387,9 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if ((rc = dev_alloc(&g->edge_label, 2 * g->W, "edge labels"))) return fail(rc);
   if ((rc = dev_alloc(&g->halo, 2 * g->W, "halo rows"))) return fail(rc);
   if ((rc = grow_slots(g, 1 << 16))) return fail(rc);
-  if ((rc = grow_host_out(g, 1 << 14))) return fail(rc);
+  for (int sl = 0; sl <= dm_grid::kRbSlots; ++sl)
+    if ((rc = grow_host_out(g, sl, 1 << 14))) return fail(rc);
+  dm_select_slot(g, 0);
   e = hipHostMalloc((void**)&g->h_cnt, sizeof(unsigned long long) * CNT_N, hipHostMallocDefault);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipHostMalloc(counters)"));
   e = hipHostMalloc((void**)&g->h_sh, sizeof(unsigned long long) * 2 * kShards * kShardWords,
@@ -400,13 +407,16 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(front-end)"));
   // ev_fe / ev_tiles only order the two streams on the device: no system-
   // scope fence (no host-visible cache writeback at every step).  The host
-  // waits on ev_frontier and then reads mapped host memory: default fences.
+  // waits on a readback slot's event and then reads mapped host memory:
+  // default fences.
   for (hipEvent_t* ev : {&g->ev_fe, &g->ev_tiles}) {
     e = hipEventCreateWithFlags(ev, hipEventDisableTiming | hipEventDisableSystemFence);
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
   }
-  e = hipEventCreateWithFlags(&g->ev_frontier, hipEventDisableTiming);
-  if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
+  for (auto& r : g->rb) {
+    e = hipEventCreateWithFlags(&r.ev, hipEventDisableTiming);
+    if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
+  }
   if ((rc = dm_reset(g))) return fail(rc);
   *out = g;
   return DM_OK;
@@ -418,8 +428,14 @@ int dm_destroy(dm_grid* g) {
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   if (g->fe_stream) (void)hipStreamSynchronize(g->fe_stream);
   for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
-  for (hipEvent_t ev : {g->ev_fe, g->ev_tiles, g->ev_frontier})
+  for (hipEvent_t ev : {g->ev_fe, g->ev_tiles})
     if (ev) (void)hipEventDestroy(ev);
+  for (auto& r : g->rb) {
+    if (r.ev) (void)hipEventDestroy(r.ev);
+    if (r.out_clu) (void)hipFree(r.out_clu - kRbRecords);
+    if (r.h_out) (void)hipHostFree(r.h_out - kRbRecords);
+    dev_free(r.m_out);
+  }
   if (g->fe_stream) (void)hipStreamDestroy(g->fe_stream);
   dev_free(g->L); dev_free(g->state); dev_free(g->tile_count); dev_free(g->tile_cur);
   dev_free(g->tile_free); dev_free(g->cnt); dev_free(g->beams); dev_free(g->blk_hist); dev_free(g->blk_n); dev_free(g->pieces);
@@ -429,14 +445,12 @@ int dm_destroy(dm_grid* g) {
   dev_free(g->border); dev_free(g->ftiles); dev_free(g->slot_label); dev_free(g->slot_parent); dev_free(g->slot_root);
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
   dev_free(g->edge_slot); dev_free(g->edge_label); dev_free(g->mask); dev_free(g->labels);
-  dev_free(g->halo); if (g->out_clu) (void)hipFree(g->out_clu - kRbRecords);
-  g->out_clu = nullptr; dev_free(g->ish); dev_free(g->act_raw);
+  dev_free(g->halo); dev_free(g->ish); dev_free(g->act_raw);
   dev_free(g->slot_k); dev_free(g->rank_of); dev_free(g->m_parent); dev_free(g->m_label);
-  dev_free(g->m_acc); dev_free(g->m_clu); dev_free(g->m_out); dev_free(g->m_cnt);
+  dev_free(g->m_acc); dev_free(g->m_clu); dev_free(g->m_cnt);
   if (g->h_mcnt) (void)hipHostFree(g->h_mcnt);
   if (g->h_cnt) (void)hipHostFree(g->h_cnt);
   if (g->h_sh) (void)hipHostFree(g->h_sh);
-  if (g->h_out) (void)hipHostFree(g->h_out - kRbRecords);
   if (g->h_pose4) (void)hipHostFree(g->h_pose4);
   if (g->stream && g->own_stream) (void)hipStreamDestroy(g->stream);
   delete g;
@@ -619,8 +633,10 @@ int dm_frontiers(dm_grid* g, uint8_t* mask, int64_t* labels, dm_cluster* out, in
     if ((rc = dev_alloc(&g->cell_slot, cells, "dense cell slots"))) return rc;
     if ((rc = dev_alloc(&g->labels, cells, "dense labels"))) return rc;
   }
-  if (g->fr_pending)  // an unfinished asynchronous pass shares the readback buffer
-    return dm_set_error(DM_ERR_INVALID_ARG, "a frontier / merge pass is in flight: end it first");
+  // its own readback slot: asynchronous passes may be in flight (this pass
+  // runs after them in stream order and sees the map as it is now)
+  const int slot = dm_grid::kRbSync;
+  dm_select_slot(g, slot);
   int64_t n = 0, copied = 0;
   for (int attempt = 0; attempt < 8; ++attempt) {
     rc = dm_launch_frontiers(g, mask != nullptr, labels != nullptr, &n, &copied);
@@ -633,7 +649,7 @@ int dm_frontiers(dm_grid* g, uint8_t* mask, int64_t* labels, dm_cluster* out, in
   const int64_t nw = std::min<int64_t>(n, cap);
   if ((rc = copy_clusters(g, g->h_cnt[CNT_SORTED] != 0, n, nw, copied, g->out_clu, g->clusters, out)))
     return rc;
-  if (n + n / 4 + 64 > g->h_out_cap && (rc = grow_host_out(g, n + n / 4 + 64))) return rc;
+  if ((rc = grow_host_out(g, slot, n + n / 4 + 64))) return rc;
   if (mask) DM_HIP(hipMemcpy(mask, g->mask, (size_t)cells, hipMemcpyDeviceToHost));
   if (labels) DM_HIP(hipMemcpy(labels, g->labels, sizeof(int64_t) * (size_t)cells, hipMemcpyDeviceToHost));
   if (n_out) *n_out = n;
@@ -658,40 +674,47 @@ int dm_frontiers_export_device(dm_grid* g, void* d_export, int64_t rec_cap) {
     return dm_set_error(DM_ERR_INVALID_ARG,
                         "export needs a band handle with min_frontier_size <= 1 (the size filter "
                         "applies to merged clusters)");
+  if (g->rb_count == dm_grid::kRbSlots)
+    return dm_set_error(DM_ERR_INVALID_ARG, "%d passes in flight: end one first", dm_grid::kRbSlots);
+  dm_select_slot(g, (g->rb_head + g->rb_count) % dm_grid::kRbSlots);
   if ((rc = dm_enqueue_frontiers(g, false, false))) return rc;
   if ((rc = dm_launch_export(g, d_export, rec_cap))) return rc;
   g->frontier_valid = true;
   return DM_OK;
 }
 
-int dm_merge_bands_begin(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap,
-                         int64_t min_size) {
-  int rc = check_grid(g);
-  if (rc || (rc = use_device(g))) return rc;
-  if (g->fr_pending)
-    return dm_set_error(DM_ERR_INVALID_ARG, "a frontier / merge pass is in flight: end it first");
-  if (!d_gathered || nranks < 1 || rec_cap < 1)
-    return dm_set_error(DM_ERR_INVALID_ARG, "need d_gathered, nranks >= 1, rec_cap >= 1");
-  const int64_t n = (int64_t)nranks * rec_cap;
-  if (n >= (1ll << 31)) return dm_set_error(DM_ERR_SHAPE, "nranks * rec_cap must be < 2^31");
-  if ((rc = grow_merge(g, n))) return rc;
-  if ((rc = dm_launch_merge(g, d_gathered, nranks, rec_cap, min_size))) return rc;
-  DM_HIP(hipEventRecord(g->ev_frontier, g->stream));
-  g->fr_pending = 2;
-  g->fr_merge_n = n;
+namespace {
+
+// Claim the next readback slot for an asynchronous pass (selected as the
+// current slot), or fail if every slot holds a pass not collected yet.
+int claim_slot(dm_grid* g, int* slot) {
+  if (g->rb_count == dm_grid::kRbSlots)
+    return dm_set_error(DM_ERR_INVALID_ARG, "%d passes in flight: end the oldest first", dm_grid::kRbSlots);
+  *slot = (g->rb_head + g->rb_count) % dm_grid::kRbSlots;
+  dm_select_slot(g, *slot);
   return DM_OK;
 }
 
-int dm_merge_bands_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out) {
-  int rc = check_grid(g);
-  if (rc || (rc = use_device(g))) return rc;
-  if (g->fr_pending != 2) return dm_set_error(DM_ERR_INVALID_ARG, "no dm_merge_bands_begin pass in flight");
-  if (cap < 0 || (cap > 0 && !out)) return dm_set_error(DM_ERR_INVALID_ARG, "bad cluster buffer");
-  DM_HIP(hipEventSynchronize(g->ev_frontier));
-  g->fr_pending = 0;
+// The oldest pending pass, if it is of `kind`: wait for it, select its slot.
+int wait_oldest(dm_grid* g, int kind, const char* what) {
+  if (!g->rb_count || g->rb[g->rb_head].kind != kind)
+    return dm_set_error(DM_ERR_INVALID_ARG, "the oldest pass in flight is not a %s pass", what);
+  DM_HIP(hipEventSynchronize(g->rb[g->rb_head].ev));
+  dm_select_slot(g, g->rb_head);
+  return DM_OK;
+}
+
+void retire_oldest(dm_grid* g) {
+  g->rb[g->rb_head].kind = 0;
+  g->rb_head = (g->rb_head + 1) % dm_grid::kRbSlots;
+  --g->rb_count;
+}
+
+// A completed merge in readback slot `slot` (selected): header -> result.
+int merge_readback(dm_grid* g, int slot, int64_t n, dm_cluster* out, int64_t cap, int64_t* n_out) {
+  dm_select_slot(g, slot);
   // the merge's sort kernel wrote the merge counters and the first h_out_cap
-  // records into the mapped host readback buffer: no copy command
-  const int64_t n = g->fr_merge_n;
+  // records into the slot's mapped readback buffer: no copy command
   const int64_t hint = std::min<int64_t>(g->h_out_cap, n);
   memcpy(g->h_mcnt, dm_rb_header(g->h_out), sizeof(unsigned long long) * 4);
   if (g->h_mcnt[1]) {
@@ -703,65 +726,121 @@ int dm_merge_bands_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out)
   }
   const int64_t K = (int64_t)g->h_mcnt[0];
   if (n_out) *n_out = K;
-  if (K > cap) {  // the result stays pending: call again with cap >= K
-    g->fr_pending = 2;
+  if (K > cap)
     return dm_set_error(DM_ERR_CAPACITY, "%lld clusters, capacity %lld", (long long)K, (long long)cap);
-  }
-  if ((rc = copy_clusters(g, g->h_mcnt[2] != 0, K, K, hint, g->m_out, g->m_clu, out))) return rc;
-  if (K + K / 4 + 64 > g->h_out_cap && (rc = grow_host_out(g, K + K / 4 + 64))) return rc;
+  if (K > hint && slot != dm_grid::kRbSync &&
+      (g->rb[slot].gen != g->rb_gen || (!g->h_mcnt[2] && g->rb[slot].pass != g->m_pass)))
+    return dm_set_error(DM_ERR_INCOMPLETE, "merge result lost to a workspace reallocation or a later "
+                                           "unsorted merge: rerun");
+  int rc = copy_clusters(g, g->h_mcnt[2] != 0, K, K, hint, g->m_out, g->m_clu, out);
+  if (rc) return rc;
+  return grow_host_out(g, slot, K + K / 4 + 64);
+}
+
+}  // namespace
+
+int dm_merge_bands_begin(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap,
+                         int64_t min_size) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (!d_gathered || nranks < 1 || rec_cap < 1)
+    return dm_set_error(DM_ERR_INVALID_ARG, "need d_gathered, nranks >= 1, rec_cap >= 1");
+  const int64_t n = (int64_t)nranks * rec_cap;
+  if (n >= (1ll << 31)) return dm_set_error(DM_ERR_SHAPE, "nranks * rec_cap must be < 2^31");
+  int slot = 0;
+  if ((rc = grow_merge(g, n)) || (rc = claim_slot(g, &slot))) return rc;
+  if ((rc = dm_launch_merge(g, d_gathered, nranks, rec_cap, min_size))) return rc;
+  dm_grid::RbSlot& r = g->rb[slot];
+  DM_HIP(hipEventRecord(r.ev, g->stream));
+  r.kind = 2;
+  r.merge_n = n;
+  r.gen = g->rb_gen;
+  r.pass = g->m_pass;
+  ++g->rb_count;
   return DM_OK;
+}
+
+int dm_merge_bands_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (cap < 0 || (cap > 0 && !out)) return dm_set_error(DM_ERR_INVALID_ARG, "bad cluster buffer");
+  if ((rc = wait_oldest(g, 2, "dm_merge_bands_begin"))) return rc;
+  const int slot = g->rb_head;
+  rc = merge_readback(g, slot, g->rb[slot].merge_n, out, cap, n_out);
+  if (rc != DM_ERR_CAPACITY) retire_oldest(g);  // on a capacity error the result stays pending
+  return rc;
 }
 
 int dm_merge_bands(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap, int64_t min_size,
                    dm_cluster* out, int64_t cap, int64_t* n_out) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (!d_gathered || nranks < 1 || rec_cap < 1)
+    return dm_set_error(DM_ERR_INVALID_ARG, "need d_gathered, nranks >= 1, rec_cap >= 1");
   if (cap < 0 || (cap > 0 && !out)) return dm_set_error(DM_ERR_INVALID_ARG, "bad cluster buffer");
-  int rc = dm_merge_bands_begin(g, d_gathered, nranks, rec_cap, min_size);
-  if (rc) return rc;
-  rc = dm_merge_bands_end(g, out, cap, n_out);
-  g->fr_pending = 0;  // synchronous form: a capacity error ends the pass (rerun with more room)
-  return rc;
+  const int64_t n = (int64_t)nranks * rec_cap;
+  if (n >= (1ll << 31)) return dm_set_error(DM_ERR_SHAPE, "nranks * rec_cap must be < 2^31");
+  if ((rc = grow_merge(g, n))) return rc;
+  dm_select_slot(g, dm_grid::kRbSync);  // its own slot: asynchronous passes may be in flight
+  if ((rc = dm_launch_merge(g, d_gathered, nranks, rec_cap, min_size))) return rc;
+  DM_HIP(hipStreamSynchronize(g->stream));
+  return merge_readback(g, dm_grid::kRbSync, n, out, cap, n_out);
 }
 
 int dm_frontiers_begin(dm_grid* g) {
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
-  if (g->fr_pending)
-    return dm_set_error(DM_ERR_INVALID_ARG, "a frontier / merge pass is in flight: end it first");
+  int slot = 0;
+  if ((rc = claim_slot(g, &slot))) return rc;
   if ((rc = dm_enqueue_frontiers(g, false, false))) return rc;
-  DM_HIP(hipEventRecord(g->ev_frontier, g->stream));
-  g->fr_pending = 1;
-  g->fr_seq = g->integrate_seq;
+  dm_grid::RbSlot& r = g->rb[slot];
+  DM_HIP(hipEventRecord(r.ev, g->stream));
+  r.kind = 1;
+  r.seq = g->integrate_seq;
+  r.gen = g->rb_gen;
+  r.pass = g->fr_pass;
+  ++g->rb_count;
   return DM_OK;
 }
 
 int dm_frontiers_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out) {
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
-  if (g->fr_pending != 1) return dm_set_error(DM_ERR_INVALID_ARG, "no dm_frontiers_begin pass in flight");
   if (cap < 0 || (cap > 0 && !out)) return dm_set_error(DM_ERR_INVALID_ARG, "bad cluster buffer");
-  DM_HIP(hipEventSynchronize(g->ev_frontier));
-  g->fr_pending = 0;
+  if ((rc = wait_oldest(g, 1, "dm_frontiers_begin"))) return rc;
+  const int slot = g->rb_head;
+  const dm_grid::RbSlot& r = g->rb[slot];
   int64_t n = 0, copied = 0;
   rc = dm_frontiers_readback(g, &n, &copied);
   if (rc == DM_ERR_CAPACITY) {
+    retire_oldest(g);
     if ((rc = grow_slots(g, n + n / 2 + 1024))) return rc;
     if (n_out) *n_out = 0;
     return dm_set_error(DM_ERR_INCOMPLETE, "frontier slot arrays overflowed (grown now): this pass "
                                            "has no result, run dm_frontiers");
   }
-  if (rc) return rc;
-  // the slot data (dm_get_edge_labels) describes the map only if no
-  // integrate call came in between
-  g->frontier_valid = g->fr_seq == g->integrate_seq;
-  if (n_out) *n_out = n;
-  if (n > cap) {  // the result stays pending: call again with cap >= n
-    g->fr_pending = 1;
-    return dm_set_error(DM_ERR_CAPACITY, "%lld clusters, capacity %lld", (long long)n, (long long)cap);
-  }
-  if ((rc = copy_clusters(g, g->h_cnt[CNT_SORTED] != 0, n, n, copied, g->out_clu, g->clusters, out)))
+  if (rc) {
+    retire_oldest(g);
     return rc;
-  if (n + n / 4 + 64 > g->h_out_cap && (rc = grow_host_out(g, n + n / 4 + 64))) return rc;
-  return DM_OK;
+  }
+  if (n_out) *n_out = n;
+  if (n > cap)  // the result stays pending: call again with cap >= n
+    return dm_set_error(DM_ERR_CAPACITY, "%lld clusters, capacity %lld", (long long)n, (long long)cap);
+  // the device records were reallocated meanwhile, or the result is unsorted
+  // (raw records, shared by every pass) and a later pass overwrote them
+  const bool sorted = g->h_cnt[CNT_SORTED] != 0;
+  if ((n > copied && r.gen != g->rb_gen) || (!sorted && r.pass != g->fr_pass)) {
+    retire_oldest(g);
+    return dm_set_error(DM_ERR_INCOMPLETE, "frontier result lost to a workspace reallocation or a "
+                                           "later pass: rerun");
+  }
+  // the slot data (dm_get_edge_labels) describes the map only if this was
+  // the last pass and no map change came in between
+  g->frontier_valid = g->rb_count == 1 && r.seq == g->integrate_seq;
+  rc = copy_clusters(g, sorted, n, n, copied, g->out_clu, g->clusters, out);
+  retire_oldest(g);
+  if (rc) return rc;
+  return grow_host_out(g, slot, n + n / 4 + 64);
 }
 
 int dm_set_overlap(dm_grid* g, int32_t on) {

@@ -733,6 +733,7 @@ int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const uns
 int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   const FGeom fg = make_fgeom(g, want_mask, want_labels);
   const int64_t cells = g->R * g->W;
+  ++g->fr_pass;
   g->fparity ^= 1;
   unsigned long long* list_n = g->cnt + (g->fparity ? CNT_FL1 : CNT_FL0);
   unsigned long long* other_n = g->cnt + (g->fparity ? CNT_FL0 : CNT_FL1);
@@ -740,6 +741,10 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
                      g->stream, g->NT, g->tile_free, g->ftiles, list_n, other_n, 2 * g->W, g->cnt, g->fsh,
                      g->edge_slot);
   DM_HIP(hipGetLastError());
+  // the last integrate call's tile workspace is free once the map update
+  // (ahead of the prep in stream order) is done: the next call's front-end
+  // may start now, beside the rest of this pass
+  DM_HIP(dm_mark_tiles(g));
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));
   KernelTimer t;

@@ -346,9 +346,16 @@ __device__ inline float apply_one(const ApplyArgs& p, float L, uint32_t h, uint3
   const float u = (float)m * p.l_free;
   L = L + t;
   L = L + u;
-  if (L < p.l_min) L = p.l_min;
-  if (L > p.l_max) L = p.l_max;
-  return L;
+  // clamp: if (L < l_min) L = l_min; if (L > l_max) L = l_max — one v_med3
+  // for finite L and l_min <= l_max (validate_params checks both)
+  return __builtin_amdgcn_fmed3f(L, p.l_min, p.l_max);
+}
+
+// Number of zero bytes of x (exact, no false positives).
+__device__ inline int32_t zero_bytes(uint32_t x) {
+  uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  t = ~(t | x | 0x7F7F7F7Fu);
+  return __popc(t);
 }
 
 // Cells of one tile owned by one thread: 4 consecutive cells (float4 / char4)
@@ -378,7 +385,12 @@ struct CellRows {
     }
   }
 
-  // counts(ly, h4, m4) supplies the counts of this thread's 4 cells of row ly
+  // counts(ly, h4, m4) supplies the counts of this thread's 4 cells of row ly.
+  // Adds the touched cells to *sh_T and the change in free cells to
+  // *sh_free; the updates U of the applied cells to *sh_U only if sh_U is
+  // given (a tile inside the map counts them in the walk instead: every cell
+  // step is one update; an edge tile's pieces also step over cells past the
+  // map's edge, which are not updates).
   template <class Counts>
   __device__ void apply(const Geom& g, const ApplyArgs& p, int32_t tx0, int32_t ty0, int ly0, int dly,
                         int cx, float* __restrict__ L, int8_t* __restrict__ state, Counts&& counts,
@@ -394,6 +406,10 @@ struct CellRows {
       counts(ly, h4, m4);
       if (((h4[0] | m4[0]) | (h4[1] | m4[1]) | (h4[2] | m4[2]) | (h4[3] | m4[3])) == 0u) continue;
       const int64_t base = (int64_t)y * g.r.W + tx0 + cx;
+      if (sh_U) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dU += tx0 + cx + e < g.r.W ? h4[e] + m4[e] : 0u;
+      }
       if (vec) {
         // branch-free per cell: untouched cells keep their values
         float lv[4] = {l[rr].x, l[rr].y, l[rr].z, l[rr].w};
@@ -401,21 +417,20 @@ struct CellRows {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const bool hit = (h4[e] | m4[e]) != 0u;
-          const int8_t old = sv[e];
           const float nl = apply_one(p, lv[e], h4[e], m4[e]);
           const int8_t ns = state_of(p, nl);
           lv[e] = hit ? nl : lv[e];
-          sv[e] = hit ? ns : old;
-          dU += h4[e] + m4[e];
+          sv[e] = hit ? ns : sv[e];
           dT += hit ? 1 : 0;
-          dFree += hit ? (int32_t)(ns == 0) - (int32_t)(old == 0) : 0;
         }
+        const char4 ns4 = make_char4(sv[0], sv[1], sv[2], sv[3]);
+        dFree += zero_bytes(*reinterpret_cast<const uint32_t*>(&ns4)) -
+                 zero_bytes(*reinterpret_cast<const uint32_t*>(&s[rr]));
         *reinterpret_cast<float4*>(L + base) = make_float4(lv[0], lv[1], lv[2], lv[3]);
-        *reinterpret_cast<char4*>(state + base) = make_char4(sv[0], sv[1], sv[2], sv[3]);
+        *reinterpret_cast<char4*>(state + base) = ns4;
       } else {
         for (int e = 0; e < 4; ++e) {
           if ((h4[e] | m4[e]) == 0u || tx0 + cx + e >= g.r.W) continue;
-          dU += h4[e] + m4[e];
           const int64_t i = base + e;
           const int8_t old = state[i];
           const float nl = apply_one(p, L[i], h4[e], m4[e]);
@@ -440,7 +455,7 @@ struct CellRows {
 // (every ray of a scan starts at the sensor's cell) then sit on different
 // cells at every step instead of piling a wave's atomics onto one LDS word.
 // The wave's trip count is its longest piece.
-__device__ inline void walk_piece(uint32_t* tl, const PackedPiece& mine, bool valid, int lane) {
+__device__ inline int32_t walk_piece(uint32_t* tl, const PackedPiece& mine, bool valid, int lane) {
   const TilePiece tp = dm_unpack_piece(mine.x, mine.y, mine.z, mine.w);
   const int32_t len = valid ? tp.len : 0;
   int32_t wl = len;
@@ -463,6 +478,29 @@ __device__ inline void walk_piece(uint32_t* tl, const PackedPiece& mine, bool va
     }
   }
   if (len > 0 && tp.addr_end >= 0) atomicAdd(&tl[tp.addr_end], 0xFFFFu);
+  return len;
+}
+
+// Light tiles: their pieces cross the tile from different directions and
+// rarely share cells, so each lane walks from its piece's first cell, with
+// no stagger and no wrap.  A lane whose piece has ended adds into its own
+// spare word past the tile (tl[kTileWords + lane], never read) instead of
+// masking the step: no exec-mask branch per step, no pile-up on one word.
+// Returns the piece's length (its cell updates).
+__device__ inline int32_t walk_piece_plain(uint32_t* tl, const PackedPiece& mine, bool valid, int lane) {
+  const TilePiece tp = dm_unpack_piece(mine.x, mine.y, mine.z, mine.w);
+  const int32_t len = valid ? tp.len : 0;
+  int32_t wl = len;
+  for (int o = 32; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o));
+  const int32_t spare = kTileWords + lane;
+  PieceCursor cur;
+  cur.init(tp);
+  for (int32_t st = 0; st < wl; ++st) {
+    atomicAdd(&tl[st < len ? cur.addr : spare], 1u);
+    cur.step(tp);
+  }
+  if (len > 0 && tp.addr_end >= 0) atomicAdd(&tl[tp.addr_end], 0xFFFFu);
+  return len;
 }
 
 __device__ inline PackedPiece no_piece() {
@@ -505,7 +543,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     int cnt_b, const PackedPiece* __restrict__ pieces, int32_t* tile_count, int32_t* tile_free,
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
     const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok) {
-  __shared__ uint32_t tl[kTileWords];
+  __shared__ uint32_t tl[kTileWords + 64];  // + one spare word per lane (walk_piece_plain)
   __shared__ int32_t s_T, s_free;
   __shared__ uint32_t s_U;
   const int tid = threadIdx.x, lane = lane_id();
@@ -573,10 +611,20 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
       // the walk
       tfree = tile_free[tile];
       cells.prefetch(g, tx0, ty0, tid >> 4, 16, cx, L, state, vec_ok);
-      walk_piece(tl, mine, tid < c, lane);
-      for (int32_t r0 = kChunk; r0 < c; r0 += kChunk) {
-        const PackedPiece more = r0 + tid < c ? pieces[c0 + r0 + tid] : no_piece();
-        walk_piece(tl, more, r0 + tid < c, lane);
+      int32_t u;  // this thread's cell updates (one per step)
+      if (c <= kChunk) {
+        u = walk_piece_plain(tl, mine, tid < c, lane);
+      } else {  // medium: near a sensor, the staggered walk
+        u = walk_piece(tl, mine, tid < c, lane);
+        for (int32_t r0 = kChunk; r0 < c; r0 += kChunk) {
+          const PackedPiece more = r0 + tid < c ? pieces[c0 + r0 + tid] : no_piece();
+          u += walk_piece(tl, more, r0 + tid < c, lane);
+        }
+      }
+      const bool inside = tx0 + DM_TS <= g.r.W && ty0 + DM_TS <= g.r.R;  // workgroup-uniform
+      if (inside) {
+        for (int o = 32; o > 0; o >>= 1) u += __shfl_xor(u, o);
+        if (lane == 0) atomicAdd(&s_U, (uint32_t)u);
       }
       __syncthreads();
       DM_PH(dm_phase_acc_integrate, 3);
@@ -590,7 +638,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
                       m4[e] = v & 0xFFFFu;
                     }
                   },
-                  &s_T, &s_free, &s_U);
+                  &s_T, &s_free, inside ? nullptr : &s_U);
       DM_PH(dm_phase_acc_integrate, 4);
     }
     __syncthreads();
@@ -780,8 +828,10 @@ ApplyArgs make_apply(const dm_grid* g) {
   ApplyArgs a;
   a.l_occ = g->p.l_occ;
   a.l_free = g->p.l_free;
-  a.l_min = g->p.l_min;
-  a.l_max = g->p.l_max;
+  // signed zeros normalised to +0: the SPEC's compare-based clamp gives the
+  // same result for a bound of -0 or +0 (L is never -0), v_med3 only for +0
+  a.l_min = g->p.l_min == 0.0f ? 0.0f : g->p.l_min;
+  a.l_max = g->p.l_max == 0.0f ? 0.0f : g->p.l_max;
   a.occ_t = g->p.occ_thresh;
   a.free_t = g->p.free_thresh;
   return a;

@@ -96,19 +96,43 @@ struct dm_grid {
   // dm_set_overlap: the integrate front-end (reset, beam_prep, plan, scatter)
   // runs on fe_stream and waits only for the previous call's accumulation
   // (ev_tiles), so it overlaps a frontier pass still running on `stream`;
-  // the accumulation waits for it (ev_fe).  ev_frontier marks the end of an
-  // asynchronous frontier / band-merge pass (dm_frontiers_begin,
-  // dm_merge_bands_begin); fr_pending says which one is in flight.
+  // the accumulation waits for it (ev_fe).
   bool overlap = false;
   hipStream_t fe_stream = nullptr;
-  hipEvent_t ev_fe = nullptr, ev_tiles = nullptr, ev_frontier = nullptr;
+  hipEvent_t ev_fe = nullptr, ev_tiles = nullptr;
   // ev_tiles is recorded lazily: after the next frontier pass's first
   // kernel (an event marker right behind the write-heavy map update costs
   // the stream several microseconds), or at the next integrate call
   bool tiles_mark_pending = false;
-  int fr_pending = 0;  // 0 none, 1 band frontiers, 2 band merge
-  uint64_t integrate_seq = 0, fr_seq = 0;  // map changes so far / at the pending pass's start
-  int64_t fr_merge_n = 0;  // nranks * rec_cap of the pending merge
+  uint64_t integrate_seq = 0;  // map changes so far
+  // Asynchronous passes (dm_frontiers_begin / dm_merge_bands_begin) use a
+  // ring of kRbSlots readback slots, so a pass can be started before the
+  // previous one was collected.  Each slot owns what its _end reads: the
+  // mapped readback buffer (header + first records), the device sorted
+  // records, the event marking the pass's end.  out_clu / h_out / h_out_dev /
+  // h_out_cap / m_out below point at the slot in use (dm_select_slot).
+  struct RbSlot {
+    dm_cluster* out_clu = nullptr;    // device sorted band records (after kRbRecords header records)
+    dm_cluster* h_out = nullptr;      // mapped host readback (after the header)
+    dm_cluster* h_out_dev = nullptr;  // its device address
+    int64_t h_out_cap = 0;
+    dm_cluster* m_out = nullptr;      // device sorted merged records
+    hipEvent_t ev = nullptr;
+    int kind = 0;                     // pending pass: 0 none, 1 band frontiers, 2 band merge
+    uint64_t seq = 0;                 // integrate_seq at the pass's start
+    uint64_t gen = 0;                 // rb_gen at the pass's start
+    uint64_t pass = 0;                // fr_pass / m_pass of the pass
+    int64_t merge_n = 0;              // nranks * rec_cap of a merge
+  };
+  static constexpr int kRbSlots = 2;   // ring slots of asynchronous passes
+  static constexpr int kRbSync = 2;    // the slot of synchronous calls (dm_frontiers, dm_merge_bands)
+  RbSlot rb[kRbSlots + 1];
+  int rb_head = 0, rb_count = 0;      // oldest pending slot, pending passes
+  uint64_t rb_gen = 0;                // bumped when device record buffers are reallocated
+  // frontier / merge passes enqueued so far: an unsorted result (more
+  // clusters than the sort kernel takes) lives in the shared raw arrays
+  // (clusters / m_clu), valid only while no later pass of its kind ran
+  uint64_t fr_pass = 0, m_pass = 0;
   int64_t W = 0, H = 0, R = 0, row0 = 0;
   int64_t TX = 0, TY = 0, NT = 0;
   int32_t nmax = 0;  // max ray length (cells) bound
@@ -186,6 +210,17 @@ struct dm_grid {
   std::vector<KernelTimer> pending;
   std::vector<dm_kernel_stat> stats;
 };
+
+// Point the current-slot views (out_clu, h_out, h_out_dev, h_out_cap, m_out)
+// at readback slot `slot`.
+inline void dm_select_slot(dm_grid* g, int slot) {
+  const dm_grid::RbSlot& r = g->rb[slot];
+  g->out_clu = r.out_clu;
+  g->h_out = r.h_out;
+  g->h_out_dev = r.h_out_dev;
+  g->h_out_cap = r.h_out_cap;
+  g->m_out = r.m_out;
+}
 
 // Record ev_tiles (the tile workspace of the last integrate call is free
 // once the work enqueued so far on g->stream is done) if it is still owed.

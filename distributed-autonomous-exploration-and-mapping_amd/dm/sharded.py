@@ -32,6 +32,8 @@ All messages are KB-MB: latency-bound on xGMI, no ring all-reduce needed.
 """
 from __future__ import annotations
 
+import collections
+
 import numpy as np
 
 from ._ffi import CLUSTER_DTYPE, DM_TILE, DmParams
@@ -158,7 +160,7 @@ class ShardedMapper:
         self.W = int(params.width)
         self._device = None
         self._dev_path = False
-        self._pending = None  # frontiers_begin() pass in flight
+        self._pending = collections.deque()  # frontiers_begin() passes in flight, oldest first
         if world_size > 1:
             import torch.distributed as dist
 
@@ -179,7 +181,7 @@ class ShardedMapper:
                 # around them: RCCL orders itself against it
                 self.stream = torch.cuda.Stream(device=self._tdev)
                 self.band.set_stream(self.stream.cuda_stream)
-                self.rec_cap = 4096
+                self.rec_cap = 16384  # records per band export (grown on an incomplete record)
                 self._bufs = {}
                 self.fallbacks = 0
 
@@ -259,10 +261,10 @@ class ShardedMapper:
             gexp = self._buf("gexp", P * nb, torch.uint8)
             self.band.frontiers_export_device(exp.data_ptr(), self.rec_cap)
             self._gather_dev(exp, gexp)
-            self.band.merge_bands_begin(gexp.data_ptr(), P, self.rec_cap, self.min_size)
+            return gexp
 
-    def _device_finish(self) -> Frontiers:
-        clusters, max_k = self.band.merge_bands_end()
+    def _device_finish(self, result) -> Frontiers:
+        clusters, max_k = result
         if clusters is not None:
             return Frontiers(clusters=clusters)
         # a band's record was incomplete; every rank merged the same gathered
@@ -273,12 +275,14 @@ class ShardedMapper:
         return self._frontiers_host(False, False)
 
     def _frontiers_device(self):
-        self._device_enqueue()
-        return self._device_finish()
+        gexp = self._device_enqueue()
+        with self._torch.cuda.stream(self.stream):
+            res = self.band.merge_bands(gexp.data_ptr(), self.world_size, self.rec_cap, self.min_size)
+        return self._device_finish(res)
 
     def frontiers(self, want_mask=False, want_labels=False) -> Frontiers:
-        if self._pending is not None:
-            raise RuntimeError("a frontiers_begin() pass is in flight: call frontiers_end() first")
+        """Frontiers of the map as it is now (synchronous; passes started with
+        frontiers_begin() may still be in flight)."""
         if self.world_size == 1:
             return self.band.frontiers(want_mask=want_mask, want_labels=want_labels)
         if self._dev_path and not (want_mask or want_labels):
@@ -295,27 +299,30 @@ class ShardedMapper:
     def frontiers_begin(self):
         """Start a clusters-only frontier pass over the map as it is now and
         return; frontiers_end() returns its clusters (the same as frontiers()
-        would have), and integrate calls may be made in between."""
-        if self._pending is not None:
-            raise RuntimeError("a frontiers_begin() pass is already in flight")
+        would have), and integrate calls may be made in between.  Up to two
+        passes may be in flight; frontiers_end() collects the oldest."""
+        if len(self._pending) == 2:
+            raise RuntimeError("two frontiers_begin() passes are in flight: call frontiers_end() first")
         if self.world_size == 1 and hasattr(self.band, "frontiers_begin"):
             self.band.frontiers_begin()
-            self._pending = ("band", None)
+            self._pending.append(("band", None))
         elif self.world_size > 1 and self._dev_path:
-            self._device_enqueue()
-            self._pending = ("merge", None)
+            gexp = self._device_enqueue()
+            with self._torch.cuda.stream(self.stream):
+                self.band.merge_bands_begin(gexp.data_ptr(), self.world_size, self.rec_cap, self.min_size)
+            self._pending.append(("merge", None))
         else:  # host exchange (or a non-libdm band): computed now
-            self._pending = ("done", self.frontiers())
+            self._pending.append(("done", self.frontiers()))
 
     def frontiers_end(self) -> Frontiers:
-        kind, res = self._pending
-        self._pending = None
+        """Clusters of the oldest pass started with frontiers_begin()."""
+        kind, res = self._pending.popleft()
         if kind == "band":
             fr = self.band.frontiers_end()
             # slot overflow (workspace grown): rerun on the map as it is now
             return fr if fr is not None else self.band.frontiers()
         if kind == "merge":
-            return self._device_finish()
+            return self._device_finish(self.band.merge_bands_end())
         return res
 
     def _frontiers_host(self, want_mask, want_labels) -> Frontiers:

@@ -83,12 +83,18 @@ def test_frontiers_end_protocol():
         assert len(ref) > 2
         lib, h = m._lib, m._handle()
         n = ctypes.c_int64(-1)
-        # end without begin, begin twice, synchronous pass while one is pending
+        # end without begin; two passes may be in flight, a third is refused
         assert lib.dm_frontiers_end(h, None, 0, ctypes.byref(n)) == _ffi.DM_ERR_INVALID_ARG
         assert lib.dm_frontiers_begin(h) == 0
+        assert lib.dm_frontiers_begin(h) == 0
         assert lib.dm_frontiers_begin(h) == _ffi.DM_ERR_INVALID_ARG
-        with pytest.raises(dm.DmError):
-            m.frontiers()
+        # a synchronous pass while two are pending uses its own readback slot
+        np.testing.assert_array_equal(m.frontiers().clusters, ref)
+        # a merge end while the oldest pending pass is a frontier pass
+        assert lib.dm_merge_bands_end(h, None, 0, ctypes.byref(n)) == _ffi.DM_ERR_INVALID_ARG
+        buf2 = np.empty(len(ref), dtype=np.dtype(dm.CLUSTER_DTYPE))
+        assert lib.dm_frontiers_end(h, buf2.ctypes.data_as(ctypes.c_void_p), len(ref), ctypes.byref(n)) == 0
+        np.testing.assert_array_equal(buf2, ref)
         # too small a buffer: DM_ERR_CAPACITY with the count, the pass stays pending
         assert lib.dm_frontiers_end(h, None, 0, ctypes.byref(n)) == _ffi.DM_ERR_CAPACITY
         assert n.value == len(ref)
@@ -122,6 +128,31 @@ def test_sharded_single_band_pipelined(oracle_lib):
             np.testing.assert_array_equal(fr.clusters, expect[k])
     finally:
         sm.close()
+
+
+@pytest.mark.parametrize("W,H,S,N,nb,seed", [(1500, 1500, 8, 1024, 7, 47), (700, 500, 3, 720, 6, 48)])
+def test_two_passes_in_flight_match_oracle(oracle_lib, W, H, S, N, nb, seed):
+    """Depth-2 pipelining: pass k is collected after batch k+2's integrate was
+    enqueued (two frontier passes in flight); each equals the oracle's
+    frontiers after batch k."""
+    p, batches, amin, inc = cases.world_case(seed, W, H, 0.05, S, N, nb, region_frac=0.6)
+    om, expect = _oracle_steps(oracle_lib, p, batches, amin, inc)
+    dev = _device_batches(batches)
+    with dm.OccupancyMapper(p) as m:
+        m.set_overlap(True)
+        got = []
+        for k, (pose4, rng) in enumerate(dev):
+            m.integrate_device(pose4.data_ptr(), pose4.shape[0], rng.data_ptr(), N, amin, inc)
+            if k > 1:
+                got.append(m.frontiers_end())
+            m.frontiers_begin()
+        got.append(m.frontiers_end())
+        got.append(m.frontiers_end())
+        assert len(got) == len(expect)
+        for k, fr in enumerate(got):
+            assert fr is not None
+            np.testing.assert_array_equal(fr.clusters, expect[k])
+        assert_map_equal(m, om)
 
 
 @pytest.mark.parametrize("P,W,H,seed", [(2, 300, 640, 3), (4, 1000, 1024, 7)])

@@ -25,7 +25,7 @@ NAMES = {
                  5: "roots", 6: "sums+slot atomic", 7: "slot/border/edge writes", 8: "empty tile exit",
                  16: "#tiles", 17: "#runs", 18: "#tiles with F"},
     "integrate": {0: "item setup (pieces, prefetch)", 1: "heavy accum", 2: "heavy slab flush",
-                  3: "light accum", 4: "light apply", 8: "heavy_apply loads", 9: "heavy_apply apply", 10: "heavy_apply finish", 11: "plan: shard offsets",
+                  3: "light accum", 5: "light: wait for cell loads", 4: "light apply", 8: "heavy_apply loads", 9: "heavy_apply apply", 10: "heavy_apply finish", 11: "plan: shard offsets",
                   12: "plan: list loads", 13: "plan: scans", 14: "plan: writes", 16: "#light items",
                   17: "#heavy items", 18: "#light pieces", 19: "#heavy pieces", 20: "#heavy tiles applied"},
 }
