@@ -56,11 +56,18 @@ def parse():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1")
     ap.add_argument("--device-override", type=int, default=None,
                     help="put every rank on this GPU (rehearsal with --backend gloo)")
+    ap.add_argument("--config", default="C3", choices=["C3", "C2", "C5"],
+                    help="C3 (default, the bench line): 16384² batches; C2: 4096² single-robot "
+                         "scan-by-scan replay; C5: 65536² @1cm beam-density sweep (single GPU)")
+    ap.add_argument("--scans", type=int, default=10000, help="C2: scans in the replay")
+    ap.add_argument("--sweep", default="12,48,192,768,4096", help="C5: beams per scan")
     return ap.parse_args()
 
 
 def main():
     args = parse()
+    if args.config != "C3":
+        return run_config(args)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -367,6 +374,266 @@ def _cpu_model():
     except OSError:
         pass
     return None
+
+
+# ---------------------------------------------------------------------------
+# Secondary BASELINE configs (single GPU, not the bench line): C2 replay and
+# the C5 beam-density sweep.  Same step definition as C3 (integrate + full
+# frontier extraction, pipelined), same roofline bookkeeping.
+# ---------------------------------------------------------------------------
+
+def _profiled_roofline(band, run, U_mean, T_mean, TH_mean):
+    """Per-kernel average launch time (HIP events on the library's stream)
+    over `run()`, and the k_tile_accum roofline (SURVEY.md §8(d) bytes)."""
+    band.profile(True)
+    band.profile_reset()
+    run()
+    kstats = band.profile_read()
+    band.profile(False)
+    avg = {name: tot / max(1, n) for name, (n, tot) in kstats.items()}
+    t_ms = avg.get("tile_accum", float("nan"))
+    bytes_accum = (TILE_APPLY_BYTES_PER_UPDATE * U_mean
+                   + TILE_APPLY_BYTES_PER_TOUCHED * (T_mean - TH_mean))
+    achieved = bytes_accum / (t_ms * 1e-3) / 1e9 if t_ms > 0 else None
+    return avg, {
+        "kernel": "tile_accum", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
+        "traffic": None, "avg_launch_ms": t_ms, "algorithmic_bytes_per_launch": bytes_accum,
+        "bytes_model": "8*U + 25*(T - T_heavy) per call (SURVEY.md §8(d) per-unit figures)",
+    }
+
+
+def _pipelined(mapper, integrate, ks):
+    """integrate(k) + frontier pass per k, step k's pass collected after step
+    k+1's integrate was enqueued (as the C3 bench)."""
+    fr = None
+
+    def end():
+        r = mapper.frontiers_end()
+        return r if r is not None else mapper.frontiers()
+
+    first = True
+    for k in ks:
+        integrate(k)
+        if not first:
+            fr = end()
+        mapper.frontiers_begin()
+        first = False
+    if not first:
+        fr = end()
+    return fr
+
+
+def run_config(args):
+    import numpy as np
+    import torch
+
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1 or args.gpus != 1:
+        raise SystemExit(f"--config {args.config} is a single-GPU measurement")
+    dev_i = args.device_override or 0
+    torch.cuda.set_device(dev_i)
+    dev = torch.device("cuda", dev_i)
+    import dm
+    from dm import synth
+
+    world, W, H, res, ox, oy = synth.config_world(args.config, args.seed)
+    params = dm.default_params(W, H, resolution=res)
+    params.origin_x, params.origin_y = ox, oy
+    amin = float(synth.LD06_ANGLE_MIN)
+    base = {
+        "metric": f"beam-cell updates/sec + frontier-extract ms ({args.config})",
+        "unit": "beam-cell updates/s", "n_gpus": 1, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int32/u32 ray math + fp32 log-odds (fp64 endpoints)",
+        "data": "synthetic: seeded rectangle world, random-walk robots, LD06-format scans",
+    }
+    mapper = dm.OccupancyMapper(params, device=dev_i)
+    mapper.set_overlap(True)
+    try:
+        if args.config == "C2":
+            out = _run_c2(args, np, torch, synth, mapper, params, amin, dev)
+        else:
+            out = _run_c5(args, np, torch, synth, mapper, params, amin, dev, world)
+    finally:
+        mapper.close()
+    out = {**base, **out}
+    print(json.dumps(out), flush=True)
+    return out
+
+
+def _run_c2(args, np, torch, synth, m, params, amin, dev):
+    """C2: 4096² @5 cm, one robot, N=360, scan-by-scan replay (S=1): every
+    scan is integrated and followed by a full frontier extraction."""
+    N, n = 360, args.scans
+    inc = float(synth.ld06_angle_increment(N))
+    world = synth.config_world("C2", args.seed)[0]
+    stream = synth.ScanStream(world, 1, N, args.seed * 1000 + 2)
+    t_gen = time.perf_counter()
+    batches = [stream.next_batch() for _ in range(n)]
+    t_gen = time.perf_counter() - t_gen
+    poses = np.concatenate([b[0] for b in batches])
+    ranges = np.ascontiguousarray(np.concatenate([b[1] for b in batches]), np.float32)
+    d_pose = torch.from_numpy(synth.pose4(poses)).to(dev)
+    d_rng = torch.from_numpy(ranges).to(dev)
+    torch.cuda.synchronize()
+    p0, r0 = d_pose.data_ptr(), d_rng.data_ptr()
+
+    def integrate(k):
+        m.integrate_device(p0 + 32 * k, 1, r0 + 4 * N * k, N, amin, inc)
+
+    # per-scan U / T (properties of the scan, not of the map), untimed
+    U = T = TH = 0
+    for k in range(n):
+        integrate(k)
+        st = m.last_stats()
+        U += st["updates"]
+        T += st["touched"]
+        TH += st["touched_heavy"]
+    m.reset()
+    _pipelined(m, integrate, range(min(args.warmup * 20, n)))
+    m.reset()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fr = _pipelined(m, integrate, range(n))
+    m.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    reps = min(200, n)
+    ti, tf = [], []
+    for k in range(reps):
+        a = time.perf_counter()
+        integrate(k)
+        m.synchronize()
+        ti.append(time.perf_counter() - a)
+    for _ in range(reps):
+        a = time.perf_counter()
+        m.frontiers()
+        tf.append(time.perf_counter() - a)
+    avg, roof = _profiled_roofline(m, lambda: [(integrate(k), m.frontiers()) for k in range(reps)],
+                                   U / n, T / n, TH / n)
+    cpu = None
+    if args.cpu_seconds > 0:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle
+
+        oracle.build()
+        om = oracle.OracleMap(params)
+        u_c, t_i, t_f, done = 0, 0.0, [], 0
+        for k in range(n):
+            a = time.perf_counter()
+            u_c += om.integrate(poses[k:k + 1], ranges[k:k + 1], amin, inc)[0]
+            t_i += time.perf_counter() - a
+            a = time.perf_counter()
+            om.frontiers(want_mask=False, want_labels=False)
+            t_f.append(time.perf_counter() - a)
+            done += 1
+            if t_i + sum(t_f) > args.cpu_seconds:
+                break
+        cpu = {"value": u_c / t_i, "unit": "beam-cell updates/s", "cores": 1, "kind": "port",
+               "sample": f"first {done} scans of the replay, integrate + frontier pass per scan",
+               "scans_per_s": done / (t_i + sum(t_f)), "frontier_ms": float(np.median(t_f)) * 1e3,
+               "cpu": _cpu_model()}
+    return {
+        "value": U / elapsed, "steps": n, "warmup": min(args.warmup * 20, n),
+        "ms_per_step": elapsed / n * 1e3, "scans_per_s": n / elapsed,
+        "config": {"workload": f"C2: 4096² grid @5cm, single robot, {n}-scan replay x {N} beams, "
+                               "integrate + full frontier extraction per scan (S=1)",
+                   "grid": [4096, 4096], "resolution_m": 0.05, "scans_per_batch": 1,
+                   "beams_per_scan": N, "parallelism": "single GPU"},
+        "updates_total": U, "touched_total": T,
+        "integrate_ms": float(np.median(ti)) * 1e3, "frontier_ms": float(np.median(tf)) * 1e3,
+        "clusters": len(fr) if fr is not None else None, "kernel_avg_ms": avg, "roofline": roof,
+        "pipelined": "scan k+1's integrate front-end overlaps scan k's frontier pass",
+        "cpu_baseline": cpu, "gen_seconds": t_gen,
+    }
+
+
+def _run_c5(args, np, torch, synth, m, params, amin, dev, world):
+    """C5: 65536² @1 cm (12 m = 1200 cells), 64 robots, beam-density sweep:
+    for each N, K pipelined steps of integrate(64 x N) + frontier pass on a
+    fresh map."""
+    S = args.robots
+    sweep = [int(x) for x in args.sweep.split(",") if x]
+    rows, cpu = [], None
+    for N in sweep:
+        inc = float(synth.ld06_angle_increment(N))
+        stream = synth.ScanStream(world, S, N, args.seed * 1000 + 7 + N)
+        pool = [stream.next_batch() for _ in range(max(2, min(args.pool, 4)))]
+        dpool = [(torch.from_numpy(synth.pose4(p)).to(dev),
+                  torch.from_numpy(np.ascontiguousarray(r, np.float32)).to(dev)) for p, r in pool]
+        torch.cuda.synchronize()
+
+        def integrate(k):
+            pp, rr = dpool[k % len(dpool)]
+            m.integrate_device(pp.data_ptr(), pp.shape[0], rr.data_ptr(), N, amin, inc)
+
+        stats = []
+        for k in range(len(dpool)):
+            integrate(k)
+            stats.append(m.last_stats())
+        m.reset()
+        _pipelined(m, integrate, range(args.warmup))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fr = _pipelined(m, integrate, range(args.warmup, args.warmup + args.steps))
+        m.synchronize()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        U = sum(stats[k % len(stats)]["updates"] for k in range(args.warmup, args.warmup + args.steps))
+        ti, tf = [], []
+        for k in range(max(3, min(args.steps, 10))):
+            a = time.perf_counter()
+            integrate(k)
+            m.synchronize()
+            ti.append(time.perf_counter() - a)
+            a = time.perf_counter()
+            m.frontiers()
+            tf.append(time.perf_counter() - a)
+        mean = lambda key: float(np.mean([st[key] for st in stats]))  # noqa: E731
+        avg, roof = _profiled_roofline(m, lambda: [(integrate(k), m.frontiers()) for k in range(5)],
+                                       mean("updates"), mean("touched"), mean("touched_heavy"))
+        rows.append({"beams_per_scan": N, "value": U / elapsed,
+                     "ms_per_step": elapsed / args.steps * 1e3,
+                     "integrate_ms": float(np.median(ti)) * 1e3,
+                     "frontier_ms": float(np.median(tf)) * 1e3,
+                     "integrate_updates_per_s": mean("updates") / float(np.median(ti)),
+                     "updates_per_batch": mean("updates"), "touched_cells_per_batch": mean("touched"),
+                     "clusters": len(fr) if fr is not None else None,
+                     "kernel_avg_ms": avg, "roofline": roof})
+        if N == sweep[-1] and args.cpu_seconds > 0:
+            # CPU restatement, integrate only: its frontier pass over 2^32
+            # cells needs 64 GiB of int64 work arrays
+            sys.path.insert(0, os.path.join(REPO, "oracle"))
+            import oracle
+
+            oracle.build()
+            om = oracle.OracleMap(params)
+            u_c, t_c, done = 0, 0.0, 0
+            for p_, r_ in pool:
+                a = time.perf_counter()
+                u_c += om.integrate(p_, r_, amin, inc)[0]
+                t_c += time.perf_counter() - a
+                done += 1
+                if t_c > args.cpu_seconds:
+                    break
+            del om
+            cpu = {"value": u_c / t_c, "unit": "beam-cell updates/s", "cores": 1, "kind": "port",
+                   "sample": f"{done} batch(es) of {S}x{N} beams into a fresh 65536² map "
+                             "(integrate only)", "cpu": _cpu_model()}
+        m.reset()
+        del dpool
+    head = rows[-1]
+    return {
+        "value": head["value"], "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": head["ms_per_step"],
+        "config": {"workload": f"C5: 65536² grid @1cm, {S}-scan batches, beam-density sweep "
+                               f"{sweep}; integrate + full frontier extraction per step "
+                               "(value = last sweep point)",
+                   "grid": [65536, 65536], "resolution_m": 0.01, "scans_per_batch": S,
+                   "beams_per_scan": sweep, "parallelism": "single GPU"},
+        "frontier_ms": head["frontier_ms"], "roofline": head["roofline"], "sweep": rows,
+        "pipelined": "step k+1's integrate front-end overlaps step k's frontier pass",
+        "cpu_baseline": cpu,
+    }
 
 
 if __name__ == "__main__":

@@ -151,6 +151,21 @@ int ensure_trig(dm_grid* g, int32_t N, float amin, float inc) {
   return DM_OK;
 }
 
+}  // namespace
+
+// Record workspace of the row-bucket sort (k_bs_*): >= every record count a
+// sort may be asked to order (band slot_cap, merge m_cap).
+int dm_grow_bucket_sort(dm_grid* g, int64_t n) {
+  if (n <= g->bs_cap) return DM_OK;
+  int rc = dev_alloc(&g->bs_key, n, "bucket-sort keys");
+  if (!rc) rc = dev_alloc(&g->bs_idx, n, "bucket-sort indices");
+  if (rc) { g->bs_cap = 0; return rc; }
+  g->bs_cap = n;
+  return DM_OK;
+}
+
+namespace {
+
 int grow_slots(dm_grid* g, int64_t need) {
   int64_t cap = std::max<int64_t>(need, 2 * g->slot_cap);
   if (cap < (1 << 16)) cap = 1 << 16;
@@ -170,6 +185,7 @@ int grow_slots(dm_grid* g, int64_t need) {
   g->out_clu = g->rb[g->rb_head].out_clu;
   if (!rc) rc = dev_alloc(&g->slot_k, cap, "slot cluster index");
   if (!rc) rc = dev_alloc(&g->rank_of, cap, "cluster sorted position");
+  if (!rc) rc = dm_grow_bucket_sort(g, cap);
   if (rc) return rc;
   g->slot_cap = cap;
   return DM_OK;
@@ -240,6 +256,7 @@ int grow_merge(dm_grid* g, int64_t n) {
   for (int sl = 0; sl <= dm_grid::kRbSlots && !rc; ++sl)
     rc = dev_alloc(&g->rb[sl].m_out, n, "merged clusters (sorted)");
   ++g->rb_gen;
+  if (!rc) rc = dm_grow_bucket_sort(g, n);
   if (rc) { g->m_cap = 0; return rc; }
   g->m_cap = n;
   return DM_OK;
@@ -386,6 +403,8 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if ((rc = dev_alloc(&g->edge_slot, 2 * g->W, "edge slots"))) return fail(rc);
   if ((rc = dev_alloc(&g->edge_label, 2 * g->W, "edge labels"))) return fail(rc);
   if ((rc = dev_alloc(&g->halo, 2 * g->W, "halo rows"))) return fail(rc);
+  if ((rc = dev_alloc(&g->bs_rows, 3 * (kBuckets + 1), "bucket-sort buckets"))) return fail(rc);
+  DM_HIP(hipMemset(g->bs_rows, 0, sizeof(int32_t) * 3 * (kBuckets + 1)));  // counts start at zero
   if ((rc = grow_slots(g, 1 << 16))) return fail(rc);
   for (int sl = 0; sl <= dm_grid::kRbSlots; ++sl)
     if ((rc = grow_host_out(g, sl, 1 << 14))) return fail(rc);
@@ -442,6 +461,7 @@ int dm_destroy(dm_grid* g) {
   dev_free(g->trig);
   dev_free(g->hitems); dev_free(g->litems); dev_free(g->heavy_list); dev_free(g->slabs);
   dev_free(g->pose4); dev_free(g->ranges); 
+  dev_free(g->bs_rows); dev_free(g->bs_key); dev_free(g->bs_idx);
   dev_free(g->border); dev_free(g->ftiles); dev_free(g->slot_label); dev_free(g->slot_parent); dev_free(g->slot_root);
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
   dev_free(g->edge_slot); dev_free(g->edge_label); dev_free(g->mask); dev_free(g->labels);
@@ -725,6 +745,7 @@ int merge_readback(dm_grid* g, int slot, int64_t n, dm_cluster* out, int64_t cap
                         (unsigned long long)g->h_mcnt[1], (unsigned long long)g->h_mcnt[3]);
   }
   const int64_t K = (int64_t)g->h_mcnt[0];
+  g->msort_hint = K;
   if (n_out) *n_out = K;
   if (K > cap)
     return dm_set_error(DM_ERR_CAPACITY, "%lld clusters, capacity %lld", (long long)K, (long long)cap);

@@ -566,6 +566,47 @@ __global__ __launch_bounds__(256) void k_frontier_compact(FGeom g, const int32_t
   }
 }
 
+// Block 0 of the sort kernel (the pipeline's last kernel: every counter is
+// final) sets the sorted flag and writes the readback header: the counters,
+// then the fullest slot shard; the host reads it together with the first
+// sorted records from the mapped buffer in ONE step.
+__device__ inline void write_rb_header(int64_t K, int64_t cap, unsigned long long* sorted,
+                                       const unsigned long long* __restrict__ cnt, int ncnt,
+                                       int sorted_idx, const unsigned long long* __restrict__ fsh,
+                                       dm_cluster* host_out) {
+  const int tid = threadIdx.x;
+  if (tid == 0) *sorted = K <= cap ? 1ull : 0ull;
+  if (!host_out) return;
+  unsigned long long* header = dm_rb_header(host_out);
+  if (tid < ncnt) header[tid] = tid == sorted_idx ? (K <= cap ? 1ull : 0ull) : cnt[tid];
+  if (tid == ncnt && fsh) {
+    unsigned long long most = 0;
+    for (int i = 0; i < kShards; ++i) most = max(most, fsh[i * kShardWords + SH_SLOT]);
+    header[ncnt] = most;
+  }
+}
+
+// Raw record i ([4] int64 label, size, sum_x, sum_y) -> dm_cluster at its
+// sorted position, centroid cx_m = ox + ((double)sum_x / (double)size + 0.5)
+// * res (SPEC a10: one IEEE division, then add; no FMA contraction).
+__device__ inline void put_sorted(double ox, double oy, double res, const long long* __restrict__ clusters,
+                                  int64_t i, int64_t rank, dm_cluster* __restrict__ out,
+                                  int32_t* __restrict__ rank_of, dm_cluster* __restrict__ host_out,
+                                  int64_t host_cap) {
+  dm_cluster c;
+  c.label = clusters[4 * i];
+  c.size = clusters[4 * i + 1];
+  c.sum_x = clusters[4 * i + 2];
+  c.sum_y = clusters[4 * i + 3];
+  const double mx = (double)c.sum_x / (double)c.size;
+  const double my = (double)c.sum_y / (double)c.size;
+  c.cx_m = ox + (mx + 0.5) * res;
+  c.cy_m = oy + (my + 0.5) * res;
+  out[rank] = c;
+  if (host_out && rank < host_cap) host_out[rank] = c;  // mapped host readback
+  if (rank_of) rank_of[i] = (int32_t)rank;
+}
+
 // Cluster list sorted by label, with centroids (SPEC a10).  Labels are
 // unique (one per component), so a record's position is the number of
 // records with a smaller label.  One workgroup per 64 records (lane = record),
@@ -599,19 +640,7 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
   __shared__ int32_t part[kSortWaves][64];
   const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
   const int64_t K = (int64_t)*count;
-  if (blockIdx.x == 0 && tid == 0) *sorted = K <= cap ? 1ull : 0ull;
-  if (host_out && blockIdx.x == 0) {
-    unsigned long long* header = dm_rb_header(host_out);
-    // readback header (this is the pipeline's last kernel: every counter is
-    // final): the counters, then the fullest slot shard; the host copies it
-    // together with the first sorted records in ONE transfer
-    if (tid < ncnt) header[tid] = tid == sorted_idx ? (K <= cap ? 1ull : 0ull) : cnt[tid];
-    if (tid == ncnt && fsh) {
-      unsigned long long most = 0;
-      for (int i = 0; i < kShards; ++i) most = max(most, fsh[i * kShardWords + SH_SLOT]);
-      header[ncnt] = most;
-    }
-  }
+  if (blockIdx.x == 0) write_rb_header(K, cap, sorted, cnt, ncnt, sorted_idx, fsh, host_out);
   if (K > cap) return;
   const int64_t i = (int64_t)blockIdx.x * 64 + lane;
   if ((int64_t)blockIdx.x * 64 >= K) return;  // whole workgroup: no barrier skipped
@@ -647,18 +676,109 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
     int32_t rank = 0;
 #pragma unroll
     for (int q = 0; q < kSortWaves; ++q) rank += part[q][lane];
-    dm_cluster c;
-    c.label = key;
-    c.size = clusters[4 * i + 1];
-    c.sum_x = clusters[4 * i + 2];
-    c.sum_y = clusters[4 * i + 3];
-    const double mx = (double)c.sum_x / (double)c.size;
-    const double my = (double)c.sum_y / (double)c.size;
-    c.cx_m = ox + (mx + 0.5) * res;
-    c.cy_m = oy + (my + 0.5) * res;
-    out[rank] = c;
-    if (host_out && rank < host_cap) host_out[rank] = c;  // mapped host readback
-    if (rank_of) rank_of[i] = rank;
+    put_sorted(ox, oy, res, clusters, i, rank, out, rank_of, host_out, host_cap);
+  }
+}
+
+// ---- row-bucket sort for many clusters (K > kBucketSortMin) ---------------
+// The rank sort is O(K^2): ~0.1 ms at 23k clusters, far more at the 2e5+
+// clusters of a sparse 1 cm map (C5).  Labels are row-major cell indices, so
+// sorting by label = counting sort by row, then by column inside the row:
+// Buckets are runs of 2^shift consecutive labels (at most kBuckets of them
+// over the label range of the rows sorted):
+//   k_bs_count  per-bucket cluster counts (one atomic per record)
+//   k_bs_scan   one workgroup: exclusive offsets per bucket, cursors, counts
+//               zeroed again for the next sort
+//   k_bs_place  each label to its bucket's segment (atomic cursor: unordered)
+//   k_bs_rank   position = bucket offset + labels of the same segment that
+//               are smaller (a bucket holds few components), then the same
+//               record write + readback header as k_rank_sort.
+// Every kernel reads the device-side count; K > cap leaves the result
+// unsorted (flag 0), as the rank sort does.
+__global__ __launch_bounds__(256) void k_bs_count(const long long* __restrict__ clusters,
+                                                  const unsigned long long* __restrict__ count, int64_t cap,
+                                                  long long base, int shift,
+                                                  int32_t* __restrict__ rcnt) {
+  const int64_t K = (int64_t)*count;
+  if (K > cap) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < K; i += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(&rcnt[(clusters[4 * i] - base) >> shift], 1);
+}
+
+constexpr int kScanThreads = 1024;
+static_assert(kBuckets == 4 * kScanThreads, "k_bs_scan loads 4 buckets per thread");
+
+// One workgroup, every bucket count loaded at once (4 contiguous per
+// thread): exclusive offsets and cursors, counts zeroed for the next sort.
+__global__ __launch_bounds__(kScanThreads) void k_bs_scan(const unsigned long long* __restrict__ count,
+                                                          int64_t cap, int nbk, int32_t* __restrict__ rcnt,
+                                                          int32_t* __restrict__ roff, int32_t* __restrict__ rcur) {
+  __shared__ int32_t wsum[kScanThreads / 64];
+  if ((int64_t)*count > cap) return;
+  const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+  int32_t c[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) c[q] = 4 * tid + q < nbk ? rcnt[4 * tid + q] : 0;
+  const int32_t s = c[0] + c[1] + c[2] + c[3];
+  int32_t incl = s;  // inclusive wave scan, then across the 16 waves
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int32_t v = __shfl_up(incl, d);
+    if (lane >= d) incl += v;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int32_t run = incl - s;
+  for (int q = 0; q < w; ++q) run += wsum[q];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int b = 4 * tid + q;
+    if (b < nbk) {
+      roff[b] = run;
+      rcur[b] = run;
+      rcnt[b] = 0;
+    }
+    run += c[q];
+  }
+  if (tid == kScanThreads - 1) roff[nbk] = run;
+}
+
+__global__ __launch_bounds__(256) void k_bs_place(const long long* __restrict__ clusters,
+                                                  const unsigned long long* __restrict__ count, int64_t cap,
+                                                  long long base, int shift,
+                                                  int32_t* __restrict__ rcur, long long* __restrict__ bkey,
+                                                  int32_t* __restrict__ bidx) {
+  const int64_t K = (int64_t)*count;
+  if (K > cap) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < K; i += (int64_t)gridDim.x * blockDim.x) {
+    const long long key = clusters[4 * i];
+    const int32_t p = atomicAdd(&rcur[(key - base) >> shift], 1);
+    bkey[p] = key;
+    bidx[p] = (int32_t)i;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bs_rank(double ox, double oy, double res,
+                                                 const long long* __restrict__ clusters,
+                                                 const unsigned long long* __restrict__ count, int64_t cap,
+                                                 long long base, int shift,
+                                                 const int32_t* __restrict__ roff,
+                                                 const long long* __restrict__ bkey,
+                                                 const int32_t* __restrict__ bidx, dm_cluster* __restrict__ out,
+                                                 int32_t* __restrict__ rank_of, unsigned long long* sorted,
+                                                 const unsigned long long* __restrict__ cnt, int ncnt,
+                                                 int sorted_idx, const unsigned long long* __restrict__ fsh,
+                                                 dm_cluster* __restrict__ host_out, int64_t host_cap) {
+  const int64_t K = (int64_t)*count;
+  if (blockIdx.x == 0) write_rb_header(K, cap, sorted, cnt, ncnt, sorted_idx, fsh, host_out);
+  if (K > cap) return;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < K; p += (int64_t)gridDim.x * blockDim.x) {
+    const long long key = bkey[p];
+    const int64_t b = (key - base) >> shift;
+    const int32_t lo = roff[b], hi = roff[b + 1];
+    int64_t rank = lo;
+    for (int32_t j = lo; j < hi; ++j) rank += bkey[j] < key;
+    put_sorted(ox, oy, res, clusters, bidx[p], rank, out, rank_of, host_out, host_cap);
   }
 }
 
@@ -727,6 +847,40 @@ int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const uns
   return DM_OK;
 }
 
+int dm_launch_bucket_sort(dm_grid* g, const long long* clusters, const unsigned long long* d_count,
+                          int64_t max_records, int64_t row_base, int64_t rows, dm_cluster* out,
+                          int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
+                          int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
+                          int64_t host_cap) {
+  if (max_records > g->bs_cap)
+    return dm_set_error(DM_ERR_INVALID_ARG, "bucket sort: %lld records exceed its workspace",
+                        (long long)max_records);
+  // buckets of 2^shift consecutive labels over the rows' label range
+  const long long base = row_base * g->W;
+  const int64_t span = rows * g->W;
+  int shift = 0;
+  while (((span - 1) >> shift) + 1 > kBuckets) ++shift;
+  const int nbk = (int)(((span - 1) >> shift) + 1);
+  int32_t* rcnt = g->bs_rows;
+  int32_t* roff = rcnt + (kBuckets + 1);
+  int32_t* rcur = roff + (kBuckets + 1);
+  const int eg = grid_for(max_records, 256, 2048);
+  hipLaunchKernelGGL(k_bs_count, dim3(eg), dim3(256), 0, g->stream, clusters, d_count, max_records, base,
+                     shift, rcnt);
+  DM_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_bs_scan, dim3(1), dim3(kScanThreads), 0, g->stream, d_count, max_records, nbk, rcnt,
+                     roff, rcur);
+  DM_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_bs_place, dim3(eg), dim3(256), 0, g->stream, clusters, d_count, max_records, base,
+                     shift, rcur, g->bs_key, g->bs_idx);
+  DM_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_bs_rank, dim3(eg), dim3(256), 0, g->stream, g->p.origin_x, g->p.origin_y,
+                     g->p.resolution, clusters, d_count, max_records, base, shift, roff, g->bs_key,
+                     g->bs_idx, out, rank_of, d_sorted, cnt, ncnt, sorted_idx, fsh, host_out, host_cap);
+  DM_HIP(hipGetLastError());
+  return DM_OK;
+}
+
 // Enqueues the band pipeline (no synchronisation): tile list, tile CCL,
 // border merge, roots, compaction, sort.  Shared by dm_launch_frontiers and
 // the cross-band export (dm_merge.hip).
@@ -779,9 +933,15 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
     DM_HIP(hipGetLastError());
   }
   dm_timer_begin(g, "sort_clusters", &t);
-  const int rc = dm_launch_rank_sort(g->stream, g->clusters, g->cnt + CNT_CLUSTERS, g->slot_cap, g->p.origin_x,
-                           g->p.origin_y, g->p.resolution, g->out_clu, g->rank_of, g->cnt + CNT_SORTED,
-                           g->cnt, CNT_N, CNT_SORTED, g->fsh, g->h_out_dev, g->h_out_cap);
+  // the last collected pass predicts this one's cluster count (either sort
+  // is exact for any count; only their speed differs)
+  const int rc = g->sort_hint > kBucketSortMin
+      ? dm_launch_bucket_sort(g, g->clusters, g->cnt + CNT_CLUSTERS, g->slot_cap, g->row0, g->R, g->out_clu,
+                              g->rank_of, g->cnt + CNT_SORTED, g->cnt, CNT_N, CNT_SORTED, g->fsh,
+                              g->h_out_dev, g->h_out_cap)
+      : dm_launch_rank_sort(g->stream, g->clusters, g->cnt + CNT_CLUSTERS, g->slot_cap, g->p.origin_x,
+                            g->p.origin_y, g->p.resolution, g->out_clu, g->rank_of, g->cnt + CNT_SORTED,
+                            g->cnt, CNT_N, CNT_SORTED, g->fsh, g->h_out_dev, g->h_out_cap);
   dm_timer_end(g, &t);
   if (rc) return rc;
   return DM_OK;
@@ -802,6 +962,7 @@ int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied) {
     return DM_ERR_CAPACITY;
   }
   *n_clusters = (int64_t)g->h_cnt[CNT_CLUSTERS];
+  g->sort_hint = *n_clusters;
   return DM_OK;
 }
 

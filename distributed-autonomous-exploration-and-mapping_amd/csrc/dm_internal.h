@@ -195,6 +195,14 @@ struct dm_grid {
   int has_halo[2] = {0, 0};
   bool frontier_valid = false;
 
+  // large-K cluster sort (row buckets, dm_frontier.hip k_bs_*): used when
+  // the last collected pass of its kind had more than kBucketSortMin clusters
+  int32_t* bs_rows = nullptr;     // [3][kBuckets + 1] per-bucket counts (kept zero), offsets, cursors
+  long long* bs_key = nullptr;    // [bs_cap] labels placed by row
+  int32_t* bs_idx = nullptr;      // [bs_cap] their record indices
+  int64_t bs_cap = 0;
+  int64_t sort_hint = 0, msort_hint = 0;  // clusters of the last band / merge readback
+
   // cross-band merge workspace (dm_merge.hip), sized nranks * rec_cap
   int64_t m_cap = 0;
   int32_t* m_parent = nullptr;
@@ -247,6 +255,17 @@ int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const uns
                         int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
                         int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
                         int64_t host_cap);
+// Clusters above which the row-bucket sort replaces the O(K^2) rank sort.
+constexpr int64_t kBucketSortMin = 4096;
+constexpr int kBuckets = 4096;  // row buckets of the bucket sort (k_bs_scan: 4 per thread)
+int dm_grow_bucket_sort(dm_grid* g, int64_t n);
+// Row-bucket sort of the raw records (labels of rows [row_base, row_base +
+// rows)): same outputs, readback header and flags as dm_launch_rank_sort.
+int dm_launch_bucket_sort(dm_grid* g, const long long* clusters, const unsigned long long* d_count,
+                          int64_t max_records, int64_t row_base, int64_t rows, dm_cluster* out,
+                          int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
+                          int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
+                          int64_t host_cap);
 // cross-band exchange (dm_merge.hip)
 int64_t dm_export_nbytes(int64_t W, int64_t rec_cap);
 int dm_launch_export(dm_grid* g, void* d_export, int64_t rec_cap);
