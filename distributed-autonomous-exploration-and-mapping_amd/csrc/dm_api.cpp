@@ -83,14 +83,19 @@ int validate_params(const dm_params* p) {
 
 int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   const int64_t nb = (int64_t)S * N;
-  const int64_t per_beam = 2 * (g->nmax / DM_TILE) + 8;
-  if (nb > g->beams_cap) {
-    const int64_t blocks = ceil_div(nb, 256);
-    int rc = dev_alloc(&g->beams, nb, "beams");
-    if (!rc) rc = dev_alloc(&g->blk_hist, blocks * 1024, "per-block tile histograms");
-    if (!rc) rc = dev_alloc(&g->blk_n, blocks, "per-block histogram sizes");
-    if (rc) return rc;
-    g->beams_cap = nb;
+  const int64_t chunks = dm_integrate_chunks(g, nb);
+  // pieces per beam: <= 2 per 64 steps + 8, and every chunk adds <= 3
+  const int64_t per_beam = 2 * (g->nmax / DM_TILE) + 8 + 4 * chunks;
+  const int64_t blocks = ceil_div(nb * chunks, 256);  // k_beam_prep / k_scatter workgroups
+  if (nb > g->beams_cap || blocks > g->blk_cap) {
+    const int64_t nbc = std::max<int64_t>(nb, g->beams_cap);
+    const int64_t bc = std::max<int64_t>(blocks, g->blk_cap);
+    int rc = dev_alloc(&g->beams, nbc, "beams");
+    if (!rc) rc = dev_alloc(&g->blk_hist, bc * 1024, "per-block tile histograms");
+    if (!rc) rc = dev_alloc(&g->blk_n, bc, "per-block histogram sizes");
+    if (rc) { g->beams_cap = g->blk_cap = 0; return rc; }
+    g->beams_cap = nbc;
+    g->blk_cap = bc;
   }
   const int64_t segs = nb * per_beam;
   if (segs > g->segs_cap) {

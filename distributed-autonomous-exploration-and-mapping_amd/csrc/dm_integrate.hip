@@ -37,7 +37,29 @@ struct Geom {
   int32_t act_cap;
   int64_t seg_cap;
   int64_t nb;  // beams in this call
+  int32_t chunks, chunk_len;  // each beam enumerated as `chunks` k-ranges (dm_integrate_chunks)
 };
+
+// Thread v of k_beam_prep / k_scatter: beam v % nb, k-range v / nb (chunk-
+// major, so a wave's lanes stay on neighbouring beams and the lane-run /
+// per-block tile aggregation keeps working).  The last chunk runs to the end.
+struct BeamChunk {
+  int64_t b;
+  int32_t k_lo, k_hi;
+};
+
+__device__ inline BeamChunk beam_chunk(const Geom& g, int64_t v) {
+  BeamChunk c;
+  if (g.chunks == 1) {
+    c.b = v; c.k_lo = 0; c.k_hi = 0x7FFFFFFF;
+    return c;
+  }
+  const int32_t q = (int32_t)(v / g.nb);
+  c.b = v - (int64_t)q * g.nb;
+  c.k_lo = q * g.chunk_len;
+  c.k_hi = q + 1 == g.chunks ? 0x7FFFFFFF : c.k_lo + g.chunk_len - 1;
+  return c;
+}
 
 __device__ inline int lane_id() { return __lane_id(); }
 
@@ -127,13 +149,13 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
   const int tid = threadIdx.x;
   for (int e = tid; e < kHash; e += 256) { hkey[e] = -1; hcnt[e] = 0; }
   __syncthreads();
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + tid;
-  const int64_t nb = (int64_t)a.S * a.N;
-  if (b < nb) {
-    const int32_t s = (int32_t)(b / a.N), i = (int32_t)(b % a.N);
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + tid;
+  if (v < g.nb * g.chunks) {
+    const BeamChunk bc = beam_chunk(g, v);
+    const int32_t s = (int32_t)(bc.b / a.N), i = (int32_t)(bc.b % a.N);
     const Beam bm = dm_make_beam(a, pose4, ranges, trig, s, i);
-    beams[b] = bm;
-    if (bm.flags & 1) {
+    if (bc.k_lo == 0) beams[bc.b] = bm;
+    if ((bm.flags & 1) && bc.k_lo <= bm.n) {
       dm_for_each_piece(bm, g.r, [&](int32_t tile, int32_t, int32_t) {
         const LaneRun run = lane_run(tile);
         if (run.head) {
@@ -145,7 +167,7 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
             first_touch(g, tile, old, act_raw, ish, cnt);
           }
         }
-      });
+      }, bc.k_lo, bc.k_hi);
     }
   }
   if (tid == 0) s_nh = 0;
@@ -297,11 +319,12 @@ __global__ __launch_bounds__(256) void k_scatter(RayArgs a, Geom g, const Beam* 
   __shared__ int32_t hbase[kHash];
   const int tid = threadIdx.x;
   for (int e = tid; e < kHash; e += 256) { hkey[e] = -1; hcnt[e] = 0; }
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + tid;
-  const int64_t nb = (int64_t)a.S * a.N;
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + tid;
+  const bool in = v < g.nb * g.chunks;
+  const BeamChunk bc = beam_chunk(g, in ? v : 0);
   Beam bm;
   bm.flags = 0;
-  if (b < nb) bm = beams[b];
+  if (in) bm = beams[bc.b];
   const int32_t nh = blk_n[blockIdx.x];
   __syncthreads();
   const int2* my_hist = blk_hist + (int64_t)blockIdx.x * kHash;
@@ -311,7 +334,7 @@ __global__ __launch_bounds__(256) void k_scatter(RayArgs a, Geom g, const Beam* 
     if (h >= 0) hbase[h] = atomicAdd(&tile_cur[te.x], te.y);
   }
   __syncthreads();
-  const bool valid = (b < nb) && (bm.flags & 1);
+  const bool valid = in && (bm.flags & 1) && bc.k_lo <= bm.n;
   if (valid) {
     dm_for_each_piece(bm, g.r, [&](int32_t tile, int32_t k0, int32_t k1) {
       const LaneRun run = lane_run(tile);
@@ -322,7 +345,7 @@ __global__ __launch_bounds__(256) void k_scatter(RayArgs a, Geom g, const Beam* 
       }
       pos = __shfl(pos, run.head_lane);
       put_piece(g, pieces, (int64_t)pos + run.rank, bm, tile, k0, k1, cnt);
-    });
+    }, bc.k_lo, bc.k_hi);
   }
 }
 
@@ -821,6 +844,8 @@ Geom make_geom(const dm_grid* g) {
   ge.act_cap = (int32_t)g->act_cap;
   ge.seg_cap = g->segs_cap;
   ge.nb = 0;
+  ge.chunks = 1;
+  ge.chunk_len = 0;
   return ge;
 }
 
@@ -880,7 +905,9 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   a.range_max = g->p.range_max;
   Geom ge = make_geom(g);
   ge.nb = nb;
-  const int nblk = (int)((nb + 255) / 256);
+  ge.chunks = dm_integrate_chunks(g, nb);
+  ge.chunk_len = (int32_t)((g->nmax + ge.chunks) / ge.chunks);  // ceil((nmax + 1) / chunks)
+  const int nblk = (int)((nb * ge.chunks + 255) / 256);
   KernelTimer t;
   dm_timer_begin(g, "beam_prep", &t, fs);
   hipLaunchKernelGGL(k_beam_prep, dim3(nblk), dim3(256), 0, fs, a, ge, d_pose4, d_ranges,

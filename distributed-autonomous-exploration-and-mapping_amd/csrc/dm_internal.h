@@ -150,6 +150,7 @@ struct dm_grid {
 
   // integrate workspace
   Beam* beams = nullptr; int64_t beams_cap = 0;
+  int64_t blk_cap = 0;            // workgroups blk_hist / blk_n hold
   int2* blk_hist = nullptr;       // [beam blocks][1024] k_beam_prep's (tile, pieces) histogram
   int32_t* blk_n = nullptr;       // [beam blocks] its entries
   PackedPiece* pieces = nullptr; int64_t segs_cap = 0;  // ray pieces binned by tile
@@ -236,6 +237,18 @@ inline hipError_t dm_mark_tiles(dm_grid* g) {
   if (!g->overlap || !g->tiles_mark_pending) return hipSuccess;
   g->tiles_mark_pending = false;
   return hipEventRecord(g->ev_tiles, g->stream);
+}
+
+// A call with too few beams to fill the chip enumerates each beam's pieces
+// in `chunks` k-ranges on different threads (k_beam_prep / k_scatter): one
+// thread per beam would walk up to 2*nmax/64 pieces serially on a mostly
+// idle GPU (sparse scans, 1 cm maps).  Chunks stay >= 64 steps long.
+inline int32_t dm_integrate_chunks(const dm_grid* g, int64_t nb) {
+  const int64_t want = 512 * (int64_t)(g->n_cu > 0 ? g->n_cu : 256);
+  if (nb <= 0 || nb >= want) return 1;
+  const int64_t by_len = (g->nmax + 1) / 64 > 1 ? (g->nmax + 1) / 64 : 1;
+  const int64_t by_fill = (want + nb - 1) / nb;
+  return (int32_t)(by_fill < by_len ? by_fill : by_len);
 }
 
 // ---- launchers (dm_integrate.hip / dm_frontier.hip) -----------------------

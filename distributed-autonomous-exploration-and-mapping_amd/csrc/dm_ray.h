@@ -117,22 +117,26 @@ DM_HD inline Beam dm_make_beam(const RayArgs& a, const double* pose4, const floa
 // the minor one is monotone in k, so the k at which each coordinate leaves
 // its tile is exact integer arithmetic.  Every pass advances
 // k by >= 1; the pass cap only guards against a logic error.
+// With k_lo / k_hi only the steps k in [k_lo, min(n, k_hi)] are enumerated
+// (a chunk of the beam: pieces are cut at the chunk's ends too).
 template <class Emit>
-DM_HD inline void dm_for_each_piece(const Beam& b, const RayGeom& g, Emit&& emit) {
+DM_HD inline void dm_for_each_piece(const Beam& b, const RayGeom& g, Emit&& emit, int32_t k_lo = 0,
+                                    int32_t k_hi = 0x7FFFFFFF) {
   const int32_t n = b.n;
+  const int32_t kend = n < k_hi ? n : k_hi;
   const int32_t off_a = b.xmajor ? 0 : g.row0;
   const int32_t off_b = b.xmajor ? g.row0 : 0;
   const int32_t lim_a = b.xmajor ? g.TX : g.TY;
   const int32_t lim_b = b.xmajor ? g.TY : g.TX;
-  const int32_t max_iter = 2 * (n / DM_TS) + 8;
+  const int32_t max_iter = 2 * ((kend - k_lo) / DM_TS) + 8;
   // k at which the minor coordinate reaches step count Q:
   //   ceil(n*(2Q-1) / (2*adb)); operands < 2^31 (n, adb <= 16386, Q <= adb+1),
   //   so a double reciprocal (once per beam) + one exact correction replaces a
   //   64-bit integer division per piece
   const int32_t den_b = 2 * b.adb;
   const double rden_b = b.adb > 0 ? 1.0 / (double)den_b : 0.0;
-  int32_t k = 0;
-  for (int32_t it = 0; k <= n && it < max_iter; ++it) {
+  int32_t k = k_lo;
+  for (int32_t it = 0; k <= kend && it < max_iter; ++it) {
     const int32_t q = dm_minor_steps(b, k);
     const int32_t ma = b.sa + k * b.ia - off_a;
     const int32_t mb = b.sb + b.ib * q - off_b;
@@ -151,7 +155,7 @@ DM_HD inline void dm_for_each_piece(const Beam& b, const RayGeom& g, Emit&& emit
       kb = dm_udiv(num + den_b - 1, den_b, rden_b);
     }
     int64_t ke = ka < kb ? ka : kb;
-    if (ke > (int64_t)n + 1) ke = (int64_t)n + 1;
+    if (ke > (int64_t)kend + 1) ke = (int64_t)kend + 1;
     ke -= 1;
     if (ke < k) ke = k;  // never step backwards
     if (ta >= 0 && ta < lim_a && tb >= 0 && tb < lim_b) {

@@ -15,7 +15,7 @@ extern "C" int emu_integrate(int32_t W, int32_t R, int32_t row0, double ox, doub
                              float l_min, float l_max, float occ_t, float free_t, float* L,
                              int8_t* state, int32_t S, const double* pose4, int32_t N,
                              const float* ranges, const double* trig, uint64_t* out_U,
-                             uint64_t* out_T, uint64_t* out_segs) {
+                             uint64_t* out_T, uint64_t* out_segs, int32_t chunk_len) {
   RayGeom g;
   g.W = W; g.R = R; g.row0 = row0;
   g.TX = (W + DM_TS - 1) / DM_TS;
@@ -26,11 +26,19 @@ extern "C" int emu_integrate(int32_t W, int32_t R, int32_t row0, double ox, doub
   const int64_t NT = (int64_t)g.TX * g.TY, nb = (int64_t)S * N;
   std::vector<int32_t> count(NT, 0), slot(NT, -1), act;
   std::vector<Beam> beams(nb);
+  // k_beam_prep / k_scatter may enumerate a beam as k-ranges of chunk_len
+  // steps on different threads (dm_integrate_chunks); 0 = whole beams
+  auto for_chunks = [&](const Beam& bm, auto&& f) {
+    if (chunk_len <= 0) { f(0, 0x7FFFFFFF); return; }
+    for (int32_t k_lo = 0; k_lo <= bm.n; k_lo += chunk_len) f(k_lo, k_lo + chunk_len - 1);
+  };
   for (int64_t b = 0; b < nb; ++b) {  // k_beam_prep
     beams[b] = dm_make_beam(a, pose4, ranges, trig, (int32_t)(b / N), (int32_t)(b % N));
     if (!(beams[b].flags & 1)) continue;
-    dm_for_each_piece(beams[b], g, [&](int32_t t, int32_t, int32_t) {
-      if (count[t]++ == 0) { slot[t] = (int32_t)act.size(); act.push_back(t); }
+    for_chunks(beams[b], [&](int32_t k_lo, int32_t k_hi) {
+      dm_for_each_piece(beams[b], g, [&](int32_t t, int32_t, int32_t) {
+        if (count[t]++ == 0) { slot[t] = (int32_t)act.size(); act.push_back(t); }
+      }, k_lo, k_hi);
     });
   }
   std::vector<int64_t> off(act.size() + 1, 0), cur(act.size());
@@ -40,8 +48,10 @@ extern "C" int emu_integrate(int32_t W, int32_t R, int32_t row0, double ox, doub
   std::vector<Seg> segs(off[act.size()]);
   for (int64_t b = 0; b < nb; ++b) {  // k_scatter
     if (!(beams[b].flags & 1)) continue;
-    dm_for_each_piece(beams[b], g, [&](int32_t t, int32_t k0, int32_t k1) {
-      segs[cur[slot[t]]++] = Seg{b, k0, k1};
+    for_chunks(beams[b], [&](int32_t k_lo, int32_t k_hi) {
+      dm_for_each_piece(beams[b], g, [&](int32_t t, int32_t k0, int32_t k1) {
+        segs[cur[slot[t]]++] = Seg{b, k0, k1};
+      }, k_lo, k_hi);
     });
   }
   uint64_t U = 0, T = 0;

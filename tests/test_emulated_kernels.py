@@ -22,13 +22,13 @@ def emu():
     lib = ctypes.CDLL(os.path.join(NATIVE, "libemu.so"))
     f = lib.emu_integrate
     i32, d, fl, vp = ctypes.c_int32, ctypes.c_double, ctypes.c_float, ctypes.c_void_p
-    f.argtypes = [i32, i32, i32, d, d, d] + [fl] * 8 + [vp, vp, i32, vp, i32, vp, vp, vp, vp, vp]
+    f.argtypes = [i32, i32, i32, d, d, d] + [fl] * 8 + [vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, i32]
     return lib
 
 
 class EmuMap:
-    def __init__(self, lib, p):
-        self.lib, self.p = lib, p
+    def __init__(self, lib, p, chunk_len=0):
+        self.lib, self.p, self.chunk_len = lib, p, chunk_len
         R = int(p.band_rows) if p.band_rows > 0 else int(p.height - p.band_row0)
         self.L = np.zeros((R, int(p.width)), np.float32)
         self.state = np.full((R, int(p.width)), -1, np.int8)
@@ -48,7 +48,7 @@ class EmuMap:
                                p.resolution, p.range_min, p.range_max, p.l_occ, p.l_free, p.l_min,
                                p.l_max, p.occ_thresh, p.free_thresh, ptr(self.L), ptr(self.state), S,
                                ptr(pose4), N, ptr(ranges), ptr(trig), ctypes.byref(U),
-                               ctypes.byref(T), ctypes.byref(G))
+                               ctypes.byref(T), ctypes.byref(G), self.chunk_len)
         assert rc == 0, "incremental piece walk disagrees with the closed form"
         return int(U.value), int(T.value)
 
@@ -68,10 +68,13 @@ def test_emulated_kernels_match_golden(emu, name):
     (257, 513, 6, 700, 0.05, 4, 0, 0), (1000, 300, 4, 2048, 0.02, 5, 0, 0),
     (96, 96, 12, 256, 0.1, 6, 0, 0), (300, 700, 8, 600, 0.05, 7, 320, 192),
     (500, 500, 3, 3000, 0.01, 8, 128, 0)])
-def test_emulated_kernels_random(emu, oracle_lib, W, H, S, N, res, seed, r0, rows):
+@pytest.mark.parametrize("chunk_len", [0, 64, 97])
+def test_emulated_kernels_random(emu, oracle_lib, W, H, S, N, res, seed, r0, rows, chunk_len):
+    """chunk_len > 0: beams enumerated in k-ranges as k_beam_prep / k_scatter
+    do for small batches (dm_integrate_chunks)."""
     p = cases.make_params(W, H, resolution=res, band_row0=r0, band_rows=rows)
     om = oracle_lib.OracleMap(p)
-    m = EmuMap(emu, p)
+    m = EmuMap(emu, p, chunk_len)
     for k in range(2):
         poses, ranges, amin, inc = cases.random_scans(seed * 10 + k, p, S, N,
                                                       spread=4.0 if seed == 6 else 1.0)
