@@ -512,23 +512,58 @@ __device__ inline bool slot_used(const FGeom& g, const int64_t* s_n, int64_t s) 
   return s < g.slot_cap && (s % g.slot_per) < s_n[s / g.slot_per];
 }
 
+// Roots, and every non-root slot's sums added into its root.  A component
+// spread over many tiles (a robot's star of long thin rays on a 1 cm map)
+// has thousands of slots: one global atomic each would queue them on the
+// same three addresses.  The sums are first combined per workgroup in an LDS
+// table keyed by root (64-bit LDS atomics), then flushed with one global
+// atomic per (workgroup, root, field); a root that finds no LDS entry within
+// kRootProbe probes goes straight to global memory.
+constexpr int kRootHash = 512;
+constexpr int kRootProbe = 8;
+
+__device__ inline void add_to_root(long long* slot_acc, int32_t r, const long long* v) {
+  for (int f = 0; f < 3; ++f)
+    atomicAdd((unsigned long long*)&slot_acc[3 * (int64_t)r + f], (unsigned long long)v[f]);
+}
+
 __global__ __launch_bounds__(256) void k_frontier_resolve(FGeom g, const int32_t* __restrict__ slot_parent,
                                                           int32_t* __restrict__ slot_root,
                                                           const long long* __restrict__ slot_own,
                                                           long long* slot_acc,
                                                           const unsigned long long* fsh) {
   __shared__ int64_t s_n[kShards];
-  load_shard_counts(g, fsh, s_n);
+  __shared__ int32_t hkey[kRootHash];
+  __shared__ unsigned long long hacc[3][kRootHash];
+  for (int e = threadIdx.x; e < kRootHash; e += blockDim.x) {
+    hkey[e] = -1;
+    hacc[0][e] = hacc[1][e] = hacc[2][e] = 0;
+  }
+  load_shard_counts(g, fsh, s_n);  // (its barrier also orders the table init)
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < g.slot_cap;
        s += (int64_t)gridDim.x * blockDim.x) {
     if (!slot_used(g, s_n, s)) continue;
     const int32_t r = dm_uf_root(slot_parent, (int32_t)s);
     slot_root[s] = r;
-    if (r != (int32_t)s) {
-      atomicAdd((unsigned long long*)&slot_acc[3 * (int64_t)r + 0], (unsigned long long)slot_own[3 * s + 0]);
-      atomicAdd((unsigned long long*)&slot_acc[3 * (int64_t)r + 1], (unsigned long long)slot_own[3 * s + 1]);
-      atomicAdd((unsigned long long*)&slot_acc[3 * (int64_t)r + 2], (unsigned long long)slot_own[3 * s + 2]);
+    if (r == (int32_t)s) continue;
+    const long long v[3] = {slot_own[3 * s + 0], slot_own[3 * s + 1], slot_own[3 * s + 2]};
+    uint32_t h = ((uint32_t)r * 2654435761u) >> 23;  // 9 bits
+    bool done = false;
+    for (int p = 0; p < kRootProbe && !done; ++p, h = (h + 1) & (kRootHash - 1)) {
+      const int32_t k = atomicCAS(&hkey[h], -1, r);
+      if (k == -1 || k == r) {
+        for (int f = 0; f < 3; ++f) atomicAdd(&hacc[f][h], (unsigned long long)v[f]);
+        done = true;
+      }
     }
+    if (!done) add_to_root(slot_acc, r, v);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < kRootHash; e += blockDim.x) {
+    const int32_t r = hkey[e];
+    if (r < 0) continue;
+    const long long v[3] = {(long long)hacc[0][e], (long long)hacc[1][e], (long long)hacc[2][e]};
+    add_to_root(slot_acc, r, v);
   }
 }
 
@@ -918,7 +953,8 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   DM_HIP(hipGetLastError());
   const int sgrid = grid_for(g->slot_cap, 256, 1024);
   dm_timer_begin(g, "frontier_resolve", &t);
-  hipLaunchKernelGGL(k_frontier_resolve, dim3(sgrid), dim3(256), 0, g->stream, fg,
+  // one workgroup per CU: fewer workgroups = fewer per-root flushes
+  hipLaunchKernelGGL(k_frontier_resolve, dim3(grid_for(g->slot_cap, 256, g->n_cu)), dim3(256), 0, g->stream, fg,
                      g->slot_parent, g->slot_root, g->slot_own, g->slot_acc, g->fsh);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
