@@ -742,6 +742,9 @@ int merge_readback(dm_grid* g, int slot, int64_t n, dm_cluster* out, int64_t cap
   // records into the slot's mapped readback buffer: no copy command
   const int64_t hint = std::min<int64_t>(g->h_out_cap, n);
   memcpy(g->h_mcnt, dm_rb_header(g->h_out), sizeof(unsigned long long) * 4);
+  // the band exports (dm_frontiers_export_device) never pass through
+  // dm_frontiers_readback: the largest band's K hints the next export's sort
+  g->sort_hint = (int64_t)g->h_mcnt[3];
   if (g->h_mcnt[1]) {
     if (n_out) *n_out = (int64_t)g->h_mcnt[3];
     return dm_set_error(DM_ERR_INCOMPLETE,
