@@ -56,10 +56,12 @@ def parse():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1")
     ap.add_argument("--device-override", type=int, default=None,
                     help="put every rank on this GPU (rehearsal with --backend gloo)")
-    ap.add_argument("--config", default="C3", choices=["C3", "C2", "C5"],
-                    help="C3 (default, the bench line): 16384² batches; C2: 4096² single-robot "
-                         "scan-by-scan replay; C5: 65536² @1cm beam-density sweep (single GPU)")
-    ap.add_argument("--scans", type=int, default=10000, help="C2: scans in the replay")
+    ap.add_argument("--config", default="C3", choices=["C3", "C1", "C2", "C5"],
+                    help="C3 (default, the bench line): 16384² batches; C1 / C2: 400² / 4096² "
+                         "single-robot scan-by-scan replay; C5: 65536² @1cm beam-density sweep "
+                         "(single GPU)")
+    ap.add_argument("--scans", type=int, default=None,
+                    help="C1 / C2: scans in the replay (default 1000 / 10000)")
     ap.add_argument("--sweep", default="12,48,192,768,4096", help="C5: beams per scan")
     return ap.parse_args()
 
@@ -449,8 +451,8 @@ def run_config(args):
     mapper = dm.OccupancyMapper(params, device=dev_i)
     mapper.set_overlap(True)
     try:
-        if args.config == "C2":
-            out = _run_c2(args, np, torch, synth, mapper, params, amin, dev)
+        if args.config in ("C1", "C2"):
+            out = _run_replay(args, np, torch, synth, mapper, params, amin, dev)
         else:
             out = _run_c5(args, np, torch, synth, mapper, params, amin, dev, world)
     finally:
@@ -460,12 +462,16 @@ def run_config(args):
     return out
 
 
-def _run_c2(args, np, torch, synth, m, params, amin, dev):
-    """C2: 4096² @5 cm, one robot, N=360, scan-by-scan replay (S=1): every
-    scan is integrated and followed by a full frontier extraction."""
-    N, n = 360, args.scans
+def _run_replay(args, np, torch, synth, m, params, amin, dev):
+    """C1 (400²) / C2 (4096²) @5 cm, one robot, N=360, scan-by-scan replay
+    (S=1): every scan is integrated and followed by a full frontier
+    extraction.  CPU baseline: C1 the NumPy restatement (the reference's
+    Python idiom, BASELINE config C1), C2 the C restatement."""
+    cfg = args.config
+    N = 360
+    n = args.scans if args.scans is not None else (1000 if cfg == "C1" else 10000)
     inc = float(synth.ld06_angle_increment(N))
-    world = synth.config_world("C2", args.seed)[0]
+    world, G = synth.config_world(cfg, args.seed)[:2]
     stream = synth.ScanStream(world, 1, N, args.seed * 1000 + 2)
     t_gen = time.perf_counter()
     batches = [stream.next_batch() for _ in range(n)]
@@ -513,31 +519,44 @@ def _run_c2(args, np, torch, synth, m, params, amin, dev):
     cpu = None
     if args.cpu_seconds > 0:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import oracle
+        if cfg == "C1":
+            import np_oracle
 
-        oracle.build()
-        om = oracle.OracleMap(params)
+            L = np.zeros((params.height, params.width), np.float32)
+            st = np.full((params.height, params.width), -1, np.int8)
+            integ = lambda k: np_oracle.integrate(params, L, st, poses[k:k + 1], ranges[k:k + 1],  # noqa: E731
+                                                  amin, inc)[0]
+            front = lambda: np_oracle.frontiers(params, st)  # noqa: E731
+            impl = "NumPy restatement (oracle/np_oracle.py)"
+        else:
+            import oracle
+
+            oracle.build()
+            om = oracle.OracleMap(params)
+            integ = lambda k: om.integrate(poses[k:k + 1], ranges[k:k + 1], amin, inc)[0]  # noqa: E731
+            front = lambda: om.frontiers(want_mask=False, want_labels=False)  # noqa: E731
+            impl = "C restatement (oracle/dm_oracle.c)"
         u_c, t_i, t_f, done = 0, 0.0, [], 0
         for k in range(n):
             a = time.perf_counter()
-            u_c += om.integrate(poses[k:k + 1], ranges[k:k + 1], amin, inc)[0]
+            u_c += integ(k)
             t_i += time.perf_counter() - a
             a = time.perf_counter()
-            om.frontiers(want_mask=False, want_labels=False)
+            front()
             t_f.append(time.perf_counter() - a)
             done += 1
             if t_i + sum(t_f) > args.cpu_seconds:
                 break
         cpu = {"value": u_c / t_i, "unit": "beam-cell updates/s", "cores": 1, "kind": "port",
-               "sample": f"first {done} scans of the replay, integrate + frontier pass per scan",
+               "sample": f"first {done} scans of the replay, integrate + frontier pass per scan, {impl}",
                "scans_per_s": done / (t_i + sum(t_f)), "frontier_ms": float(np.median(t_f)) * 1e3,
                "cpu": _cpu_model()}
     return {
         "value": U / elapsed, "steps": n, "warmup": min(args.warmup * 20, n),
         "ms_per_step": elapsed / n * 1e3, "scans_per_s": n / elapsed,
-        "config": {"workload": f"C2: 4096² grid @5cm, single robot, {n}-scan replay x {N} beams, "
+        "config": {"workload": f"{cfg}: {G}² grid @5cm, single robot, {n}-scan replay x {N} beams, "
                                "integrate + full frontier extraction per scan (S=1)",
-                   "grid": [4096, 4096], "resolution_m": 0.05, "scans_per_batch": 1,
+                   "grid": [G, G], "resolution_m": 0.05, "scans_per_batch": 1,
                    "beams_per_scan": N, "parallelism": "single GPU"},
         "updates_total": U, "touched_total": T,
         "integrate_ms": float(np.median(ti)) * 1e3, "frontier_ms": float(np.median(tf)) * 1e3,
