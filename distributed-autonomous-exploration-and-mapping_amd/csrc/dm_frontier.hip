@@ -677,41 +677,44 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
   const int64_t K = (int64_t)*count;
   if (blockIdx.x == 0) write_rb_header(K, cap, sorted, cnt, ncnt, sorted_idx, fsh, host_out);
   if (K > cap) return;
-  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
-  if ((int64_t)blockIdx.x * 64 >= K) return;  // whole workgroup: no barrier skipped
-  const long long key = i < K ? clusters[4 * i] : 0;
-  int32_t r = 0;
-  for (int64_t c0 = 0; c0 < K; c0 += kSortChunk) {
-    const int n = (int)min((int64_t)kSortChunk, K - c0);
-    __syncthreads();
-    {
-      long long v[kSortChunk / kSortThreads];
+  // grid-stride over groups of 64 records (the grid is sized from the
+  // expected count; the loop bound is uniform within a workgroup)
+  for (int64_t g0 = (int64_t)blockIdx.x * 64; g0 < K; g0 += (int64_t)gridDim.x * 64) {
+    const int64_t i = g0 + lane;
+    const long long key = i < K ? clusters[4 * i] : 0;
+    int32_t r = 0;
+    for (int64_t c0 = 0; c0 < K; c0 += kSortChunk) {
+      const int n = (int)min((int64_t)kSortChunk, K - c0);
+      __syncthreads();
+      {
+        long long v[kSortChunk / kSortThreads];
 #pragma unroll
-      for (int q = 0; q < kSortChunk / kSortThreads; ++q) {
-        const int e = tid + q * kSortThreads;
-        v[q] = e < n ? clusters[4 * (c0 + e)] : 0;
-      }
+        for (int q = 0; q < kSortChunk / kSortThreads; ++q) {
+          const int e = tid + q * kSortThreads;
+          v[q] = e < n ? clusters[4 * (c0 + e)] : 0;
+        }
 #pragma unroll
-      for (int q = 0; q < kSortChunk / kSortThreads; ++q) {
-        const int e = tid + q * kSortThreads;
-        if (e < n) keys[e] = v[q];
+        for (int q = 0; q < kSortChunk / kSortThreads; ++q) {
+          const int e = tid + q * kSortThreads;
+          if (e < n) keys[e] = v[q];
+        }
       }
+      __syncthreads();
+      const int per = (n + kSortWaves - 1) / kSortWaves;
+      const int lo = min(n, w * per), hi = min(n, lo + per);
+      int e = lo;
+      for (; e + 4 <= hi; e += 4)
+        r += (keys[e] < key) + (keys[e + 1] < key) + (keys[e + 2] < key) + (keys[e + 3] < key);
+      for (; e < hi; ++e) r += keys[e] < key;
     }
-    __syncthreads();
-    const int per = (n + kSortWaves - 1) / kSortWaves;
-    const int lo = min(n, w * per), hi = min(n, lo + per);
-    int e = lo;
-    for (; e + 4 <= hi; e += 4)
-      r += (keys[e] < key) + (keys[e + 1] < key) + (keys[e + 2] < key) + (keys[e + 3] < key);
-    for (; e < hi; ++e) r += keys[e] < key;
-  }
-  part[w][lane] = r;
-  __syncthreads();
-  if (w == 0 && i < K) {
-    int32_t rank = 0;
+    part[w][lane] = r;
+    __syncthreads();  // (the next group's first barrier keeps part until wave 0 read it)
+    if (w == 0 && i < K) {
+      int32_t rank = 0;
 #pragma unroll
-    for (int q = 0; q < kSortWaves; ++q) rank += part[q][lane];
-    put_sorted(ox, oy, res, clusters, i, rank, out, rank_of, host_out, host_cap);
+      for (int q = 0; q < kSortWaves; ++q) rank += part[q][lane];
+      put_sorted(ox, oy, res, clusters, i, rank, out, rank_of, host_out, host_cap);
+    }
   }
 }
 
@@ -873,9 +876,12 @@ int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const uns
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
                         int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
                         int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
-                        int64_t host_cap) {
+                        int64_t host_cap, int64_t expect) {
   const int64_t cap = std::min<int64_t>(max_records, kRankSortCap);
-  hipLaunchKernelGGL(k_rank_sort, dim3(grid_for(cap, 64, 1 << 20)), dim3(kSortThreads), 0, stream,
+  // one workgroup per 64 expected records (twice the last pass's count, at
+  // least 2048): a thousand idle 1024-thread workgroups cost microseconds
+  const int64_t want = std::max<int64_t>(2 * expect, 2048);
+  hipLaunchKernelGGL(k_rank_sort, dim3(grid_for(std::min(cap, want), 64, 1 << 20)), dim3(kSortThreads), 0, stream,
                      ox, oy, res, clusters, d_count, cap, out, rank_of, d_sorted, cnt, ncnt, sorted_idx,
                      fsh, host_out, host_cap);
   DM_HIP(hipGetLastError());
@@ -977,7 +983,7 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
                               g->h_out_dev, g->h_out_cap)
       : dm_launch_rank_sort(g->stream, g->clusters, g->cnt + CNT_CLUSTERS, g->slot_cap, g->p.origin_x,
                             g->p.origin_y, g->p.resolution, g->out_clu, g->rank_of, g->cnt + CNT_SORTED,
-                            g->cnt, CNT_N, CNT_SORTED, g->fsh, g->h_out_dev, g->h_out_cap);
+                            g->cnt, CNT_N, CNT_SORTED, g->fsh, g->h_out_dev, g->h_out_cap, g->sort_hint);
   dm_timer_end(g, &t);
   if (rc) return rc;
   return DM_OK;

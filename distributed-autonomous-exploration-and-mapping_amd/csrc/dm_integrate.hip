@@ -939,6 +939,15 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                      g->pieces, g->tile_count, g->tile_free, g->slabs, g->L, g->state, g->cnt, g->ish, vec_ok);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
+  // A beam meets a (convex) tile in one k-range of <= 64 steps, and chunks
+  // are >= 64 steps long, so a tile gets at most 1 piece per beam (2 when
+  // beams are chunked).  Calls that cannot reach kMedium pieces in any tile
+  // (one 360-beam scan: C1 / C2) have no heavy tile: no k_heavy_apply.
+  const int64_t max_tile_pieces = nb * (ge.chunks > 1 ? 2 : 1);
+  if (max_tile_pieces <= kMedium) {
+    if (g->overlap) g->tiles_mark_pending = true;
+    return DM_OK;
+  }
   dm_timer_begin(g, "heavy_apply", &t);
   hipLaunchKernelGGL(k_heavy_apply, dim3(grid_for(4 * g->heavy_cap, 1, 1024)), dim3(kQuarter), 0, g->stream, ge,
                      make_apply(g), g->heavy_list, g->tile_count, g->tile_free, g->slabs, g->L, g->state,

@@ -267,7 +267,7 @@ int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const uns
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
                         int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
                         int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
-                        int64_t host_cap);
+                        int64_t host_cap, int64_t expect);
 // Clusters above which the row-bucket sort replaces the O(K^2) rank sort.
 constexpr int64_t kBucketSortMin = 4096;
 constexpr int kBuckets = 4096;  // row buckets of the bucket sort (k_bs_scan: 4 per thread)

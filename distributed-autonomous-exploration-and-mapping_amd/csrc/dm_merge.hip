@@ -291,7 +291,7 @@ int dm_launch_merge(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t 
                               g->m_cnt, 4, M_SORTED, nullptr, g->h_out_dev, g->h_out_cap)
       : dm_launch_rank_sort(g->stream, g->m_clu, g->m_cnt + M_K, n, g->p.origin_x, g->p.origin_y,
                             g->p.resolution, g->m_out, nullptr, g->m_cnt + M_SORTED, g->m_cnt, 4,
-                            M_SORTED, nullptr, g->h_out_dev, g->h_out_cap);
+                            M_SORTED, nullptr, g->h_out_dev, g->h_out_cap, g->msort_hint);
   dm_timer_end(g, &t);
   return rc;
 }
