@@ -56,10 +56,11 @@ def parse():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1")
     ap.add_argument("--device-override", type=int, default=None,
                     help="put every rank on this GPU (rehearsal with --backend gloo)")
-    ap.add_argument("--config", default="C3", choices=["C3", "C1", "C2", "C5"],
+    ap.add_argument("--config", default="C3", choices=["C3", "C1", "C2", "C4", "C5"],
                     help="C3 (default, the bench line): 16384² batches; C1 / C2: 400² / 4096² "
-                         "single-robot scan-by-scan replay; C5: 65536² @1cm beam-density sweep "
-                         "(single GPU)")
+                         "single-robot scan-by-scan replay; C4: one 32768² map shared by 32 robots, "
+                         "row bands over the ranks (strong scaling); C5: 65536² @1cm "
+                         "beam-density sweep (single GPU)")
     ap.add_argument("--scans", type=int, default=None,
                     help="C1 / C2: scans in the replay (default 1000 / 10000)")
     ap.add_argument("--sweep", default="12,48,192,768,4096", help="C5: beams per scan")
@@ -68,8 +69,9 @@ def parse():
 
 def main():
     args = parse()
-    if args.config != "C3":
+    if args.config not in ("C3", "C4"):
         return run_config(args)
+    c4 = args.config == "C4"
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -93,12 +95,19 @@ def main():
     from dm import synth
     from dm.sharded import ShardedMapper
 
-    G, res = args.grid, 0.05
-    H_total = G * world_size
+    res = 0.05
+    if c4:  # BASELINE C4: one 32768² map, 32 robots anywhere in it, bands = ranks
+        G = H_total = 32768
+        args.robots = 32
+    else:   # C3 per GPU: a 16384-row band per rank (weak scaling)
+        G = args.grid
+        H_total = G * world_size
     half_w = G * res / 2.0
     oy_global = -H_total * res / 2.0
     # one world over the whole map (every rank builds the same one)
     world = synth.make_world(args.seed * 1000, -half_w, oy_global, half_w, -oy_global)
+    from dm.sharded import band_rows as _band_rows
+    b_row0, b_rows = _band_rows(H_total, world_size, rank) if world_size > 1 else (0, H_total)
 
     def band_stream(q):
         """Rank q's robots: random-walking anywhere in q's band."""
@@ -110,11 +119,17 @@ def main():
     # integrates its own robots' scans plus the neighbours' scans whose
     # max-range disk reaches its band (host-side replication of the scan
     # stream); libdm clips every ray to the band, so each
-    # cell update is counted by exactly one rank.
+    # cell update is counted by exactly one rank.  C4: every rank replays the
+    # same 32-robot stream and keeps the scans that reach its band.
     reach = 12.0 + 2 * res
-    ylo = oy_global + rank * G * res - reach
-    yhi = oy_global + (rank + 1) * G * res + reach
-    streams = {q: band_stream(q) for q in (rank - 1, rank, rank + 1) if 0 <= q < world_size}
+    ylo = oy_global + b_row0 * res - reach
+    yhi = oy_global + (b_row0 + b_rows) * res + reach
+    if c4:
+        streams = {-1: synth.ScanStream(world, args.robots, args.beams, args.seed * 1000 + 500,
+                                        region=(-half_w + 1.0, oy_global + 1.0, half_w - 1.0,
+                                                -oy_global - 1.0))}
+    else:
+        streams = {q: band_stream(q) for q in (rank - 1, rank, rank + 1) if 0 <= q < world_size}
     t_gen = time.perf_counter()
     pool = []
     for _ in range(args.pool):
@@ -258,7 +273,8 @@ def main():
             cpu = cpu_baseline(params, pool, amin, inc, args.cpu_seconds)
         fr_clusters = int(len(fr))
         result = {
-            "metric": "beam-cell updates/sec + frontier-extract ms on 16384² grid",
+            "metric": ("beam-cell updates/sec + frontier-extract ms (C4: 32768² shared map)" if c4
+                       else "beam-cell updates/sec + frontier-extract ms on 16384² grid"),
             "value": U_all / elapsed,
             "unit": "beam-cell updates/s",
             "n_gpus": world_size,
@@ -266,13 +282,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if c4 else "weak",
             "vs_baseline": None,
             "dtype": "int32/u32 ray math + fp32 log-odds (fp64 endpoints)",
             "data": "synthetic: seeded rectangle world, random-walk robots, LD06-format scans",
             "config": {
-                "workload": "C3: 16384² grid @5cm per GPU, 64-scan x 4096-beam batch "
-                            "integrate + full frontier extraction per step",
+                "workload": ("C4: one 32768² grid @5cm shared by 32 robots (32 x 4096-beam scans "
+                             "per step), row bands over the ranks, integrate + full frontier "
+                             "extraction per step" if c4 else
+                             "C3: 16384² grid @5cm per GPU, 64-scan x 4096-beam batch "
+                             "integrate + full frontier extraction per step"),
                 "grid": [G, H_total],
                 "resolution_m": res,
                 "scans_per_batch": S,
@@ -362,7 +381,8 @@ def cpu_baseline(params, pool, amin, inc, budget_s):
         "unit": "beam-cell updates/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"{done} batch(es) of 64x4096 beams into a fresh 16384² map + 1 frontier pass",
+        "sample": (f"{done} batch(es) of {pool[0][1].shape[0]}x{pool[0][1].shape[1]} beams into a fresh "
+                   f"{params.width}x{params.height} map + 1 frontier pass"),
         "frontier_ms": t_fr * 1e3,
         "cpu": _cpu_model(),
     }
