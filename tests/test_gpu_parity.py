@@ -333,3 +333,24 @@ def test_colocated_scans_heavy_slab_widths(oracle_lib, S):
         assert_map_equal(m, om)
         fr = m.frontiers(want_mask=True, want_labels=True)
         assert_frontiers_equal(fr, *om.frontiers())
+
+
+@pytest.mark.parametrize("S,N", [(1, 360), (1, 512), (1, 513), (2, 256), (1, 1100), (3, 400)])
+def test_heavy_apply_skip_boundary(oracle_lib, S, N):
+    """Co-located scans around the bound below which dm_launch_integrate
+    skips k_heavy_apply (a tile gets <= 1 piece per beam, <= 2 when beams are
+    chunked: no tile can exceed kMedium = 1024 pieces).  Above the bound the
+    sensor tile may be heavy and must be applied."""
+    p = cases.make_params(700, 600, resolution=0.02)
+    rng = np.random.Generator(np.random.PCG64(100 + N + S))
+    poses = np.tile(np.array([[0.011, 0.017, 0.2]]), (S, 1))
+    ranges = (np.round(rng.uniform(0.05, 6.0, (S, N)) * 1000) / 1000).astype(np.float32)
+    amin, inc = 0.0, float(np.float32(2 * np.pi / (N - 1)))
+    om = oracle_lib.OracleMap(p)
+    with dm.OccupancyMapper(p) as m:
+        for k in range(2):
+            assert m.integrate(poses, ranges, amin, inc) == om.integrate(poses, ranges, amin, inc)
+        if S * N > 1024:
+            assert m.last_stats()["heavy_tiles"] >= 1
+        assert_map_equal(m, om)
+        assert_frontiers_equal(m.frontiers(want_mask=True, want_labels=True), *om.frontiers())
