@@ -531,7 +531,11 @@ __global__ __launch_bounds__(256) void k_frontier_resolve(FGeom g, const int32_t
                                                           int32_t* __restrict__ slot_root,
                                                           const long long* __restrict__ slot_own,
                                                           long long* slot_acc,
-                                                          const unsigned long long* fsh) {
+                                                          const unsigned long long* fsh, int fuse,
+                                                          const long long* __restrict__ slot_label,
+                                                          long long* __restrict__ clusters,
+                                                          int32_t* __restrict__ slot_k,
+                                                          unsigned long long* cnt) {
   __shared__ int64_t s_n[kShards];
   __shared__ int32_t hkey[kRootHash];
   __shared__ unsigned long long hacc[3][kRootHash];
@@ -540,12 +544,35 @@ __global__ __launch_bounds__(256) void k_frontier_resolve(FGeom g, const int32_t
     hacc[0][e] = hacc[1][e] = hacc[2][e] = 0;
   }
   load_shard_counts(g, fsh, s_n);  // (its barrier also orders the table init)
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < g.slot_cap;
-       s += (int64_t)gridDim.x * blockDim.x) {
-    if (!slot_used(g, s_n, s)) continue;
-    const int32_t r = dm_uf_root(slot_parent, (int32_t)s);
-    slot_root[s] = r;
-    if (r == (int32_t)s) continue;
+  const int lane = __lane_id();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  // wave-aligned (the fused compaction below allocates per wave)
+  for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); s0 < g.slot_cap; s0 += stride) {
+    const int64_t s = s0 + lane;
+    const bool used = slot_used(g, s_n, s);
+    const int32_t r = used ? dm_uf_root(slot_parent, (int32_t)s) : -1;
+    if (used) slot_root[s] = r;
+    if (fuse) {
+      // min_size <= 1: every root is a cluster, so k_frontier_compact's
+      // work happens here; its sums are not final yet (other workgroups
+      // still add into the root), so the record holds -(slot + 1) and the
+      // sort kernel reads the sums (put_sorted)
+      const bool root = used && r == (int32_t)s;
+      const unsigned long long bal = __ballot(root);
+      if (bal) {
+        const int lead = __ffsll(bal) - 1;
+        unsigned long long k0 = 0;
+        if (lane == lead) k0 = atomicAdd(&cnt[CNT_CLUSTERS], (unsigned long long)__popcll(bal));
+        k0 = __shfl(k0, lead);
+        const unsigned long long k = k0 + __popcll(bal & ((1ull << lane) - 1));
+        if (root && (int64_t)k < g.clu_cap) {
+          slot_k[s] = (int32_t)k;
+          clusters[4 * k + 0] = slot_label[s];
+          clusters[4 * k + 1] = -(long long)s - 1;
+        }
+      }
+    }
+    if (!used || r == (int32_t)s) continue;
     const long long v[3] = {slot_own[3 * s + 0], slot_own[3 * s + 1], slot_own[3 * s + 2]};
     uint32_t h = ((uint32_t)r * 2654435761u) >> 23;  // 9 bits
     bool done = false;
@@ -621,18 +648,50 @@ __device__ inline void write_rb_header(int64_t K, int64_t cap, unsigned long lon
   }
 }
 
+// A record written by the fused compaction (k_frontier_resolve, min_size
+// <= 1) holds -(slot + 1) instead of its sums: read them from slot_acc
+// (final after resolve) and write them into the raw record too (the host
+// sort fallback reads raw records).  One writer per record.
+__device__ inline void record_sums(long long* clusters, const long long* sums, int64_t i, long long* sz,
+                                   long long* sx, long long* sy) {
+  *sz = clusters[4 * i + 1];
+  if (sums && *sz < 0) {
+    const int64_t sl = -*sz - 1;
+    *sz = sums[3 * sl];
+    *sx = sums[3 * sl + 1];
+    *sy = sums[3 * sl + 2];
+    clusters[4 * i + 1] = *sz;
+    clusters[4 * i + 2] = *sx;
+    clusters[4 * i + 3] = *sy;
+  } else {
+    *sx = clusters[4 * i + 2];
+    *sy = clusters[4 * i + 3];
+  }
+}
+
+// Raw records of a pass the device does not sort (K > cap): sums in place.
+__device__ inline void fix_raw_records(long long* clusters, const long long* sums, int64_t K) {
+  if (!sums) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < K; i += (int64_t)gridDim.x * blockDim.x) {
+    long long sz, sx, sy;
+    record_sums(clusters, sums, i, &sz, &sx, &sy);
+  }
+}
+
 // Raw record i ([4] int64 label, size, sum_x, sum_y) -> dm_cluster at its
 // sorted position, centroid cx_m = ox + ((double)sum_x / (double)size + 0.5)
 // * res (SPEC a10: one IEEE division, then add; no FMA contraction).
-__device__ inline void put_sorted(double ox, double oy, double res, const long long* __restrict__ clusters,
+__device__ inline void put_sorted(double ox, double oy, double res, long long* clusters, const long long* sums,
                                   int64_t i, int64_t rank, dm_cluster* __restrict__ out,
                                   int32_t* __restrict__ rank_of, dm_cluster* __restrict__ host_out,
                                   int64_t host_cap) {
   dm_cluster c;
   c.label = clusters[4 * i];
-  c.size = clusters[4 * i + 1];
-  c.sum_x = clusters[4 * i + 2];
-  c.sum_y = clusters[4 * i + 3];
+  long long sz, sx, sy;
+  record_sums(clusters, sums, i, &sz, &sx, &sy);
+  c.size = sz;
+  c.sum_x = sx;
+  c.sum_y = sy;
   const double mx = (double)c.sum_x / (double)c.size;
   const double my = (double)c.sum_y / (double)c.size;
   c.cx_m = ox + (mx + 0.5) * res;
@@ -661,7 +720,7 @@ constexpr int kSortWaves = kSortThreads / 64;
 constexpr int64_t kRankSortCap = 1 << 16;
 
 __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy, double res,
-                                                            const long long* __restrict__ clusters,
+                                                            long long* clusters, const long long* sums,
                                                             const unsigned long long* __restrict__ count,
                                                             int64_t cap, dm_cluster* __restrict__ out,
                                                             int32_t* __restrict__ rank_of,
@@ -676,7 +735,10 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
   const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
   const int64_t K = (int64_t)*count;
   if (blockIdx.x == 0) write_rb_header(K, cap, sorted, cnt, ncnt, sorted_idx, fsh, host_out);
-  if (K > cap) return;
+  if (K > cap) {
+    fix_raw_records(clusters, sums, K);
+    return;
+  }
   // grid-stride over groups of 64 records (the grid is sized from the
   // expected count; the loop bound is uniform within a workgroup)
   for (int64_t g0 = (int64_t)blockIdx.x * 64; g0 < K; g0 += (int64_t)gridDim.x * 64) {
@@ -713,7 +775,7 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
       int32_t rank = 0;
 #pragma unroll
       for (int q = 0; q < kSortWaves; ++q) rank += part[q][lane];
-      put_sorted(ox, oy, res, clusters, i, rank, out, rank_of, host_out, host_cap);
+      put_sorted(ox, oy, res, clusters, sums, i, rank, out, rank_of, host_out, host_cap);
     }
   }
 }
@@ -797,7 +859,7 @@ __global__ __launch_bounds__(256) void k_bs_place(const long long* __restrict__ 
 }
 
 __global__ __launch_bounds__(256) void k_bs_rank(double ox, double oy, double res,
-                                                 const long long* __restrict__ clusters,
+                                                 long long* clusters, const long long* sums,
                                                  const unsigned long long* __restrict__ count, int64_t cap,
                                                  long long base, int shift,
                                                  const int32_t* __restrict__ roff,
@@ -809,14 +871,17 @@ __global__ __launch_bounds__(256) void k_bs_rank(double ox, double oy, double re
                                                  dm_cluster* __restrict__ host_out, int64_t host_cap) {
   const int64_t K = (int64_t)*count;
   if (blockIdx.x == 0) write_rb_header(K, cap, sorted, cnt, ncnt, sorted_idx, fsh, host_out);
-  if (K > cap) return;
+  if (K > cap) {
+    fix_raw_records(clusters, sums, K);
+    return;
+  }
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < K; p += (int64_t)gridDim.x * blockDim.x) {
     const long long key = bkey[p];
     const int64_t b = (key - base) >> shift;
     const int32_t lo = roff[b], hi = roff[b + 1];
     int64_t rank = lo;
     for (int32_t j = lo; j < hi; ++j) rank += bkey[j] < key;
-    put_sorted(ox, oy, res, clusters, bidx[p], rank, out, rank_of, host_out, host_cap);
+    put_sorted(ox, oy, res, clusters, sums, bidx[p], rank, out, rank_of, host_out, host_cap);
   }
 }
 
@@ -872,7 +937,8 @@ int dm_launch_edge_labels(dm_grid* g) {
   return DM_OK;
 }
 
-int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const unsigned long long* d_count,
+int dm_launch_rank_sort(hipStream_t stream, long long* clusters, const long long* sums,
+                        const unsigned long long* d_count,
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
                         int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
                         int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
@@ -882,13 +948,14 @@ int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const uns
   // least 2048): a thousand idle 1024-thread workgroups cost microseconds
   const int64_t want = std::max<int64_t>(2 * expect, 2048);
   hipLaunchKernelGGL(k_rank_sort, dim3(grid_for(std::min(cap, want), 64, 1 << 20)), dim3(kSortThreads), 0, stream,
-                     ox, oy, res, clusters, d_count, cap, out, rank_of, d_sorted, cnt, ncnt, sorted_idx,
+                     ox, oy, res, clusters, sums, d_count, cap, out, rank_of, d_sorted, cnt, ncnt, sorted_idx,
                      fsh, host_out, host_cap);
   DM_HIP(hipGetLastError());
   return DM_OK;
 }
 
-int dm_launch_bucket_sort(dm_grid* g, const long long* clusters, const unsigned long long* d_count,
+int dm_launch_bucket_sort(dm_grid* g, long long* clusters, const long long* sums,
+                          const unsigned long long* d_count,
                           int64_t max_records, int64_t row_base, int64_t rows, dm_cluster* out,
                           int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
                           int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
@@ -916,7 +983,7 @@ int dm_launch_bucket_sort(dm_grid* g, const long long* clusters, const unsigned 
                      shift, rcur, g->bs_key, g->bs_idx);
   DM_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_bs_rank, dim3(eg), dim3(256), 0, g->stream, g->p.origin_x, g->p.origin_y,
-                     g->p.resolution, clusters, d_count, max_records, base, shift, roff, g->bs_key,
+                     g->p.resolution, clusters, sums, d_count, max_records, base, shift, roff, g->bs_key,
                      g->bs_idx, out, rank_of, d_sorted, cnt, ncnt, sorted_idx, fsh, host_out, host_cap);
   DM_HIP(hipGetLastError());
   return DM_OK;
@@ -959,16 +1026,22 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   DM_HIP(hipGetLastError());
   const int sgrid = grid_for(g->slot_cap, 256, 1024);
   dm_timer_begin(g, "frontier_resolve", &t);
+  // min_size <= 1: every root is a cluster, compacted by the resolve itself
+  // (no k_frontier_compact); the sort reads the sums by slot
+  const int fuse = g->p.min_frontier_size <= 1 ? 1 : 0;
   // one workgroup per CU: fewer workgroups = fewer per-root flushes
   hipLaunchKernelGGL(k_frontier_resolve, dim3(grid_for(g->slot_cap, 256, g->n_cu)), dim3(256), 0, g->stream, fg,
-                     g->slot_parent, g->slot_root, g->slot_own, g->slot_acc, g->fsh);
+                     g->slot_parent, g->slot_root, g->slot_own, g->slot_acc, g->fsh, fuse, g->slot_label,
+                     g->clusters, g->slot_k, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
-  dm_timer_begin(g, "frontier_compact", &t);
-  hipLaunchKernelGGL(k_frontier_compact, dim3(sgrid), dim3(256), 0, g->stream, fg,
-                     g->slot_root, g->slot_label, g->slot_acc, g->clusters, g->slot_k, g->cnt, g->fsh);
-  dm_timer_end(g, &t);
-  DM_HIP(hipGetLastError());
+  if (!fuse) {
+    dm_timer_begin(g, "frontier_compact", &t);
+    hipLaunchKernelGGL(k_frontier_compact, dim3(sgrid), dim3(256), 0, g->stream, fg,
+                       g->slot_root, g->slot_label, g->slot_acc, g->clusters, g->slot_k, g->cnt, g->fsh);
+    dm_timer_end(g, &t);
+    DM_HIP(hipGetLastError());
+  }
   if (want_labels) {
     hipLaunchKernelGGL(k_slot_labels, dim3(grid_for(cells, 256, 8192)), dim3(256), 0, g->stream,
                        cells, g->slot_cap, g->cell_slot, g->slot_root, g->slot_label, g->labels);
@@ -978,10 +1051,10 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   // the last collected pass predicts this one's cluster count (either sort
   // is exact for any count; only their speed differs)
   const int rc = g->sort_hint > kBucketSortMin
-      ? dm_launch_bucket_sort(g, g->clusters, g->cnt + CNT_CLUSTERS, g->slot_cap, g->row0, g->R, g->out_clu,
+      ? dm_launch_bucket_sort(g, g->clusters, fuse ? g->slot_acc : nullptr, g->cnt + CNT_CLUSTERS, g->slot_cap, g->row0, g->R, g->out_clu,
                               g->rank_of, g->cnt + CNT_SORTED, g->cnt, CNT_N, CNT_SORTED, g->fsh,
                               g->h_out_dev, g->h_out_cap)
-      : dm_launch_rank_sort(g->stream, g->clusters, g->cnt + CNT_CLUSTERS, g->slot_cap, g->p.origin_x,
+      : dm_launch_rank_sort(g->stream, g->clusters, fuse ? g->slot_acc : nullptr, g->cnt + CNT_CLUSTERS, g->slot_cap, g->p.origin_x,
                             g->p.origin_y, g->p.resolution, g->out_clu, g->rank_of, g->cnt + CNT_SORTED,
                             g->cnt, CNT_N, CNT_SORTED, g->fsh, g->h_out_dev, g->h_out_cap, g->sort_hint);
   dm_timer_end(g, &t);

@@ -263,7 +263,10 @@ int dm_launch_edge_labels(dm_grid* g);
 int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied);
 int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters,
                         int64_t* copied);
-int dm_launch_rank_sort(hipStream_t stream, const long long* clusters, const unsigned long long* d_count,
+// sums: slot sums (slot_acc) when the records were written by the fused
+// compaction (-(slot + 1) in place of the size), else nullptr.
+int dm_launch_rank_sort(hipStream_t stream, long long* clusters, const long long* sums,
+                        const unsigned long long* d_count,
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
                         int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
                         int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
@@ -274,7 +277,8 @@ constexpr int kBuckets = 4096;  // row buckets of the bucket sort (k_bs_scan: 4 
 int dm_grow_bucket_sort(dm_grid* g, int64_t n);
 // Row-bucket sort of the raw records (labels of rows [row_base, row_base +
 // rows)): same outputs, readback header and flags as dm_launch_rank_sort.
-int dm_launch_bucket_sort(dm_grid* g, const long long* clusters, const unsigned long long* d_count,
+int dm_launch_bucket_sort(dm_grid* g, long long* clusters, const long long* sums,
+                          const unsigned long long* d_count,
                           int64_t max_records, int64_t row_base, int64_t rows, dm_cluster* out,
                           int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
                           int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
