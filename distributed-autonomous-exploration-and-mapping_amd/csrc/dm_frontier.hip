@@ -66,16 +66,26 @@ __global__ __launch_bounds__(256) void k_frontier_prep(int64_t NT, const int32_t
   if (i0 == 0) *other_n = 0ull;
   if (i0 < kShards * kShardWords) fsh[i0] = 0ull;
   for (int64_t i = i0; i < n_edge; i += stride) edge_slot[i] = -1;
-  for (int64_t t0 = i0 - lane; t0 < NT; t0 += stride) {  // whole waves: ballot compaction
-    const int64_t t = t0 + lane;
+  // ballot compaction, one list_n atomic per workgroup and round (the
+  // loop bound is uniform within the workgroup: its barriers are safe)
+  __shared__ int32_t s_wn[4];
+  __shared__ unsigned long long s_base;
+  const int w = threadIdx.x >> 6;
+  for (int64_t b0 = (int64_t)blockIdx.x * blockDim.x; b0 < NT; b0 += stride) {
+    const int64_t t = b0 + threadIdx.x;
     const bool f = t < NT && tile_free[t] > 0;
     const unsigned long long bal = __ballot(f);
-    if (!bal) continue;
-    const int first = __ffsll(bal) - 1;
-    unsigned long long base = 0;
-    if (lane == first) base = atomicAdd(list_n, (unsigned long long)__popcll(bal));
-    base = __shfl(base, first);
-    if (f) ftiles[base + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)t;
+    if (lane == 0) s_wn[w] = __popcll(bal);
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int q = 0; q < 4; ++q) {
+      before += q < w ? s_wn[q] : 0;
+      total += s_wn[q];
+    }
+    if (threadIdx.x == 0 && total) s_base = atomicAdd(list_n, (unsigned long long)total);
+    __syncthreads();
+    if (f) ftiles[s_base + before + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)t;
+    __syncthreads();  // s_wn / s_base are rewritten next round
   }
 }
 
