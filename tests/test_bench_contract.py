@@ -1,0 +1,64 @@
+"""CPU: the committed bench lines (profiles/) keep the bench.py contract
+(DESIGN.md §5): metric / value / unit / steps fields, a roofline object whose
+frac is achieved / peak, a cpu_baseline object, and the configs named by
+BASELINE.json.  Also checks that bench.py's option parser knows every config
+without touching a GPU."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROFILES = os.path.join(REPO, "profiles")
+
+LINES = {
+    "r01_s4_bench.json": "C3",
+    "r01_c1_replay_bench.json": "C1",
+    "r01_c2_replay_bench.json": "C2",
+    "r01_c4_1gpu_bench.json": "C4",
+    "r01_c5_sweep_bench.json": "C5",
+}
+
+
+def _load(name):
+    path = os.path.join(PROFILES, name)
+    if not os.path.exists(path):
+        pytest.skip(f"{name} not committed")
+    with open(path) as f:
+        return json.loads(f.readline())
+
+
+@pytest.mark.parametrize("name,cfg", sorted(LINES.items()))
+def test_bench_line_fields(name, cfg):
+    d = _load(name)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in d, k
+    assert d["unit"] == "beam-cell updates/s" and d["higher_is_better"] is True
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    assert d["config"]["workload"].startswith(cfg)
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
+    cpu = d.get("cpu_baseline")
+    if cpu is not None:
+        assert cpu["kind"] in ("port", "reference") and cpu["cores"] >= 1 and cpu["sample"]
+
+
+def test_headline_line_has_traffic_and_cpu_baseline():
+    d = _load("r01_s4_bench.json")
+    assert d["n_gpus"] == 1 and d["scaling"] == "weak"
+    assert d["roofline"]["traffic"] and d["roofline"]["traffic"] > 0
+    assert d["cpu_baseline"] and d["cpu_baseline"]["value"] > 0
+    # the north-star targets (BASELINE.json): >= 1e10 updates/s, < 2 ms frontiers
+    assert d["value"] >= 1e10 and d["frontier_ms"] < 2.0
+
+
+def test_bench_parser_knows_every_config():
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--help"],
+                         capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    for cfg in ("C1", "C2", "C3", "C4", "C5"):
+        assert cfg in out.stdout
