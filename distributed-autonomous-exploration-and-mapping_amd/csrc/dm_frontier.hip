@@ -33,6 +33,12 @@ DM_PH_DECL(frontier)
 namespace {
 
 constexpr int kFT = 256;              // threads per frontier workgroup
+// waves per SIMD for k_frontier_tile: 7 workgroups per CU (LDS 22.6 KB each,
+// <= 72 VGPRs), so a C3 pass's ~3.3k listed tiles run in two rounds of the
+// chip's 1792 slots instead of three of 1280
+#ifndef DM_FT_OCC
+#define DM_FT_OCC 7
+#endif
 constexpr int kMaxRoots = 1024;       // 8-connected components in a 64x64 tile
 
 struct FGeom {
@@ -128,10 +134,25 @@ __device__ inline uint64_t upto_mask(int p) {  // bits 0..p inclusive
   return p >= 63 ? ~0ull : ((2ull << p) - 1ull);
 }
 
+// First cells of the runs of a 64-bit frontier row.
+__device__ inline uint64_t run_starts(uint64_t F) { return F & ~(F << 1); }
+
+// Last column of the run of row F that starts at column s0.
+__device__ inline int run_end(uint64_t F, int s0) {
+  const uint64_t rest = ~(F >> s0);
+  return rest ? s0 + __ffsll((unsigned long long)rest) - 2 : 63;
+}
+
 // Run id of frontier bit p of tile row y (p must be set): runs are numbered
 // in row-major order of their first cell.
-__device__ inline int run_of(const int32_t* rbase, const uint64_t* starts, int y, int p) {
-  return rbase[y] + __popcll(starts[y] & upto_mask(p)) - 1;
+__device__ inline int run_of(const int32_t* rbase, const uint64_t* rowF, int y, int p) {
+  return rbase[y] + __popcll(run_starts(rowF[y]) & upto_mask(p)) - 1;
+}
+
+// Component id of root run r: the number of root runs before it (root bits
+// in s_root, one 64-bit word per 64 runs, exclusive word prefix in pre).
+__device__ inline int root_rank(const uint64_t* s_root, const int32_t* pre, int r) {
+  return pre[r >> 6] + __popcll(s_root[r >> 6] & ((1ull << (r & 63)) - 1ull));
 }
 
 // State byte of one halo cell (global column x, band-local row y), or
@@ -188,7 +209,7 @@ __device__ inline void tile_issue(const FGeom& g, const int8_t* __restrict__ sta
 //     first run, whose first cell is the component's min linear index);
 //  4. per-component sums from run lengths, one slot per component, border
 //     slot ids for k_frontier_merge.
-__global__ __launch_bounds__(kFT, 5) void k_frontier_tile(
+__global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile(
     FGeom g, const int8_t* __restrict__ state, const int8_t* __restrict__ halo,
     const int32_t* __restrict__ ftiles, const unsigned long long* __restrict__ list_n,
     int32_t* __restrict__ border,
@@ -199,14 +220,12 @@ __global__ __launch_bounds__(kFT, 5) void k_frontier_tile(
   __shared__ uint64_t s_unk[DM_TS + 2];    // row y at index y+1, bit c = column c
   __shared__ uint8_t s_unkL[DM_TS + 2];    // column -1
   __shared__ uint8_t s_unkR[DM_TS + 2];    // column 64
-  __shared__ uint64_t s_free[DM_TS];
-  __shared__ uint64_t s_F[DM_TS];
-  __shared__ uint64_t s_start[DM_TS];
+  __shared__ uint64_t s_F[DM_TS];          // free bits (step 1), then frontier bits (step 2)
   __shared__ int32_t s_rbase[DM_TS + 1];
   __shared__ int32_t r_par[kMaxRuns];
-  __shared__ uint8_t r_s[kMaxRuns], r_e[kMaxRuns], r_y[kMaxRuns];
-  __shared__ int16_t r_rid[kMaxRuns];
-  __shared__ int16_t c_run[kMaxRoots];
+  __shared__ uint8_t r_s[kMaxRuns], r_y[kMaxRuns];  // run end: run_end(s_F[y], s)
+  __shared__ uint64_t s_root[kMaxRuns / 64];        // root-run bits
+  __shared__ int32_t s_rootpre[kMaxRuns / 64];
   // per-component size << 18 | sum of x (size <= 4096 < 2^13, sum of x <=
   // 4096 * 63 < 2^18: one 32-bit LDS add per run for both) and sum of y
   __shared__ uint32_t szx[kMaxRoots], ssy[kMaxRoots];
@@ -256,7 +275,7 @@ __global__ __launch_bounds__(kFT, 5) void k_frontier_tile(
         }
       }
       reinterpret_cast<uint16_t*>(&s_unk[y + 1])[q] = (uint16_t)unk;
-      reinterpret_cast<uint16_t*>(&s_free[y])[q] = (uint16_t)fre;
+      reinterpret_cast<uint16_t*>(&s_F[y])[q] = (uint16_t)fre;
       // halo (loaded with the interior, a tile ahead): waves 0/1 the row
       // above / below (one ballot each), threads 128..255 the columns left /
       // right, threads 0..3 the four corners
@@ -287,10 +306,9 @@ __global__ __launch_bounds__(kFT, 5) void k_frontier_tile(
         const uint64_t ui = s_unk[y + d];
         D |= ui | (ui << 1) | (uint64_t)s_unkL[y + d] | (ui >> 1) | ((uint64_t)s_unkR[y + d] << 63);
       }
-      const uint64_t F = s_free[y] & D;
-      const uint64_t st = F & ~(F << 1);
+      const uint64_t F = s_F[y] & D;  // only this thread reads row y's free bits
+      const uint64_t st = run_starts(F);
       s_F[y] = F;
-      s_start[y] = st;
       any = F != 0ull;
       // exclusive scan of run counts over the 64 rows (wave 0)
       const int c = __popcll(st);
@@ -312,22 +330,18 @@ __global__ __launch_bounds__(kFT, 5) void k_frontier_tile(
     }
     if (tid < DM_TS) {  // enumerate runs of row tid
       const int y = tid;
-      uint64_t st = s_start[y];
       const uint64_t F = s_F[y];
+      uint64_t st = run_starts(F);
       int r = s_rbase[y];
       while (st) {
         const int s0 = __ffsll((unsigned long long)st) - 1;
-        const uint64_t rest = ~(F >> s0);
-        const int len = rest ? __ffsll((unsigned long long)rest) - 1 : 64 - s0;
         r_s[r] = (uint8_t)s0;
-        r_e[r] = (uint8_t)(s0 + len - 1);
         r_y[r] = (uint8_t)y;
         r_par[r] = r;
         ++r;
         st &= st - 1;
       }
     }
-    if (tid == 0) nroots = 0;
     for (int r = tid; r < kMaxRoots; r += kFT) { szx[r] = 0; ssy[r] = 0; }
     __syncthreads();
     const int nruns = s_rbase[DM_TS];
@@ -338,13 +352,14 @@ __global__ __launch_bounds__(kFT, 5) void k_frontier_tile(
     for (int r = tid; r < nruns; r += kFT) {
       const int y = r_y[r];
       if (y == 0) continue;
-      const int lo = r_s[r] > 0 ? r_s[r] - 1 : 0;
-      const int hi = r_e[r] < 63 ? r_e[r] + 1 : 63;
+      const int s0 = r_s[r], e0 = run_end(s_F[y], s0);
+      const int lo = s0 > 0 ? s0 - 1 : 0;
+      const int hi = e0 < 63 ? e0 + 1 : 63;
       const uint64_t M = upto_mask(hi) & ~(lo > 0 ? upto_mask(lo - 1) : 0ull);
       uint64_t P = s_F[y - 1] & M;
       while (P) {
         const int p = __ffsll((unsigned long long)P) - 1;
-        lds_unite(r_par, r, run_of(s_rbase, s_start, y - 1, p));
+        lds_unite(r_par, r, run_of(s_rbase, s_F, y - 1, p));
         // skip the rest of that run inside M
         const uint64_t rest = ~(s_F[y - 1] >> p);
         const int len = rest ? __ffsll((unsigned long long)rest) - 1 : 64 - p;
@@ -355,7 +370,8 @@ __global__ __launch_bounds__(kFT, 5) void k_frontier_tile(
     DM_PH(dm_phase_acc_frontier, 3);
     // compress: every run points at its root.  The finds here only read
     // (no halving), so the only stores are final roots: a find passing
-    // through a run already compressed just takes the shortcut.
+    // through a run already compressed just takes the shortcut.  Lane l of
+    // a wave holds run 64 * word + l, so one ballot is the word of root bits.
     for (int r = tid; r < nruns; r += kFT) {
       int32_t x = r, p = r_par[r];
       while (p != x) {
@@ -363,16 +379,23 @@ __global__ __launch_bounds__(kFT, 5) void k_frontier_tile(
         p = ((volatile int32_t*)r_par)[x];
       }
       r_par[r] = x;
+      const uint64_t rb = __ballot(x == r);
+      if (lane == 0) s_root[r >> 6] = rb;
     }
     __syncthreads();
     DM_PH(dm_phase_acc_frontier, 4);
     // ---- 4. components, sums, slots ------------------------------------------
-    for (int r = tid; r < nruns; r += kFT) {
-      if (r_par[r] == r) {
-        const int c = atomicAdd(&nroots, 1);
-        r_rid[r] = (int16_t)c;
-        c_run[c] = (int16_t)r;
+    // component id = rank of its root run (row-major order of first cells)
+    if (tid < 64) {
+      const int nw = (nruns + 63) >> 6;
+      const int c = tid < nw ? __popcll(s_root[tid]) : 0;
+      int incl = c;
+      for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
       }
+      if (tid < nw) s_rootpre[tid] = incl - c;
+      if (tid == 63) nroots = incl;
     }
     __syncthreads();
     DM_PH(dm_phase_acc_frontier, 5);
@@ -381,20 +404,21 @@ __global__ __launch_bounds__(kFT, 5) void k_frontier_tile(
       sbase = (long long)atomicAdd(&fsh[(blockIdx.x % kShards) * kShardWords + SH_SLOT],
                                    (unsigned long long)nroots);
     for (int r = tid; r < nruns; r += kFT) {
-      const int c = r_rid[r_par[r]];
-      const uint32_t s0 = r_s[r], e0 = r_e[r], len = e0 - s0 + 1;
+      const int c = root_rank(s_root, s_rootpre, r_par[r]);
+      const int y = r_y[r];
+      const uint32_t s0 = r_s[r], e0 = (uint32_t)run_end(s_F[y], (int)s0), len = e0 - s0 + 1;
       atomicAdd(&szx[c], (len << 18) + (s0 + e0) * len / 2);
-      atomicAdd(&ssy[c], (uint32_t)r_y[r] * len);
+      atomicAdd(&ssy[c], (uint32_t)y * len);
     }
     __syncthreads();
     DM_PH(dm_phase_acc_frontier, 6);
     const long long base = sbase;
     const long long sh0 = (long long)(blockIdx.x % kShards) * g.slot_per;
-    const int nr = nroots;
-    for (int c = tid; c < nr; c += kFT) {
+    for (int r = tid; r < nruns; r += kFT) {
+      if (r_par[r] != r) continue;
+      const int c = root_rank(s_root, s_rootpre, r);
       if (base + c >= g.slot_per) { atomicOr(&cnt[CNT_OVERFLOW], 4ull); continue; }
       const long long slot = sh0 + base + c;
-      const int r = c_run[c];
       const long long gy = (long long)g.row0 + ty0 + r_y[r];
       const long long gx = (long long)tx0 + r_s[r];
       const uint32_t zx = szx[c];
@@ -413,7 +437,7 @@ __global__ __launch_bounds__(kFT, 5) void k_frontier_tile(
       const int x = side == 0 || side == 1 ? pos : side == 2 ? 0 : 63;
       long long sl = -1;
       if ((s_F[y] >> x) & 1ull) {
-        sl = base + r_rid[r_par[run_of(s_rbase, s_start, y, x)]];
+        sl = base + root_rank(s_root, s_rootpre, r_par[run_of(s_rbase, s_F, y, x)]);
         sl = sl < g.slot_per ? sh0 + sl : -1;
       }
       border[j * 256 + tid] = (int32_t)sl;
@@ -430,7 +454,7 @@ __global__ __launch_bounds__(kFT, 5) void k_frontier_tile(
         const bool f = (s_F[y] >> x) & 1ull;
         long long sl = -1;
         if (f) {
-          sl = base + r_rid[r_par[run_of(s_rbase, s_start, y, x)]];
+          sl = base + root_rank(s_root, s_rootpre, r_par[run_of(s_rbase, s_F, y, x)]);
           sl = sl < g.slot_per ? sh0 + sl : -1;
         }
         const int64_t gi = (int64_t)gy * g.W + gx;
