@@ -556,11 +556,15 @@ __device__ inline void finish_tile(const Geom& g, int32_t tile, int32_t T, int32
 // The next item's pieces are loaded right after this item's apply, its
 // cells (unconditional loads: a fixed count, so the walk waits for the pieces
 // alone with vmcnt(N)) at the top of its iteration, in flight during its
-// walk.  The per-item statistics stay in thread 0's registers (one flush per
+// walk.  7 workgroups per CU (72 VGPRs, no spills): C3's ~3.8k items in ~2
+// rounds of the chip's slots (41 us vs 43.5 us at 6).  The per-item statistics stay in thread 0's registers (one flush per
 // workgroup) and a light tile's free count is a plain read-modify-write (one
 // workgroup owns the tile), so no memory-side atomic sits in front of the
 // next item's loads in the wave's in-order vmcnt queue.
-constexpr int kAccumPerCu = 6;  // resident k_tile_accum workgroups per CU (4 waves each)
+#ifndef DM_ACCUM_OCC
+#define DM_ACCUM_OCC 7
+#endif
+constexpr int kAccumPerCu = DM_ACCUM_OCC;  // resident k_tile_accum workgroups per CU (4 waves each)
 __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     Geom g, ApplyArgs p, const int4* __restrict__ list_a, int cnt_a, const int4* __restrict__ list_b,
     int cnt_b, const PackedPiece* __restrict__ pieces, int32_t* tile_count, int32_t* tile_free,
