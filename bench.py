@@ -257,9 +257,10 @@ def main():
     avg = {name: tot / max(1, n) for name, (n, tot) in kstats.items()}
     dominant = max(kstats, key=lambda n: kstats[n][1]) if kstats else None
     # roofline of the dominant integrate kernel, k_tile_accum: it performs
-    # every update (8 B each) and applies the touched cells of light tiles
-    # (25 B each); k_heavy_apply applies the rest
-    TH_mean = float(np.mean([st["touched_heavy"] for st in stats]))
+    # every update (8 B each) and applies the touched cells (25 B each) —
+    # all of them, heavy tiles included, unless a separate k_heavy_apply ran
+    # (DM_HEAVY_SEPARATE=1)
+    TH_mean = float(np.mean([st["touched_heavy"] for st in stats])) if "heavy_apply" in kstats else 0.0
     t_accum_ms = avg.get("tile_accum", float("nan"))
     bytes_accum = (TILE_APPLY_BYTES_PER_UPDATE * U_mean
                    + TILE_APPLY_BYTES_PER_TOUCHED * (T_mean - TH_mean))
@@ -318,7 +319,7 @@ def main():
                 "traffic_source": traffic_src,
                 "avg_launch_ms": t_accum_ms,
                 "algorithmic_bytes_per_launch": bytes_accum,
-                "bytes_model": "8*U + 25*(T - T_heavy) per call (SURVEY.md §8(d) per-unit figures)",
+                "bytes_model": ("8*U + 25*(T - T_heavy) per call" if TH_mean else "8*U + 25*T per call") + " (SURVEY.md §8(d) per-unit figures)",
             },
             "stage_stats": {k: float(np.mean([st[k] for st in stats])) for k in stats[0]},
             "scans_per_rank_batch": float(np.mean([p.shape[0] for p, _ in pool])),
@@ -414,6 +415,8 @@ def _profiled_roofline(band, run, U_mean, T_mean, TH_mean):
     band.profile(False)
     avg = {name: tot / max(1, n) for name, (n, tot) in kstats.items()}
     t_ms = avg.get("tile_accum", float("nan"))
+    if "heavy_apply" not in kstats:  # heavy tiles applied inside k_tile_accum
+        TH_mean = 0.0
     bytes_accum = (TILE_APPLY_BYTES_PER_UPDATE * U_mean
                    + TILE_APPLY_BYTES_PER_TOUCHED * (T_mean - TH_mean))
     achieved = bytes_accum / (t_ms * 1e-3) / 1e9 if t_ms > 0 else None
@@ -421,7 +424,7 @@ def _profiled_roofline(band, run, U_mean, T_mean, TH_mean):
         "kernel": "tile_accum", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
         "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
         "traffic": None, "avg_launch_ms": t_ms, "algorithmic_bytes_per_launch": bytes_accum,
-        "bytes_model": "8*U + 25*(T - T_heavy) per call (SURVEY.md §8(d) per-unit figures)",
+        "bytes_model": ("8*U + 25*(T - T_heavy) per call" if TH_mean else "8*U + 25*T per call") + " (SURVEY.md §8(d) per-unit figures)",
     }
 
 

@@ -17,6 +17,8 @@
 
 #include "dm_internal.h"
 
+#include <stdlib.h>
+
 hipError_t dm_copy_shards(dm_grid* g) {
   return hipMemcpyAsync(g->h_sh, g->ish, sizeof(unsigned long long) * 2 * kShards * kShardWords,
                         hipMemcpyDeviceToHost, g->stream);
@@ -125,8 +127,10 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   if (heavy > g->heavy_cap) {
     int rc = dev_alloc(&g->heavy_list, heavy, "heavy tiles");
     if (!rc) rc = dev_alloc(&g->slabs, heavy * 2 * DM_TILE * DM_TILE, "heavy-tile slabs");
+    if (!rc) rc = dev_alloc(&g->heavy_done, heavy, "heavy-tile item tickets");
     if (rc) return rc;
     DM_HIP(hipMemset(g->slabs, 0, sizeof(uint32_t) * (size_t)(heavy * 2 * DM_TILE * DM_TILE)));
+    DM_HIP(hipMemset(g->heavy_done, 0, sizeof(int32_t) * (size_t)heavy));
     g->heavy_cap = heavy;
   }
   if (2 * (int64_t)N > g->trig_cap) {
@@ -400,6 +404,10 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if ((rc = dev_alloc(&g->tile_count, g->NT, "tile counts"))) return fail(rc);
   if ((rc = dev_alloc(&g->tile_cur, g->NT, "tile bin cursors"))) return fail(rc);
   if ((rc = dev_alloc(&g->tile_free, g->NT, "tile free counts"))) return fail(rc);
+  {
+    const char* sep = getenv("DM_HEAVY_SEPARATE");
+    g->fuse_heavy = !(sep && sep[0] == '1');
+  }
   if ((rc = dev_alloc(&g->cnt, CNT_N, "counters"))) return fail(rc);
   if ((rc = dev_alloc(&g->ish, 2 * kShards * kShardWords, "shard counters"))) return fail(rc);
   g->fsh = g->ish + kShards * kShardWords;
@@ -464,7 +472,7 @@ int dm_destroy(dm_grid* g) {
   dev_free(g->L); dev_free(g->state); dev_free(g->tile_count); dev_free(g->tile_cur);
   dev_free(g->tile_free); dev_free(g->cnt); dev_free(g->beams); dev_free(g->blk_hist); dev_free(g->blk_n); dev_free(g->pieces);
   dev_free(g->trig);
-  dev_free(g->hitems); dev_free(g->litems); dev_free(g->heavy_list); dev_free(g->slabs);
+  dev_free(g->hitems); dev_free(g->litems); dev_free(g->heavy_list); dev_free(g->slabs); dev_free(g->heavy_done);
   dev_free(g->pose4); dev_free(g->ranges); 
   dev_free(g->bs_rows); dev_free(g->bs_key); dev_free(g->bs_idx);
   dev_free(g->border); dev_free(g->ftiles); dev_free(g->slot_label); dev_free(g->slot_parent); dev_free(g->slot_root);

@@ -545,6 +545,69 @@ __device__ inline void finish_tile(const Geom& g, int32_t tile, int32_t T, int32
   tile_count[tile] = 0;                            // ready for the next call
 }
 
+// One 16-row quarter q of heavy tile h (ordinal in heavy_list): apply the
+// merged slab counts to the quarter's cells and clear the slab words.
+// Thread tid takes cell (row 4k + tid / 64, column tid % 64) of the quarter:
+// each wave instruction touches 256 contiguous slab bytes, the full-rate
+// shape for the memory-side atomics.  The read-and-clear is an exchange:
+// the slab was only ever written by the items' device-scope atomics, which
+// execute at the memory side, so the exchange reads the merged counts there
+// and leaves no stale L2 line.  Totals go to the workgroup's LDS counters.
+__device__ inline void heavy_quarter(const Geom& g, const ApplyArgs& p, int64_t h, int q, int32_t tile,
+                                     bool wide, uint32_t* __restrict__ slabs, float* __restrict__ L,
+                                     int8_t* __restrict__ state, int32_t* s_T, int32_t* s_free,
+                                     uint32_t* s_U) {
+  constexpr int kQ = DM_TS * DM_TS / 4;  // cells per quarter
+  const int tid = threadIdx.x;
+  const int32_t x = (tile % g.r.TX) * DM_TS + (tid & 63);
+  const int32_t yq = (tile / g.r.TX) * DM_TS + q * (DM_TS / 4) + (tid >> 6);
+  uint32_t* sh = slabs + h * (2 * DM_TS * DM_TS) + q * kQ + tid;
+  uint32_t hc[4], mc[4];
+  float lv[4];
+  int8_t sv[4];
+  // L / state first: their latency then overlaps the exchanges'
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int32_t y = yq + 4 * k;
+    lv[k] = 0.0f;
+    sv[k] = 0;
+    if (y < g.r.R && x < g.r.W) {
+      lv[k] = L[(int64_t)y * g.r.W + x];
+      sv[k] = state[(int64_t)y * g.r.W + x];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    hc[k] = atomicExch(sh + k * kQuarter, 0u);
+    mc[k] = wide ? atomicExch(sh + DM_TS * DM_TS + k * kQuarter, 0u) : 0u;
+  }
+  int32_t dT = 0, dFree = 0;
+  uint32_t dU = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t hk = hc[k], mk;
+    if (wide) {
+      mk = mc[k];
+    } else {  // packed: split the word
+      mk = hk & 0xFFFFu;
+      hk >>= 16;
+    }
+    const int32_t y = yq + 4 * k;
+    if ((hk | mk) == 0u || y >= g.r.R || x >= g.r.W) continue;
+    const int64_t i = (int64_t)y * g.r.W + x;
+    const float nl = apply_one(p, lv[k], hk, mk);
+    const int8_t ns = state_of(p, nl);
+    L[i] = nl;
+    state[i] = ns;
+    dU += hk + mk;
+    dT += 1;
+    dFree += (ns == 0) - (sv[k] == 0);
+  }
+  if (dT) atomicAdd(s_T, dT);
+  if (dFree) atomicAdd(s_free, dFree);
+  if (dU) atomicAdd(s_U, dU);
+}
+
 // Per-cell hit/miss counts never touch HBM: a 256-thread workgroup takes one
 // work item (<= kChunk pieces of one tile, one piece per thread), gathers
 // them in a packed LDS count tile (hits << 16 | misses) with walk_piece,
@@ -569,9 +632,10 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     Geom g, ApplyArgs p, const int4* __restrict__ list_a, int cnt_a, const int4* __restrict__ list_b,
     int cnt_b, const PackedPiece* __restrict__ pieces, int32_t* tile_count, int32_t* tile_free,
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
-    const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok) {
+    const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok,
+    const int32_t* __restrict__ heavy_list, int32_t* heavy_done) {
   __shared__ uint32_t tl[kTileWords + 64];  // + one spare word per lane (walk_piece_plain)
-  __shared__ int32_t s_T, s_free;
+  __shared__ int32_t s_T, s_free, s_last;
   __shared__ uint32_t s_U;
   const int tid = threadIdx.x, lane = lane_id();
   const int64_t HI = (int64_t)cnt[cnt_a], LI = cnt_b >= 0 ? (int64_t)cnt[cnt_b] : 0;
@@ -632,6 +696,33 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
         }
       }
       DM_PH(dm_phase_acc_integrate, 2);
+      // the tile's last item to finish applies the merged slab.  Slab adds,
+      // ticket and the finisher's slab exchanges are all agent-scope atomics,
+      // performed at the memory side (MI355X_MICROARCH.md, global atomics):
+      // every wave waits for its adds (vmcnt 0) before the barrier behind
+      // which one lane takes the ticket, so the last ticket sees every add —
+      // no release fence (an L2 write-back per heavy item: C3's tile_accum
+      // 42 -> 172 us with __threadfence)
+      if (heavy_done) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+          const int32_t n_it = (tile_count[tile] + kChunk - 1) / kChunk;  // k_plan's item count
+          s_last = atomicAdd(&heavy_done[heavy >> 1], 1) == n_it - 1;
+        }
+        __syncthreads();
+        if (s_last) {
+          const int64_t h = heavy >> 1;
+          const bool wide = heavy_list[h] < 0;
+          for (int q = 0; q < 4; ++q)
+            heavy_quarter(g, p, h, q, tile, wide, slabs, L, state, &s_T, &s_free, &s_U);
+          __syncthreads();
+          if (tid == 0) {
+            finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
+            heavy_done[h] = 0;  // ready for the next call
+          }
+        }
+      }
     } else {
       // light / medium: one piece per thread per round (medium tiles walk
       // their later rounds with in-loop loads); the cells' loads fly during
@@ -705,7 +796,6 @@ __global__ __launch_bounds__(kQuarter) void k_heavy_apply(
     const unsigned long long* __restrict__ cnt, unsigned long long* ish) {
   __shared__ int32_t s_T, s_free;
   __shared__ uint32_t s_U;
-  constexpr int kQ = DM_TS * DM_TS / 4;  // cells per quarter
   const int tid = threadIdx.x;
   const int64_t nq = 4 * (int64_t)cnt[CNT_HEAVY];
   DM_PH_INIT();
@@ -714,65 +804,12 @@ __global__ __launch_bounds__(kQuarter) void k_heavy_apply(
     const int q = (int)(it & 3);
     const int32_t hl = __builtin_amdgcn_readfirstlane(heavy_list[h]);
     const int32_t tile = hl & 0x7FFFFFFF;
-    const bool wide = hl < 0;
-    const int32_t x = (tile % g.r.TX) * DM_TS + (tid & 63);
-    const int32_t yq = (tile / g.r.TX) * DM_TS + q * (DM_TS / 4) + (tid >> 6);
-    uint32_t* sh = slabs + h * (2 * DM_TS * DM_TS) + q * kQ + tid;
-    // read-and-clear with atomics: the slab was only ever written by the
-    // items' device-scope atomics, which execute at the memory side, so the
-    // exchange reads the merged counts there and leaves no stale L2 line
-    uint32_t hc[4], mc[4];
-    float lv[4];
-    int8_t sv[4];
-    // L / state first: their latency then overlaps the exchanges'
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int32_t y = yq + 4 * k;
-      lv[k] = 0.0f;
-      sv[k] = 0;
-      if (y < g.r.R && x < g.r.W) {
-        lv[k] = L[(int64_t)y * g.r.W + x];
-        sv[k] = state[(int64_t)y * g.r.W + x];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      hc[k] = atomicExch(sh + k * kQuarter, 0u);
-      if (wide) mc[k] = atomicExch(sh + DM_TS * DM_TS + k * kQuarter, 0u);
-    }
     if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; }
     __syncthreads();
-    DM_PH(dm_phase_acc_integrate, 8);
-    int32_t dT = 0, dFree = 0;
-    uint32_t dU = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      uint32_t hk = hc[k], mk;
-      if (wide) {
-        mk = mc[k];
-      } else {  // packed: split the word
-        mk = hk & 0xFFFFu;
-        hk >>= 16;
-      }
-      const int32_t y = yq + 4 * k;
-      if ((hk | mk) == 0u || y >= g.r.R || x >= g.r.W) continue;
-      const int64_t i = (int64_t)y * g.r.W + x;
-      const float nl = apply_one(p, lv[k], hk, mk);
-      const int8_t ns = state_of(p, nl);
-      L[i] = nl;
-      state[i] = ns;
-      dU += hk + mk;
-      dT += 1;
-      dFree += (ns == 0) - (sv[k] == 0);
-    }
-    if (dT) atomicAdd(&s_T, dT);
-    if (dFree) atomicAdd(&s_free, dFree);
-    if (dU) atomicAdd(&s_U, dU);
+    heavy_quarter(g, p, h, q, tile, hl < 0, slabs, L, state, &s_T, &s_free, &s_U);
     __syncthreads();
     DM_PH(dm_phase_acc_integrate, 9);
-    if (tid == 0) {
-      finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
-    }
+    if (tid == 0) finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
     __syncthreads();
     DM_PH(dm_phase_acc_integrate, 10);
     DM_PH_COUNT(dm_phase_acc_integrate, 20, q == 0);
@@ -940,7 +977,8 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   hipLaunchKernelGGL(k_tile_accum, dim3(grid_for(g->hitem_cap + g->act_cap, 1, 16384)),
                      dim3(kQuarter), 0,
                      g->stream, ge, make_apply(g), g->hitems, (int)CNT_ITEMS, g->litems, (int)CNT_LITEMS,
-                     g->pieces, g->tile_count, g->tile_free, g->slabs, g->L, g->state, g->cnt, g->ish, vec_ok);
+                     g->pieces, g->tile_count, g->tile_free, g->slabs, g->L, g->state, g->cnt, g->ish, vec_ok,
+                     g->heavy_list, g->fuse_heavy ? g->heavy_done : nullptr);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   // A beam meets a (convex) tile in one k-range of <= 64 steps, and chunks
@@ -948,7 +986,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   // beams are chunked).  Calls that cannot reach kMedium pieces in any tile
   // (one 360-beam scan: C1 / C2) have no heavy tile: no k_heavy_apply.
   const int64_t max_tile_pieces = nb * (ge.chunks > 1 ? 2 : 1);
-  if (max_tile_pieces <= kMedium) {
+  if (max_tile_pieces <= kMedium || g->fuse_heavy) {
     if (g->overlap) g->tiles_mark_pending = true;
     return DM_OK;
   }

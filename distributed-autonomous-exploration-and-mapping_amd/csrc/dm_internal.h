@@ -162,6 +162,10 @@ struct dm_grid {
   int32_t* heavy_list = nullptr; // heavy ordinal -> tile
   int64_t heavy_cap = 0;
   uint32_t* slabs = nullptr;     // [heavy][2][64*64] merged hit / miss counts
+  int32_t* heavy_done = nullptr; // [heavy] items finished this call (the last one applies the slab)
+  // heavy tiles applied by their last k_tile_accum item (default) instead of
+  // a separate k_heavy_apply launch (DM_HEAVY_SEPARATE=1, A/B measurement)
+  bool fuse_heavy = true;
   double* trig = nullptr; int32_t trig_n = -1; float trig_amin = 0, trig_inc = 0;
   int64_t trig_cap = 0;
   double* pose4 = nullptr; int64_t pose_cap = 0;
