@@ -14,7 +14,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROFILES = os.path.join(REPO, "profiles")
 
 LINES = {
-    "r01_occ7_bench.json": "C3",
+    "r01_fused_bench.json": "C3",
     "r01_c1_replay_bench.json": "C1",
     "r01_c2_replay_bench.json": "C2",
     "r01_c4_1gpu_bench.json": "C4",
@@ -48,7 +48,7 @@ def test_bench_line_fields(name, cfg):
 
 
 def test_headline_line_has_traffic_and_cpu_baseline():
-    d = _load("r01_occ7_bench.json")
+    d = _load("r01_fused_bench.json")
     assert d["n_gpus"] == 1 and d["scaling"] == "weak"
     assert d["roofline"]["traffic"] and d["roofline"]["traffic"] > 0
     assert d["cpu_baseline"] and d["cpu_baseline"]["value"] > 0
