@@ -354,3 +354,33 @@ def test_heavy_apply_skip_boundary(oracle_lib, S, N):
             assert m.last_stats()["heavy_tiles"] >= 1
         assert_map_equal(m, om)
         assert_frontiers_equal(m.frontiers(want_mask=True, want_labels=True), *om.frontiers())
+
+
+@pytest.mark.parametrize("separate", [False, True])
+@pytest.mark.parametrize("S", [6, 17])
+def test_heavy_apply_fused_and_separate(oracle_lib, monkeypatch, S, separate):
+    """Heavy tiles applied by their last k_tile_accum item (the ticket in
+    heavy_done, default) or by the separate k_heavy_apply launch
+    (DM_HEAVY_SEPARATE=1, read at dm_create): both bit-exact against the
+    oracle over several calls (the tickets are reset by the finisher for the
+    next call), with three sensors sharing the batch (several heavy tiles per
+    call; S=17 puts > 65535 pieces on one tile: wide slab)."""
+    if separate:
+        monkeypatch.setenv("DM_HEAVY_SEPARATE", "1")
+    else:
+        monkeypatch.delenv("DM_HEAVY_SEPARATE", raising=False)
+    p = cases.make_params(500, 400)
+    rng = np.random.Generator(np.random.PCG64(31 + S))
+    centres = np.array([[0.013, -0.021, 0.3], [4.41, 2.07, 1.1], [-6.3, -3.9, 2.0]])
+    N = 4096
+    amin, inc = 0.0, float(np.float32(2 * np.pi / (N - 1)))
+    om = oracle_lib.OracleMap(p)
+    with dm.OccupancyMapper(p) as m:
+        for k in range(3):
+            poses = centres[np.arange(S) % 3 if S < 17 else np.zeros(S, int)].copy()
+            poses[:, 2] += rng.uniform(-0.01, 0.01, S)
+            ranges = (np.round(rng.uniform(0.05, 8.0, (S, N)) * 1000) / 1000).astype(np.float32)
+            assert m.integrate(poses, ranges, amin, inc) == om.integrate(poses, ranges, amin, inc)
+            assert m.last_stats()["heavy_tiles"] >= (1 if S >= 17 else 3)
+        assert_map_equal(m, om)
+        assert_frontiers_equal(m.frontiers(want_mask=True, want_labels=True), *om.frontiers())
