@@ -64,6 +64,10 @@ def parse():
     ap.add_argument("--scans", type=int, default=None,
                     help="C1 / C2: scans in the replay (default 1000 / 10000)")
     ap.add_argument("--sweep", default="12,48,192,768,4096", help="C5: beams per scan")
+    ap.add_argument("--no-explored", action="store_true",
+                    help="skip the explored-map frontier measurement (frontier_ms_explored)")
+    ap.add_argument("--no-host-inputs", action="store_true",
+                    help="skip the PCIe-inclusive measurement (value_host_inputs)")
     return ap.parse_args()
 
 
@@ -183,21 +187,25 @@ def main():
     # unchanged, only independent kernels overlap.
     pipelined = not args.no_overlap
 
-    def run_steps(k0, n):
+    def run_steps(k0, n, integ=None):
+        integ = integ or integrate
         if n <= 0:
             return None
         if not pipelined:
             fr = None
             for k in range(n):
-                fr = step(k0 + k)
+                integ(k0 + k)
+                fr = mapper.frontiers()
             return fr
-        integrate(k0)
+        integ(k0)
         mapper.frontiers_begin()
         for k in range(1, n):
-            integrate(k0 + k)
+            integ(k0 + k)
             mapper.frontiers_end()
             mapper.frontiers_begin()
-        return mapper.frontiers_end()
+        fr = mapper.frontiers_end()
+        # None: the pass overflowed a capacity (grown now); rerun on this map
+        return fr if fr is not None else mapper.frontiers()
 
     if pipelined:
         mapper.set_overlap(True)
@@ -242,6 +250,7 @@ def main():
         a = time.perf_counter()
         fr = mapper.frontiers()
         tf.append(time.perf_counter() - a)
+    fstats = band.last_stats()  # the last pass's visited tiles / slots / clusters
     t_int = float(np.median(ti))
     t_fr = float(np.median(tf))
     U_mean = float(np.mean([c[0] for c in counts]))
@@ -265,7 +274,62 @@ def main():
     bytes_accum = (TILE_APPLY_BYTES_PER_UPDATE * U_mean
                    + TILE_APPLY_BYTES_PER_TOUCHED * (T_mean - TH_mean))
     achieved = bytes_accum / (t_accum_ms * 1e-3) / 1e9 if t_accum_ms > 0 else None
-    traffic, traffic_src = pmc_traffic("k_tile_accum")
+    workload = "C4" if c4 else "C3"
+    traffic, traffic_src = pmc_traffic("k_tile_accum", workload)
+    fr_roof = None
+    if world_size == 1:
+        F_cells = int(fr.clusters["size"].sum()) if len(fr) else 0
+        fr_roof = frontier_roofline(avg, G * H_total, F_cells, len(fr), fstats["frontier_tiles"], workload,
+                                    t_fr)
+
+    # PCIe-inclusive rate: the same pipelined steps fed from pinned host
+    # buffers through dm_integrate_async (H2D of ranges + poses on the
+    # library's front-end stream, overlapped with the previous frontier pass)
+    host_inputs = None
+    if not args.no_host_inputs:
+        pinned = [torch.from_numpy(np.ascontiguousarray(r, np.float32)).pin_memory() for _, r in pool]
+
+        def integrate_host(k):
+            poses_k = pool[k % len(pool)][0]
+            band.integrate_async(poses_k, pinned[k % len(pool)].data_ptr(), poses_k.shape[0], N, amin, inc)
+
+        band.reset()
+        run_steps(0, args.warmup, integrate_host)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run_steps(args.warmup, args.steps, integrate_host)
+        band.synchronize()
+        torch.cuda.synchronize()
+        barrier()
+        el_h = time.perf_counter() - t0
+        if world_size > 1:
+            t = torch.tensor([el_h], dtype=torch.float64, device=cdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_h = float(t.item())
+        host_inputs = {"value": U_all / el_h, "ms_per_step": el_h / args.steps * 1e3,
+                       "bytes_per_step": float(np.mean([4 * r.size + 24 * p_.shape[0] for p_, r in pool])),
+                       "how": "dm_integrate_async from pinned host buffers (poses as (x, y, yaw): cos/sin "
+                              "on the host per call), pipelined like `value`"}
+
+    # atomic throughput of the raycast against the device's measured peak
+    # (north star): every beam-cell update is one LDS add
+    atom = None
+    if rank == 0:
+        pk = dm.atomic_peak(local_rank)
+        a_ach = U_mean / (t_accum_ms * 1e-3) if t_accum_ms > 0 else None
+        atom = {"kernel": "tile_accum", "achieved": a_ach, "peak": pk["lds_add_u32_per_s"],
+                "unit": "LDS atomic adds/s", "frac": a_ach / pk["lds_add_u32_per_s"] if a_ach else None,
+                "global_peak": pk["global_add_u32_per_s"],
+                "ops_model": "one ds_add_u32 per beam-cell update (U per launch); peak = dm_atomic_peak "
+                             "(uncontended ds_add_u32, every lane its own bank, 8 workgroups/CU)"}
+
+    # frontier worst case: one pass over a mostly explored map (every tile
+    # read), N=1 only (SURVEY.md §8(d) frontier bytes 2*W*H + 16*F + 48*K)
+    explored = None
+    if world_size == 1 and not args.no_explored and not c4:
+        explored = explored_frontier(band, mapper, synth, world, G, H_total, res, -half_w, oy_global,
+                                     args.seed, reps, np)
 
     result = None
     if rank == 0:
@@ -320,7 +384,13 @@ def main():
                 "avg_launch_ms": t_accum_ms,
                 "algorithmic_bytes_per_launch": bytes_accum,
                 "bytes_model": ("8*U + 25*(T - T_heavy) per call" if TH_mean else "8*U + 25*T per call") + " (SURVEY.md §8(d) per-unit figures)",
+                "atomics": atom,
+                "frontier": fr_roof,
             },
+            "value_host_inputs": host_inputs["value"] if host_inputs else None,
+            "host_inputs": host_inputs,
+            "frontier_ms_explored": explored["frontier_ms"] if explored else None,
+            "frontier_explored": explored,
             "stage_stats": {k: float(np.mean([st[k] for st in stats])) for k in stats[0]},
             "scans_per_rank_batch": float(np.mean([p.shape[0] for p, _ in pool])),
             "exchange": ("device: RCCL all-gather of halo rows + export records, dm_merge_bands"
@@ -338,10 +408,10 @@ def main():
     return result
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary
-    (tools/pmc_passes.sh + tools/pmc_summary.py), only if it was measured on
-    the same libdm sources; otherwise None."""
+def pmc_summary(workload):
+    """The committed PMC summary of `workload` (tools/pmc_passes.sh +
+    tools/pmc_summary.py -> profiles/pmc_latest.json, keyed by workload), only
+    if it was measured on the same libdm sources; else (None, reason)."""
     sys.path.insert(0, os.path.join(REPO, "tools"))
     try:
         from src_hash import src_hash
@@ -350,8 +420,97 @@ def pmc_traffic(kernel):
         return None, None
     if summ.get("src_hash") != src_hash():
         return None, "profiles/pmc_latest.json is from other sources"
-    k = summ.get("kernels", {}).get(kernel, {})
-    return k.get("traffic_bytes"), "profiles/pmc_latest.json (2*FETCH_SIZE + WRITE_SIZE, KiB->B)"
+    w = summ.get("workloads", {}).get(workload)
+    if w is None:
+        return None, f"profiles/pmc_latest.json has no {workload} workload"
+    return w, f"profiles/pmc_latest.json [{workload}] (2*FETCH_SIZE + WRITE_SIZE, KiB->B)"
+
+
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` measured on `workload`, or None."""
+    w, src = pmc_summary(workload)
+    if w is None:
+        return None, src
+    return w.get("kernels", {}).get(kernel, {}).get("traffic_bytes"), src
+
+
+FRONTIER_KERNELS = ("frontier_prep", "frontier_tile", "frontier_merge", "frontier_resolve",
+                    "frontier_compact", "sort_clusters")
+PMC_FRONTIER_KERNELS = ("k_frontier_prep", "k_frontier_tile", "k_frontier_merge", "k_frontier_resolve",
+                        "k_frontier_compact", "k_rank_sort", "k_bs_count", "k_bs_scan", "k_bs_place",
+                        "k_bs_rank")
+
+
+def frontier_roofline(avg, cells, F, K, tiles_visited, workload, wall_s=None):
+    """Frontier pass vs the HBM roofline.  Algorithmic bytes per pass
+    (SURVEY.md §8(d)): B_fr = 2*W*H (read state, write a byte mask) + 16*F
+    (int64 label write + read per frontier cell) + 48*K (cluster records),
+    over the pass's device time (sum of its kernels' HIP-event averages).
+    The kernels read only the tiles holding a free cell, so
+    `visited_bytes` restates B_fr over those tiles alone (4096 state bytes +
+    260 halo bytes + a 4096-byte mask each)."""
+    t_ms = sum(avg.get(k, 0.0) for k in FRONTIER_KERNELS)
+    B = 2.0 * cells + 16.0 * F + 48.0 * K
+    ach = B / (t_ms * 1e-3) / 1e9 if t_ms > 0 else None
+    out = {"bound": "hbm", "bytes_model": "2*W*H + 16*F + 48*K per pass (SURVEY.md §8(d))",
+           "algorithmic_bytes": B, "frontier_cells": F, "clusters": K, "device_ms": t_ms,
+           "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+           "frac": ach / HBM_PEAK_GBPS if ach else None,
+           "kernels_ms": {k: avg[k] for k in FRONTIER_KERNELS if k in avg}}
+    if wall_s:
+        out["wall_ms"] = wall_s * 1e3
+    if tiles_visited is not None:
+        vb = (4096.0 + 260.0 + 4096.0) * tiles_visited + 16.0 * F + 48.0 * K
+        out["tiles_visited"] = tiles_visited
+        out["visited_bytes"] = vb
+        out["frac_visited"] = vb / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if t_ms > 0 else None
+    w, src = pmc_summary(workload)
+    if w is not None:
+        ks = w.get("kernels", {})
+        tr = [ks[k]["traffic_bytes"] for k in PMC_FRONTIER_KERNELS if "traffic_bytes" in ks.get(k, {})]
+        out["traffic"] = sum(tr) if tr else None
+        out["traffic_source"] = src
+    else:
+        out["traffic"] = None
+        out["traffic_source"] = src
+    return out
+
+
+def explored_frontier(band, mapper, synth, world, W, H, res, ox, oy, seed, reps, np):
+    """frontier_ms on a mostly explored W x H map (synth.explored_state:
+    free space, obstacle outlines, unknown pockets; >= 90 % of the tiles hold
+    free cells, so the pass reads the whole map): median wall time of `reps`
+    synchronous passes, per-kernel HIP-event times and the roofline."""
+    a = time.perf_counter()
+    st = synth.explored_state(world, W, H, res, ox, oy, seed=seed * 1000 + 77)
+    t_gen = time.perf_counter() - a
+    tiles = st.reshape(-1, 64, W // 64, 64)
+    tiles_free = float((tiles == 0).any(axis=(1, 3)).mean())
+    del tiles
+    band.reset()
+    band.set_state(st)
+    del st
+    mapper.set_overlap(False)
+    fr = mapper.frontiers()
+    tf = []
+    for _ in range(reps):
+        a = time.perf_counter()
+        fr = mapper.frontiers()
+        tf.append(time.perf_counter() - a)
+    fst = band.last_stats()
+    band.profile(True)
+    band.profile_reset()
+    for _ in range(reps):
+        mapper.frontiers()
+    kst = band.profile_read()
+    band.profile(False)
+    avg = {name: tot / max(1, n) for name, (n, tot) in kst.items()}
+    F = int(fr.clusters["size"].sum()) if len(fr) else 0
+    t = float(np.median(tf))
+    return {"frontier_ms": t * 1e3, "grid": [W, H], "tiles_with_free_cells": tiles_free,
+            "tiles_visited": fst["frontier_tiles"], "frontier_slots": fst["frontier_slots"],
+            "clusters": len(fr), "frontier_cells": F, "gen_seconds": t_gen,
+            "roofline": frontier_roofline(avg, W * H, F, len(fr), fst["frontier_tiles"], "C3-explored", t)}
 
 
 def cpu_baseline(params, pool, amin, inc, budget_s):

@@ -449,6 +449,10 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     e = hipEventCreateWithFlags(&r.ev, hipEventDisableTiming);
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
   }
+  for (hipEvent_t& ev : g->ev_pose) {  // host waits on these before reusing a staging buffer
+    e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
+  }
   if ((rc = dm_reset(g))) return fail(rc);
   *out = g;
   return DM_OK;
@@ -484,7 +488,10 @@ int dm_destroy(dm_grid* g) {
   if (g->h_mcnt) (void)hipHostFree(g->h_mcnt);
   if (g->h_cnt) (void)hipHostFree(g->h_cnt);
   if (g->h_sh) (void)hipHostFree(g->h_sh);
-  if (g->h_pose4) (void)hipHostFree(g->h_pose4);
+  for (int i = 0; i < dm_grid::kPoseRing; ++i) {
+    if (g->h_pose4[i]) (void)hipHostFree(g->h_pose4[i]);
+    if (g->ev_pose[i]) (void)hipEventDestroy(g->ev_pose[i]);
+  }
   if (g->stream && g->own_stream) (void)hipStreamDestroy(g->stream);
   delete g;
   return DM_OK;
@@ -511,15 +518,28 @@ int dm_get_params(const dm_grid* g, dm_params* out) {
   return DM_OK;
 }
 
-int dm_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N, const float* ranges,
-                 float angle_min, float angle_increment, uint64_t* out_updates,
-                 uint64_t* out_touched) {
-  int rc = check_grid(g);
-  if (rc || (rc = use_device(g))) return rc;
+}  // extern "C"
+
+namespace {
+
+// Host inputs -> device: poses to (x, y, cos yaw, sin yaw) with the C
+// library (as the oracle) into the next pinned staging buffer of the ring,
+// then both H2D copies on the front-end stream, then the integrate launch.
+// Nothing here waits for the device except a staging buffer whose copy (two
+// calls ago) has not finished yet.
+int enqueue_host_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N, const float* ranges,
+                           float angle_min, float angle_increment) {
+  int rc = 0;
   if ((rc = check_integrate_args(S, N, poses, ranges))) return rc;
   if ((rc = grow_integrate(g, S, N))) return rc;
   if ((rc = ensure_trig(g, N, angle_min, angle_increment))) return rc;
   const int64_t nb = (int64_t)S * N;
+  hipStream_t fs = g->overlap ? g->fe_stream : g->stream;
+  if ((int64_t)S * 4 > g->pose_cap || nb > g->ranges_cap || (int64_t)S * 4 > g->h_pose_cap) {
+    // the device buffers may still feed an in-flight call
+    DM_HIP(hipStreamSynchronize(g->stream));
+    DM_HIP(hipStreamSynchronize(g->fe_stream));
+  }
   if ((int64_t)S * 4 > g->pose_cap) {
     if ((rc = dev_alloc(&g->pose4, (int64_t)S * 4, "poses"))) return rc;
     g->pose_cap = (int64_t)S * 4;
@@ -529,29 +549,34 @@ int dm_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N, const fl
     g->ranges_cap = nb;
   }
   if ((int64_t)S * 4 > g->h_pose_cap) {
-    DM_HIP(hipStreamSynchronize(g->stream));
-    if (g->h_pose4) (void)hipHostFree(g->h_pose4);
-    g->h_pose4 = nullptr;
-    DM_HIP(hipHostMalloc((void**)&g->h_pose4, sizeof(double) * 4 * (size_t)S, hipHostMallocDefault));
-    g->h_pose_cap = (int64_t)S * 4;
+    for (int i = 0; i < dm_grid::kPoseRing; ++i) {
+      if (g->h_pose4[i]) (void)hipHostFree(g->h_pose4[i]);
+      g->h_pose4[i] = nullptr;
+    }
+    g->h_pose_cap = 0;
+    for (int i = 0; i < dm_grid::kPoseRing; ++i)
+      DM_HIP(hipHostMalloc((void**)&g->h_pose4[i], sizeof(double) * 4 * (size_t)std::max(S, 1),
+                           hipHostMallocDefault));
+    g->h_pose_cap = (int64_t)std::max(S, 1) * 4;
   }
-  // the pinned pose staging buffer may still feed an in-flight copy
-  hipStream_t fs = g->overlap ? g->fe_stream : g->stream;
-  DM_HIP(hipStreamSynchronize(fs));
+  const int slot = g->pose_head;
+  g->pose_head = (g->pose_head + 1) % dm_grid::kPoseRing;
+  DM_HIP(hipEventSynchronize(g->ev_pose[slot]));  // its copy (two calls ago) is done
+  double* hp = g->h_pose4[slot];
   for (int32_t s = 0; s < S; ++s) {
     const double x = poses[3 * s], y = poses[3 * s + 1], yaw = poses[3 * s + 2];
-    g->h_pose4[4 * s + 0] = x;
-    g->h_pose4[4 * s + 1] = y;
-    g->h_pose4[4 * s + 2] = cos(yaw);  // C library, as the oracle
-    g->h_pose4[4 * s + 3] = sin(yaw);
+    hp[4 * s + 0] = x;
+    hp[4 * s + 1] = y;
+    hp[4 * s + 2] = cos(yaw);  // C library, as the oracle
+    hp[4 * s + 3] = sin(yaw);
   }
   if (g->overlap) {  // pose4 / ranges of the last call read
     DM_HIP(dm_mark_tiles(g));
     DM_HIP(hipStreamWaitEvent(fs, g->ev_tiles, 0));
   }
   if (S > 0)
-    DM_HIP(hipMemcpyAsync(g->pose4, g->h_pose4, sizeof(double) * 4 * (size_t)S,
-                          hipMemcpyHostToDevice, fs));
+    DM_HIP(hipMemcpyAsync(g->pose4, hp, sizeof(double) * 4 * (size_t)S, hipMemcpyHostToDevice, fs));
+  DM_HIP(hipEventRecord(g->ev_pose[slot], fs));
   if (nb > 0)
     DM_HIP(hipMemcpyAsync(g->ranges, ranges, sizeof(float) * (size_t)nb, hipMemcpyHostToDevice, fs));
   if ((rc = dm_launch_integrate(g, S, g->pose4, N, g->ranges, g->trig))) return rc;
@@ -559,7 +584,27 @@ int dm_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N, const fl
   g->last_N = N;
   g->frontier_valid = false;
   ++g->integrate_seq;
+  return DM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dm_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N, const float* ranges,
+                 float angle_min, float angle_increment, uint64_t* out_updates,
+                 uint64_t* out_touched) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if ((rc = enqueue_host_integrate(g, S, poses, N, ranges, angle_min, angle_increment))) return rc;
   return finish_counts(g, out_updates, out_touched);
+}
+
+int dm_integrate_async(dm_grid* g, int32_t S, const double* poses, int32_t N, const float* ranges,
+                       float angle_min, float angle_increment) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  return enqueue_host_integrate(g, S, poses, N, ranges, angle_min, angle_increment);
 }
 
 int dm_integrate_device(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
@@ -757,7 +802,7 @@ int merge_readback(dm_grid* g, int slot, int64_t n, dm_cluster* out, int64_t cap
     if (n_out) *n_out = (int64_t)g->h_mcnt[3];
     return dm_set_error(DM_ERR_INCOMPLETE,
                         "a band export is incomplete (flags %llu: 1 slot overflow, 2 K > rec_cap, "
-                        "4 unsorted, 8 width mismatch, 16 bands not contiguous); largest band K %llu",
+                        "4 unsorted, 8 width mismatch, 16 bands not contiguous, 32 union-find bound); largest band K %llu",
                         (unsigned long long)g->h_mcnt[1], (unsigned long long)g->h_mcnt[3]);
   }
   const int64_t K = (int64_t)g->h_mcnt[0];

@@ -417,7 +417,7 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile(
     for (int r = tid; r < nruns; r += kFT) {
       if (r_par[r] != r) continue;
       const int c = root_rank(s_root, s_rootpre, r);
-      if (base + c >= g.slot_per) { atomicOr(&cnt[CNT_OVERFLOW], 4ull); continue; }
+      if (base + c >= g.slot_per) { atomicOr(&cnt[CNT_OVERFLOW], kOvSlots); continue; }
       const long long slot = sh0 + base + c;
       const long long gy = (long long)g.row0 + ty0 + r_y[r];
       const long long gx = (long long)tx0 + r_s[r];
@@ -489,7 +489,7 @@ __global__ __launch_bounds__(256) void k_frontier_merge(FGeom g, const int32_t* 
                                                         const int32_t* __restrict__ border,
                                                         const long long* __restrict__ slot_label,
                                                         int32_t* slot_parent,
-                                                        const unsigned long long* cnt) {
+                                                        unsigned long long* cnt) {
   const int lane = __lane_id();
   const int64_t nunits = 2 * (int64_t)*list_n;
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -529,7 +529,7 @@ __global__ __launch_bounds__(256) void k_frontier_merge(FGeom g, const int32_t* 
       bool dup = false;
       for (int r = 0; r < q; ++r) dup |= sb[r] == b;
       if (lane > 0 && psa == sa) dup |= (psb[0] == b) | (psb[1] == b) | (psb[2] == b);
-      if (!dup) dm_uf_unite(slot_parent, slot_label, sa, b);
+      if (!dup) dm_uf_unite(slot_parent, slot_label, sa, b, &cnt[CNT_OVERFLOW], kOvUnionFind);
     }
   }
 }
@@ -584,7 +584,7 @@ __global__ __launch_bounds__(256) void k_frontier_resolve(FGeom g, const int32_t
   for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); s0 < g.slot_cap; s0 += stride) {
     const int64_t s = s0 + lane;
     const bool used = slot_used(g, s_n, s);
-    const int32_t r = used ? dm_uf_root(slot_parent, (int32_t)s) : -1;
+    const int32_t r = used ? dm_uf_root(slot_parent, (int32_t)s, &cnt[CNT_OVERFLOW], kOvUnionFind) : -1;
     if (used) slot_root[s] = r;
     if (fuse) {
       // min_size <= 1: every root is a cluster, so k_frontier_compact's
@@ -1033,9 +1033,12 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   g->fparity ^= 1;
   unsigned long long* list_n = g->cnt + (g->fparity ? CNT_FL1 : CNT_FL0);
   unsigned long long* other_n = g->cnt + (g->fparity ? CNT_FL0 : CNT_FL1);
+  KernelTimer t;
+  dm_timer_begin(g, "frontier_prep", &t);
   hipLaunchKernelGGL(k_frontier_prep, dim3(grid_for(std::max<int64_t>(std::max<int64_t>(g->NT, 2 * g->W), kShards * kShardWords), 256, 1024)), dim3(256), 0,
                      g->stream, g->NT, g->tile_free, g->ftiles, list_n, other_n, 2 * g->W, g->cnt, g->fsh,
                      g->edge_slot);
+  dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   // the last integrate call's tile workspace is free once the map update
   // (ahead of the prep in stream order) is done: the next call's front-end
@@ -1043,7 +1046,6 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   DM_HIP(dm_mark_tiles(g));
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));
-  KernelTimer t;
   const int nft_grid = grid_for(g->NT, 1, 2048);
   // k_frontier_tile: one listed tile per workgroup (the dispatcher balances)
   const int ftile_grid = grid_for(g->NT, 1, 8192);
@@ -1106,10 +1108,13 @@ int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied) {
   memcpy(g->h_cnt, hdr, sizeof(unsigned long long) * CNT_N);
   *copied = std::min<int64_t>(g->h_out_cap, g->slot_cap);
   const unsigned long long most = hdr[CNT_N];
-  if ((int64_t)most > g->slot_cap / kShards || (g->h_cnt[CNT_OVERFLOW] & 4ull)) {
+  if ((int64_t)most > g->slot_cap / kShards || (g->h_cnt[CNT_OVERFLOW] & kOvSlots)) {
     *n_clusters = (int64_t)most * kShards;  // slot capacity that fits the fullest shard
     return DM_ERR_CAPACITY;
   }
+  if (g->h_cnt[CNT_OVERFLOW] & kOvUnionFind)
+    return dm_set_error(DM_ERR_INCOMPLETE, "frontier union-find did not converge within its bound "
+                                           "(dm_uf.h): this pass has no result");
   *n_clusters = (int64_t)g->h_cnt[CNT_CLUSTERS];
   g->sort_hint = *n_clusters;
   return DM_OK;

@@ -36,6 +36,7 @@ struct Geom {
   RayGeom r;
   int32_t act_cap;
   int64_t seg_cap;
+  int64_t hitem_cap, heavy_cap;  // capacities of hitems / heavy_list (k_plan clamps its writes)
   int64_t nb;  // beams in this call
   int32_t chunks, chunk_len;  // each beam enumerated as `chunks` k-ranges (dm_integrate_chunks)
 };
@@ -275,6 +276,14 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __
     const unsigned long long ho = wave_alloc(&cnt[CNT_HEAVY], heavy ? 1ull : 0ull);
     if (t < 0) continue;
     tile_cur[t] = (int32_t)p0;  // k_scatter's cursor: the tile's bin start
+    // the host sizes every list for the worst case (grow_integrate); a write
+    // past a capacity anyway is flagged (DM_ERR_CAPACITY) and dropped
+    const bool fits = (int64_t)(p0 + c) <= g.seg_cap && (int64_t)(hi + nh_items) <= g.hitem_cap &&
+                      (int64_t)li < (int64_t)g.act_cap && (int64_t)ho < g.heavy_cap;
+    if (!fits) {
+      atomicOr(&cnt[CNT_IOVERFLOW], 4ull);
+      continue;
+    }
     if (light) {
       litems[li] = make_int4(t, (int32_t)p0, c, -1);
     } else if (medium) {  // one item, walked in rounds of kChunk, applied directly
@@ -638,12 +647,17 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
   __shared__ int32_t s_T, s_free, s_last;
   __shared__ uint32_t s_U;
   const int tid = threadIdx.x, lane = lane_id();
-  const int64_t HI = (int64_t)cnt[cnt_a], LI = cnt_b >= 0 ? (int64_t)cnt[cnt_b] : 0;
+  // (clamped to the list capacities: k_plan flags and drops what does not fit)
+  const int64_t HI = min((int64_t)cnt[cnt_a], g.hitem_cap);
+  const int64_t LI = cnt_b >= 0 ? min((int64_t)cnt[cnt_b], (int64_t)g.act_cap) : 0;
   const int64_t n_items = HI + LI;
   const int64_t G = gridDim.x;
   if ((int64_t)blockIdx.x >= n_items) return;
   auto item_of = [&](int64_t it) {
-    return it < n_items ? (it < HI ? list_a[it] : list_b[it - HI]) : make_int4(0, 0, 0, -1);
+    int4 d = it < n_items ? (it < HI ? list_a[it] : list_b[it - HI]) : make_int4(0, 0, 0, -1);
+    // an item never reads past the piece array (k_plan keeps p0 + c <= seg_cap)
+    d.z = (int64_t)d.y + d.z <= g.seg_cap ? d.z : 0;
+    return d;
   };
   const int cx = (tid & 15) * 4;
   __shared__ unsigned long long s_accT, s_accU;  // this workgroup's light-tile totals
@@ -884,6 +898,8 @@ Geom make_geom(const dm_grid* g) {
   ge.r.TY = (int32_t)g->TY;
   ge.act_cap = (int32_t)g->act_cap;
   ge.seg_cap = g->segs_cap;
+  ge.hitem_cap = g->hitem_cap;
+  ge.heavy_cap = g->heavy_cap;
   ge.nb = 0;
   ge.chunks = 1;
   ge.chunk_len = 0;

@@ -32,7 +32,7 @@ enum {
   CNT_FTILES = 4,   // tiles visited by the frontier pass (tile_free > 0)
   CNT_SLOTS = 5,    // tile-local frontier components
   CNT_CLUSTERS = 6, // output clusters
-  CNT_OVERFLOW = 7, // capacity overflow flags
+  CNT_OVERFLOW = 7, // frontier flags: kOvSlots (slot arrays full), kOvUnionFind (bound hit)
   CNT_ITEMS = 8,    // heavy work items (<= 256 pieces of a heavy tile each)
   CNT_HEAVY = 9,    // heavy tiles (> 256 pieces)
   CNT_TH = 10,      // touched cells of heavy tiles
@@ -43,6 +43,9 @@ enum {
   CNT_IOVERFLOW = 15,  // integrate capacity overflow flags (1 first-touch list, 2 pieces)
   CNT_N = 16
 };
+// CNT_OVERFLOW bits of a frontier pass
+constexpr unsigned long long kOvSlots = 4ull;      // a slot shard region overflowed
+constexpr unsigned long long kOvUnionFind = 8ull;  // a union-find loop hit its bound (dm_uf.h)
 // Integrate counters, zeroed by each integrate call; the others belong to the
 // frontier pass, which may still be running when the next call's front-end
 // starts (dm_set_overlap), so the integrate reset never touches them.
@@ -170,7 +173,14 @@ struct dm_grid {
   int64_t trig_cap = 0;
   double* pose4 = nullptr; int64_t pose_cap = 0;
   float* ranges = nullptr; int64_t ranges_cap = 0;
-  double* h_pose4 = nullptr; int64_t h_pose_cap = 0;  // pinned
+  // pinned (x, y, cos, sin) staging of host poses: a ring of two, each
+  // reusable once the H2D copy that read it is done (ev_pose), so a host-input
+  // call never waits for the previous call (dm_integrate_async)
+  static constexpr int kPoseRing = 2;
+  double* h_pose4[kPoseRing] = {nullptr, nullptr};
+  hipEvent_t ev_pose[kPoseRing] = {nullptr, nullptr};
+  int64_t h_pose_cap = 0;
+  int pose_head = 0;
   int32_t last_S = 0, last_N = 0;
 
   // frontier workspace

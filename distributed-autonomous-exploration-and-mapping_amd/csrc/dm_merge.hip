@@ -60,7 +60,8 @@ __global__ __launch_bounds__(256) void k_export(ExportView v, int64_t row0, int6
                                                 uint8_t* __restrict__ exp) {
   const int64_t K = (int64_t)cnt[CNT_CLUSTERS];
   long long flags = 0;
-  if (cnt[CNT_OVERFLOW] & 4ull) flags |= 1;
+  if (cnt[CNT_OVERFLOW] & kOvSlots) flags |= 1;
+  if (cnt[CNT_OVERFLOW] & kOvUnionFind) flags |= 32;
   if (K > v.rec_cap) flags |= 2;
   if (!cnt[CNT_SORTED]) flags |= 4;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -141,7 +142,8 @@ __global__ __launch_bounds__(256) void k_merge_init(MGeom m, const uint8_t* __re
 // A lane skips the pairs its predecessor lane (cell x-1) already issued: a
 // frontier crossing the edge repeats the same pair over consecutive cells.
 __global__ __launch_bounds__(256) void k_merge_pairs(MGeom m, const uint8_t* __restrict__ gat,
-                                                     int32_t* parent, const long long* __restrict__ label) {
+                                                     int32_t* parent, const long long* __restrict__ label,
+                                                     unsigned long long* mcnt) {
   const int64_t W = m.v.W;
   const int64_t n = (int64_t)(m.P - 1) * W;
   const int lane = __lane_id();
@@ -176,21 +178,21 @@ __global__ __launch_bounds__(256) void k_merge_pairs(MGeom m, const uint8_t* __r
       bool dup = false;
       for (int r = 0; r < q; ++r) dup |= c[r] == bb;
       if (has_prev && pa == a) dup |= (pc[0] == bb) | (pc[1] == bb) | (pc[2] == bb);
-      if (!dup) dm_uf_unite(parent, label, a, bb);
+      if (!dup) dm_uf_unite(parent, label, a, bb, &mcnt[M_FLAGS], 32ull);
     }
   }
 }
 
 __global__ __launch_bounds__(256) void k_merge_resolve(MGeom m, const uint8_t* __restrict__ gat,
                                                        const int32_t* __restrict__ parent,
-                                                       long long* acc) {
+                                                       long long* acc, unsigned long long* mcnt) {
   const int64_t n = (int64_t)m.P * m.v.rec_cap;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int r = (int)(i / m.v.rec_cap);
     const int64_t k = i - (int64_t)r * m.v.rec_cap;
     if (k >= band_k(gat, m, r)) continue;
-    const int32_t root = dm_uf_root(parent, (int32_t)i);
+    const int32_t root = dm_uf_root(parent, (int32_t)i, &mcnt[M_FLAGS], 32ull);
     if (root == (int32_t)i) continue;
     const long long* rc = rec_of(gat, m.v, r) + 4 * k;
     atomicAdd((unsigned long long*)&acc[3 * (int64_t)root + 0], (unsigned long long)rc[1]);
@@ -277,10 +279,11 @@ int dm_launch_merge(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t 
   DM_HIP(hipGetLastError());
   if (nranks > 1) {
     hipLaunchKernelGGL(k_merge_pairs, dim3(grid_for((int64_t)(nranks - 1) * g->W, 256, 1024)), dim3(256), 0,
-                       g->stream, m, gat, g->m_parent, g->m_label);
+                       g->stream, m, gat, g->m_parent, g->m_label, g->m_cnt);
     DM_HIP(hipGetLastError());
   }
-  hipLaunchKernelGGL(k_merge_resolve, dim3(eg), dim3(256), 0, g->stream, m, gat, g->m_parent, g->m_acc);
+  hipLaunchKernelGGL(k_merge_resolve, dim3(eg), dim3(256), 0, g->stream, m, gat, g->m_parent, g->m_acc,
+                     g->m_cnt);
   DM_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_merge_compact, dim3(eg), dim3(256), 0, g->stream, m, gat, g->m_parent, g->m_label,
                      g->m_acc, g->m_clu, g->m_cnt);

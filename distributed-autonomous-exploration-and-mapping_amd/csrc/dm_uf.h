@@ -7,10 +7,18 @@
 // not depend on the order in which unions land.  Hooks are CAS at the
 // device-coherent point (per-XCD L2s are not coherent; MI355X_MICROARCH.md
 // §Workgroup dispatch); reads are relaxed agent-scope loads (below).
+//
+// Every loop is bounded.  A loop that runs out of iterations (a chain longer
+// than the bound, or a corrupted parent array) does not return a silently
+// wrong node: it sets `bit` in *flag (a counter word the readback checks:
+// CNT_OVERFLOW / M_FLAGS), and the host turns that into DM_ERR_INCOMPLETE.
 #pragma once
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+constexpr int kUfFindBound = 1 << 22;
+constexpr int kUfUniteBound = 1 << 20;
 
 // Reads of parent[] are relaxed agent-scope loads (global_load sc1: past
 // the CU's L1, served by the XCD's L2), not atomic RMWs: a find costs one
@@ -24,39 +32,49 @@ __device__ inline int32_t dm_uf_load(const int32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ inline int32_t dm_uf_find(const int32_t* par, int32_t x) {
-  for (int it = 0; it < (1 << 22); ++it) {
+__device__ inline void dm_uf_flag(unsigned long long* flag, unsigned long long bit) {
+  if (flag) atomicOr(flag, bit);
+}
+
+__device__ inline int32_t dm_uf_find(const int32_t* par, int32_t x, unsigned long long* flag,
+                                     unsigned long long bit) {
+  for (int it = 0; it < kUfFindBound; ++it) {
     const int32_t p = dm_uf_load(par + x);
     if (p == x) return x;
     x = p;
   }
+  dm_uf_flag(flag, bit);
   return x;
 }
 
 // Lock-free union: hook the root with the larger label under the other.
 // Two nodes found in the same set stay in it (sets only merge), so a == b
 // is final even from stale reads.
-__device__ inline void dm_uf_unite(int32_t* par, const long long* label, int32_t a, int32_t b) {
-  for (int it = 0; it < (1 << 20); ++it) {
-    a = dm_uf_find(par, a);
-    b = dm_uf_find(par, b);
+__device__ inline void dm_uf_unite(int32_t* par, const long long* label, int32_t a, int32_t b,
+                                   unsigned long long* flag, unsigned long long bit) {
+  for (int it = 0; it < kUfUniteBound; ++it) {
+    a = dm_uf_find(par, a, flag, bit);
+    b = dm_uf_find(par, b, flag, bit);
     if (a == b) return;
     if (label[a] < label[b]) { const int32_t t = a; a = b; b = t; }
     const int32_t old = atomicCAS(&par[a], a, b);
     if (old == a) return;
     // a was hooked meanwhile (or read stale): continue from its real parent
     a = old;
-    b = dm_uf_find(par, b);
+    b = dm_uf_find(par, b, flag, bit);
     if (a == b) return;
   }
+  dm_uf_flag(flag, bit);
 }
 
 // Plain (non-atomic) find for kernels that run after every union landed.
-__device__ inline int32_t dm_uf_root(const int32_t* par, int32_t x) {
-  for (int it = 0; it < (1 << 22); ++it) {
+__device__ inline int32_t dm_uf_root(const int32_t* par, int32_t x, unsigned long long* flag,
+                                     unsigned long long bit) {
+  for (int it = 0; it < kUfFindBound; ++it) {
     const int32_t p = par[x];
-    if (p == x) break;
+    if (p == x) return x;
     x = p;
   }
+  dm_uf_flag(flag, bit);
   return x;
 }

@@ -9,7 +9,7 @@ in hand-written HIP kernels for gfx950 behind the C-ABI in include/dm.h
 """
 from ._ffi import (CLUSTER_DTYPE, DM_TILE, DmCluster, DmError, DmParams, exported_symbols,
                    load_library)
-from .grid import Frontiers, OccupancyMapper, default_params, params_from_dict
+from .grid import Frontiers, OccupancyMapper, atomic_peak, default_params, params_from_dict
 
 __all__ = [
     "CLUSTER_DTYPE",
@@ -19,6 +19,7 @@ __all__ = [
     "DmParams",
     "Frontiers",
     "OccupancyMapper",
+    "atomic_peak",
     "default_params",
     "exported_symbols",
     "load_library",

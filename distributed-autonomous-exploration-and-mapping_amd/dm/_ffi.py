@@ -129,6 +129,7 @@ SIGNATURES = {
     "dm_get_params": [_vp, ctypes.POINTER(DmParams)],
     "dm_integrate": [_vp, _i32, _vp, _i32, _vp, _f32, _f32, _vp, _vp],
     "dm_integrate_device": [_vp, _i32, _vp, _i32, _vp, _f32, _f32],
+    "dm_integrate_async": [_vp, _i32, _vp, _i32, _vp, _f32, _f32],
     "dm_last_counts": [_vp, _vp, _vp],
     "dm_last_stats": [_vp, _vp, _i32, ctypes.POINTER(_i32)],
     "dm_get_state": [_vp, _vp],
@@ -159,6 +160,7 @@ SIGNATURES = {
     "dm_frontiers_begin": [_vp],
     "dm_frontiers_end": [_vp, _vp, _i64, ctypes.POINTER(_i64)],
     "dm_set_overlap": [_vp, _i32],
+    "dm_atomic_peak": [ctypes.c_int, _vp, _i32, ctypes.POINTER(_i32)],
 }
 # functions returning const char*
 STRING_FUNCS = ("dm_last_error", "dm_version")

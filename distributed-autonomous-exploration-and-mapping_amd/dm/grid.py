@@ -49,6 +49,16 @@ def params_from_dict(d: dict) -> DmParams:
     return p
 
 
+def atomic_peak(device: int = 0) -> dict:
+    """Measured uncontended atomic throughput of the device (dm_atomic_peak):
+    LDS ds_add_u32 and global no-return atomicAdd u32, operations per second."""
+    lib = load_library()
+    out = (ctypes.c_double * 2)()
+    n = ctypes.c_int32(0)
+    check(lib.dm_atomic_peak(int(device), out, 2, ctypes.byref(n)))
+    return {"lds_add_u32_per_s": float(out[0]), "global_add_u32_per_s": float(out[1])}
+
+
 @dataclass
 class Frontiers:
     """Result of one frontier extraction."""
@@ -129,6 +139,19 @@ class OccupancyMapper:
         ranges = np.asarray(scan.ranges, dtype=np.float32)[None, :]
         return self.integrate(np.asarray(pose, np.float64)[None, :], ranges,
                               np.float32(scan.angle_min), np.float32(scan.angle_increment))
+
+    def integrate_async(self, poses, ranges_ptr: int, S: int, N: int, angle_min, angle_increment):
+        """dm_integrate_async: poses [S,3] (read now), ranges a host pointer to
+        float32 [S,N] — pinned memory for a truly asynchronous upload — that
+        must stay valid until the second integrate_async call after this one
+        (or synchronize()).  Returns at once; U/T via last_counts()."""
+        poses = np.ascontiguousarray(poses, dtype=np.float64).reshape(-1, 3)
+        if poses.shape[0] != S:
+            raise DmError(_ffi.DM_ERR_SHAPE, f"poses has {poses.shape[0]} rows, S = {S}")
+        with self._lock:
+            check(self._lib.dm_integrate_async(self._handle(), int(S), _vp(poses), int(N),
+                                               ctypes.c_void_p(ranges_ptr), float(angle_min),
+                                               float(angle_increment)))
 
     def integrate_device(self, d_pose4_ptr: int, S: int, d_ranges_ptr: int, N: int,
                          angle_min, angle_increment):

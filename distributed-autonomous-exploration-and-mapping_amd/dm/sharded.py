@@ -263,22 +263,29 @@ class ShardedMapper:
             self._gather_dev(exp, gexp)
             return gexp
 
-    def _device_finish(self, result) -> Frontiers:
+    def _device_finish(self, result) -> Frontiers | None:
+        """Frontiers from a device merge result, or None when a band's export
+        record was incomplete (every rank merged the same gathered headers, so
+        all ranks see that together).  The record capacity is grown for the
+        next pass; the caller decides what to rerun (frontiers() falls back to
+        the host exchange on the map as it is now, frontiers_end() returns None
+        because a rerun would describe a later map than the pass it collects)."""
         clusters, max_k = result
         if clusters is not None:
             return Frontiers(clusters=clusters)
-        # a band's record was incomplete; every rank merged the same gathered
-        # headers, so all ranks take this branch together
         self.fallbacks += 1
         while self.rec_cap < max_k:
             self.rec_cap *= 2
-        return self._frontiers_host(False, False)
+        return None
 
     def _frontiers_device(self):
         gexp = self._device_enqueue()
         with self._torch.cuda.stream(self.stream):
             res = self.band.merge_bands(gexp.data_ptr(), self.world_size, self.rec_cap, self.min_size)
-        return self._device_finish(res)
+        fr = self._device_finish(res)
+        # incomplete record (capacity grown now): this call is synchronous, so
+        # the host exchange over the map as it is now is the same map
+        return fr if fr is not None else self._frontiers_host(False, False)
 
     def frontiers(self, want_mask=False, want_labels=False) -> Frontiers:
         """Frontiers of the map as it is now (synchronous; passes started with
@@ -314,13 +321,16 @@ class ShardedMapper:
         else:  # host exchange (or a non-libdm band): computed now
             self._pending.append(("done", self.frontiers()))
 
-    def frontiers_end(self) -> Frontiers:
-        """Clusters of the oldest pass started with frontiers_begin()."""
+    def frontiers_end(self) -> Frontiers | None:
+        """Clusters of the oldest pass started with frontiers_begin(), exactly
+        as frontiers() would have returned them when the pass started; None if
+        that pass has no result (the library's slot arrays or a band's export
+        record overflowed: capacities are grown now).  A None pass is not
+        recomputed here — the map may have changed since it started; call
+        frontiers() for the map as it is now."""
         kind, res = self._pending.popleft()
         if kind == "band":
-            fr = self.band.frontiers_end()
-            # slot overflow (workspace grown): rerun on the map as it is now
-            return fr if fr is not None else self.band.frontiers()
+            return self.band.frontiers_end()
         if kind == "merge":
             return self._device_finish(self.band.merge_bands_end())
         return res

@@ -212,6 +212,54 @@ def config_world(cfg: str, seed: int = 0):
     return world, n, n, res, -half, -half
 
 
+def explored_state(world: World, W: int, H: int, res: float, ox: float, oy: float, seed: int = 0,
+                   row0: int = 0, rows: int | None = None, unknown_frac: float = 0.08,
+                   r_lo: float = 0.5, r_hi: float = 6.0) -> np.ndarray:
+    """Rows [row0, row0 + rows) of a mostly explored map (OccupancyGrid.data
+    encoding, int8 [rows, W]): free space; every obstacle of `world` as an
+    occupied outline around an unobserved (unknown) interior, as a scanner
+    sees it; unexplored pockets (shadows behind obstacles, rooms not yet
+    entered) as unknown discs of radius r_lo..r_hi metres covering about
+    `unknown_frac` of the area.  Nearly every 64x64 tile holds free cells and
+    the pocket rims are frontiers: the frontier pass's worst case (every tile
+    read), as get_map_image (main.py:251-263) sees a map late in a run.
+    Seeded and independent of the row window, so bands of one map agree."""
+    rows = H - row0 if rows is None else rows
+    st = np.zeros((rows, W), np.int8)
+
+    def cells(x0, y0, x1, y1):
+        return (int(math.floor((x0 - ox) / res)), int(math.floor((y0 - oy) / res)),
+                int(math.floor((x1 - ox) / res)), int(math.floor((y1 - oy) / res)))
+
+    for x0, y0, x1, y1 in world.rects:
+        cx0, cy0, cx1, cy1 = cells(x0, y0, x1, y1)
+        cx0, cx1 = max(cx0, 0), min(cx1, W - 1)
+        ya, yb = max(cy0, row0), min(cy1, row0 + rows - 1)
+        if cx0 > cx1 or ya > yb:
+            continue
+        st[ya - row0:yb - row0 + 1, cx0:cx1 + 1] = 100
+        ia, ib = max(cy0 + 1, row0), min(cy1 - 1, row0 + rows - 1)
+        if cx1 - cx0 >= 2 and ia <= ib:
+            st[ia - row0:ib - row0 + 1, cx0 + 1:cx1] = -1
+    rng = np.random.Generator(np.random.PCG64(seed))
+    area = W * H * res * res
+    mean_r2 = (r_hi ** 3 - r_lo ** 3) / (3.0 * (r_hi - r_lo))
+    n = int(round(unknown_frac * area / (math.pi * mean_r2)))
+    cxs = rng.uniform(0, W, n)
+    cys = rng.uniform(0, H, n)
+    rads = rng.uniform(r_lo, r_hi, n) / res
+    for cx, cy, rr in zip(cxs, cys, rads):
+        ya, yb = max(int(cy - rr), row0), min(int(cy + rr) + 1, row0 + rows - 1)
+        xa, xb = max(int(cx - rr), 0), min(int(cx + rr) + 1, W - 1)
+        if ya > yb or xa > xb:
+            continue
+        yy = np.arange(ya, yb + 1)[:, None] + 0.5 - cy
+        xx = np.arange(xa, xb + 1)[None, :] + 0.5 - cx
+        sub = st[ya - row0:yb - row0 + 1, xa:xb + 1]
+        sub[(yy * yy + xx * xx <= rr * rr) & (sub == 0)] = -1
+    return st
+
+
 def pose4(poses: np.ndarray) -> np.ndarray:
     """(x, y, yaw) -> (x, y, cos yaw, sin yaw) with the C library's cos/sin
     (math.cos), the device-resident pose format of dm_integrate_device."""

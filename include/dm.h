@@ -46,7 +46,8 @@ extern "C" {
 #define DM_ERR_CAPACITY (-5)
 #define DM_ERR_IO (-6)
 #define DM_ERR_STATE (-7)
-#define DM_ERR_INCOMPLETE (-8) /* a band's export record was incomplete (dm_merge_bands) */
+#define DM_ERR_INCOMPLETE (-8) /* a pass has no result: an export record was incomplete, or a
+                                  union-find loop hit its iteration bound */
 
 /* Tile edge (cells) used by the kernels; band_row0 must be a multiple of it. */
 #define DM_TILE 64
@@ -118,6 +119,18 @@ int dm_get_params(const dm_grid* g, dm_params* out);
 int dm_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N,
                  const float* ranges, float angle_min, float angle_increment,
                  uint64_t* out_updates, uint64_t* out_touched);
+
+/* Asynchronous host-input variant of dm_integrate: the same inputs (host
+ * pointers), enqueued and not waited for — the H2D copies of poses and
+ * ranges run on the library's streams and, when `ranges` is pinned host
+ * memory (hipHostMalloc / torch pin_memory), overlap work in flight (with
+ * dm_set_overlap: the previous frontier pass).  `ranges` must stay valid and
+ * unchanged until the copy is done: until the second dm_integrate_async call
+ * after this one returns, or dm_synchronize / dm_last_counts.  `poses` is
+ * read before the call returns.  Read U and T with dm_last_counts.  This is
+ * the PCIe-inclusive form of the ROS node's per-scan call. */
+int dm_integrate_async(dm_grid* g, int32_t S, const double* poses, int32_t N,
+                       const float* ranges, float angle_min, float angle_increment);
 
 /* Device-resident variant (asynchronous on the handle's stream).
  * d_pose4: [S][4] = (x, y, cos(yaw), sin(yaw)) doubles in device memory;
@@ -202,7 +215,8 @@ int dm_get_edge_labels(dm_grid* g, int64_t* first_row, int64_t* last_row);
  * dm_export_bytes bytes):
  *   int64 hdr[8]  K (band clusters), flags (0 = complete; bit0 slot overflow,
  *                 bit1 K > rec_cap, bit2 too many clusters to sort on the
- *                 device), band_row0, band_rows, width, 0, 0, 0
+ *                 device, bit5 union-find iteration bound hit), band_row0,
+ *                 band_rows, width, 0, 0, 0
  *   int32 edge[2][width]  component of each cell of the band's first / last
  *                 row as an index into rec[], -1 off-frontier
  *   int64 rec[rec_cap][4] (label, size, sum_x, sum_y), sorted by label;
@@ -266,6 +280,16 @@ int dm_profile_reset(dm_grid* g);
  * 0 -> 255, 100 -> 0, anything else -> 127, rows flipped (flipud).
  * out: uint8[band_rows*width]. */
 int dm_map_image(dm_grid* g, uint8_t* out);
+
+/* Measured uncontended atomic throughput of HIP device `device` (the
+ * north star's "atomic throughput against MI355X peak": no vendor figure
+ * exists for integer atomics, so the peak is measured in-harness,
+ * csrc/dm_probe.hip).  out[0] = LDS ds_add_u32 per second (every lane its own
+ * bank: the form k_tile_accum's per-cell counts take), out[1] = global
+ * no-return atomicAdd u32 per second (256 contiguous bytes per wave
+ * instruction, rows over a 256 MiB buffer: the heavy tiles' slab adds).
+ * Runs a few milliseconds of probe kernels on a private stream. */
+int dm_atomic_peak(int device, double* out, int32_t cap, int32_t* n_out);
 
 const char* dm_last_error(void);
 const char* dm_version(void);

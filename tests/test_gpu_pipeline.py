@@ -178,3 +178,34 @@ def test_merge_bands_begin_end_matches_sync(P, W, H, seed):
     finally:
         for b in bands:
             b.close()
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_async_host_inputs_pipelined(oracle_lib, overlap):
+    """dm_integrate_async from pinned host buffers (the PCIe-inclusive form of
+    the bench step): each call is enqueued without waiting, its ranges buffer
+    reused only two calls later; every pipelined pass equals the oracle's
+    frontiers after its own batch and the final map is bit-exact."""
+    import torch
+
+    p, batches, amin, inc = cases.world_case(49, 1200, 1100, 0.05, 6, 1024, 7, region_frac=0.6)
+    om, expect = _oracle_steps(oracle_lib, p, batches, amin, inc)
+    S, N = batches[0][1].shape
+    pinned = [torch.empty((S, N), dtype=torch.float32).pin_memory() for _ in range(2)]
+    with dm.OccupancyMapper(p) as m:
+        m.set_overlap(overlap)
+        got = []
+        for k, (poses, ranges) in enumerate(batches):
+            buf = pinned[k % 2]  # free again: its copy was two calls ago
+            buf.numpy()[...] = ranges
+            m.integrate_async(poses, buf.data_ptr(), S, N, amin, inc)
+            if k > 0:
+                got.append(m.frontiers_end())
+            m.frontiers_begin()
+        got.append(m.frontiers_end())
+        for k, fr in enumerate(got):
+            assert fr is not None
+            np.testing.assert_array_equal(fr.clusters, expect[k])
+        assert_map_equal(m, om)
+        om2 = oracle_lib.OracleMap(p)
+        assert m.last_counts() == om2.integrate(*batches[-1], amin, inc)  # U, T of the last call

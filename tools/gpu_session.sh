@@ -1,33 +1,57 @@
 #!/bin/bash
-# One GPU-box session: parity tests -> bench (with CPU baseline) -> 2-rank
-# sharded rehearsal (gloo, both ranks on GPU 0) -> rocprofv3 kernel stats ->
-# PMC passes.  Stops at the first step that crashes, aborts or times out.
-# Usage: bash tools/gpu_session.sh [tests|bench|shard|prof|pmc]...  (default: all)
+# One GPU-box session, steps run in order, stopping at the first step that
+# crashes, aborts or times out (each step under its own time limit).
+# Usage: bash tools/gpu_session.sh STEP...   (from the repo root)
+#   tests         pytest -m gpu
+#   tests:EXPR    pytest -m gpu -k EXPR
+#   bench         python bench.py (the driver's command, with CPU baseline)
+#   shard         2-rank sharded bench rehearsal (gloo, both ranks on GPU 0)
+#   prof          rocprofv3 --kernel-trace --stats over a bench run
+#   probe         rocprofv3 --kernel-trace --stats over tools/frontier_probe.py (explored map)
+#   pmc           PMC passes over a short C3 bench -> profiles/pmc_latest.json [C3]
+#   pmcx          PMC passes over the explored-map probe -> [C3-explored]
+#   cfg:CN        bench.py --config CN
 set -o pipefail
 R=$PWD
 OUT=$R/gpurun_out
 mkdir -p $OUT
-steps="${@:-tests bench shard prof pmc}"
 ok() { [ "$1" -eq 0 ]; }
-for s in $steps; do
+for s in "$@"; do
   case $s in
-    tests)
-      timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
-      rc=$?; echo "tests rc=$rc"; grep -E "FAILED|passed|failed" $OUT/pytest_gpu.log | tail -6
-      [ $rc -le 1 ] || exit $rc ;;
+    tests|tests:*)
+      k=""; [ "$s" != tests ] && k="-k ${s#tests:}"
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v $k --timeout 400 --timeout-method thread \
+        > $OUT/pytest_gpu.log 2>&1
+      rc=$?; echo "tests rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $OUT/pytest_gpu.log | tail -8
+      ok $rc || exit $rc ;;
     bench)
       timeout -k 10 400 python -u bench.py > $OUT/bench.log 2>&1
-      rc=$?; echo "bench rc=$rc"; tail -1 $OUT/bench.log; ok $rc || exit $rc ;;
+      rc=$?; echo "bench rc=$rc"; tail -1 $OUT/bench.log | cut -c1-600; ok $rc || exit $rc ;;
     shard)
       timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --backend gloo --device-override 0 \
         --cpu-seconds 0 --pool 3 > $OUT/shard.log 2>&1
-      rc=$?; echo "shard rc=$rc"; tail -1 $OUT/shard.log; ok $rc || exit $rc ;;
+      rc=$?; echo "shard rc=$rc"; tail -1 $OUT/shard.log | cut -c1-300; ok $rc || exit $rc ;;
     prof)
-      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run \
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run \
         --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 --cpu-seconds 0 > $OUT/prof.log 2>&1)
       rc=$?; echo "prof rc=$rc"; ok $rc || exit $rc ;;
+    probe)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/probe -o run \
+        --output-format csv -- python3 $R/tools/frontier_probe.py > $OUT/probe.log 2>&1)
+      rc=$?; echo "probe rc=$rc"; tail -1 $OUT/probe.log | cut -c1-400; ok $rc || exit $rc ;;
     pmc)
-      bash $R/tools/pmc_passes.sh gpurun_out/pmc; rc=$?; ok $rc || exit $rc ;;
+      bash $R/tools/pmc_passes.sh gpurun_out/pmc; rc=$?; ok $rc || exit $rc
+      python $R/tools/pmc_summary.py $OUT/pmc $R/profiles/pmc_latest.json C3 > $OUT/pmc_summary.log 2>&1 || exit 1
+      cp $R/profiles/pmc_latest.json $OUT/pmc_latest.json ;;
+    pmcx)
+      bash $R/tools/pmc_passes.sh gpurun_out/pmcx python3 $R/tools/frontier_probe.py --passes 5; rc=$?; ok $rc || exit $rc
+      python $R/tools/pmc_summary.py $OUT/pmcx $R/profiles/pmc_latest.json C3-explored > $OUT/pmcx_summary.log 2>&1 || exit 1
+      cp $R/profiles/pmc_latest.json $OUT/pmc_latest.json ;;
+    cfg:*)
+      c=${s#cfg:}
+      timeout -k 10 400 python -u bench.py --config $c --cpu-seconds 10 > $OUT/bench_$c.log 2>&1
+      rc=$?; echo "$c rc=$rc"; tail -1 $OUT/bench_$c.log | cut -c1-300; ok $rc || exit $rc ;;
+    *) echo "unknown step $s"; exit 2 ;;
   esac
 done
