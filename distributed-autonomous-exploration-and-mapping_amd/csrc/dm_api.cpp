@@ -412,7 +412,10 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if ((rc = dev_alloc(&g->ish, 2 * kShards * kShardWords, "shard counters"))) return fail(rc);
   g->fsh = g->ish + kShards * kShardWords;
   if ((rc = dev_alloc(&g->ftiles, g->NT, "frontier tiles"))) return fail(rc);
+  if ((rc = dev_alloc(&g->big_tiles, g->NT, "frontier big tiles"))) return fail(rc);
   if ((rc = dev_alloc(&g->border, g->NT * 256, "frontier borders"))) return fail(rc);
+  if ((rc = dev_alloc(&g->rel, 4 * g->NT, "tile-edge hand-off words"))) return fail(rc);
+  DM_HIP(hipMemset(g->rel, 0, sizeof(unsigned long long) * 4 * (size_t)g->NT));
   if ((rc = dev_alloc(&g->edge_slot, 2 * g->W, "edge slots"))) return fail(rc);
   if ((rc = dev_alloc(&g->edge_label, 2 * g->W, "edge labels"))) return fail(rc);
   if ((rc = dev_alloc(&g->halo, 2 * g->W, "halo rows"))) return fail(rc);
@@ -479,7 +482,7 @@ int dm_destroy(dm_grid* g) {
   dev_free(g->hitems); dev_free(g->litems); dev_free(g->heavy_list); dev_free(g->slabs); dev_free(g->heavy_done);
   dev_free(g->pose4); dev_free(g->ranges); 
   dev_free(g->bs_rows); dev_free(g->bs_key); dev_free(g->bs_idx);
-  dev_free(g->border); dev_free(g->ftiles); dev_free(g->slot_label); dev_free(g->slot_parent); dev_free(g->slot_root);
+  dev_free(g->border); dev_free(g->rel); dev_free(g->ftiles); dev_free(g->big_tiles); dev_free(g->slot_label); dev_free(g->slot_parent); dev_free(g->slot_root);
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
   dev_free(g->edge_slot); dev_free(g->edge_label); dev_free(g->mask); dev_free(g->labels);
   dev_free(g->halo); dev_free(g->ish); dev_free(g->act_raw);

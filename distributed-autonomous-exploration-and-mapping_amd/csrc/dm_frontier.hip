@@ -16,10 +16,12 @@
 //   k_frontier_tile one workgroup per listed tile: state tile + 1-cell halo
 //                   in LDS, frontier test, LDS union-find (atomicMin hooking,
 //                   root = min index), per-component sums, one slot per
-//                   tile-local component, border slot ids
-//   k_frontier_merge unions slots across tile borders (8-connectivity),
-//                   lock-free CAS union-find keyed by label
-//   k_frontier_resolve / k_frontier_compact  roots, int64 sums, cluster list
+//                   tile-local component; then the unions across its edges
+//                   with the neighbour tiles that finished before it (the
+//                   later tile of each edge unites: a stamped hand-off word
+//                   per tile pair), lock-free CAS union-find keyed by slot
+//   k_frontier_resolve / k_frontier_compact  roots, int64 sums and the min
+//                   label of each merged set, cluster list
 #include "dm_internal.h"
 #include "dm_uf.h"
 #include "dm_phase.h"
@@ -64,14 +66,20 @@ __global__ __launch_bounds__(256) void k_frontier_prep(int64_t NT, const int32_t
                                                        unsigned long long* list_n,
                                                        unsigned long long* other_n, int64_t n_edge,
                                                        unsigned long long* cnt, unsigned long long* fsh,
-                                                       int32_t* __restrict__ edge_slot) {
+                                                       int32_t* __restrict__ edge_slot,
+                                                       int32_t* __restrict__ slot_parent, int64_t slot_cap) {
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int lane = __lane_id();
   if (i0 < 3) cnt[CNT_SLOTS + i0] = 0ull;  // slots, clusters, overflow
+  if (i0 == 3) cnt[CNT_BIG] = 0ull;
   if (i0 == 0) *other_n = 0ull;
   if (i0 < kShards * kShardWords) fsh[i0] = 0ull;
   for (int64_t i = i0; i < n_edge; i += stride) edge_slot[i] = -1;
+  // every slot starts as its own root here, a launch ahead of the tile
+  // kernel's in-kernel unions: their CASes and (possibly stale, L2-served)
+  // finds then only ever see a slot as a root or as hooked (dm_uf.h)
+  for (int64_t i = i0; i < slot_cap; i += stride) slot_parent[i] = (int32_t)i;
   // ballot compaction, one list_n atomic per workgroup and round (the
   // loop bound is uniform within the workgroup: its barriers are safe)
   __shared__ int32_t s_wn[4];
@@ -209,11 +217,11 @@ __device__ inline void tile_issue(const FGeom& g, const int8_t* __restrict__ sta
 //     first run, whose first cell is the component's min linear index);
 //  4. per-component sums from run lengths, one slot per component, border
 //     slot ids for k_frontier_merge.
-__global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile(
+__global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
     FGeom g, const int8_t* __restrict__ state, const int8_t* __restrict__ halo,
     const int32_t* __restrict__ ftiles, const unsigned long long* __restrict__ list_n,
-    int32_t* __restrict__ border,
-    long long* __restrict__ slot_label, int32_t* __restrict__ slot_parent,
+    int32_t* border, unsigned long long* rel, unsigned long long stamp,
+    long long* __restrict__ slot_label, int32_t* slot_parent,
     long long* __restrict__ slot_own, long long* __restrict__ slot_acc,
     uint8_t* __restrict__ mask, int32_t* __restrict__ cell_slot, int32_t* __restrict__ edge_slot,
     unsigned long long* cnt, unsigned long long* fsh) {
@@ -322,8 +330,7 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile(
     }
     any = __syncthreads_or(any);
     DM_PH(dm_phase_acc_frontier, 1);
-    if (!any) {
-      border[j * 256 + tid] = -1;
+    if (!any) {  // nothing to publish: the neighbours never read this tile's edges
       __syncthreads();
       DM_PH(dm_phase_acc_frontier, 8);
       continue;
@@ -423,24 +430,111 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile(
       const long long gx = (long long)tx0 + r_s[r];
       const uint32_t zx = szx[c];
       const long long sz = zx >> 18;
-      slot_label[slot] = gy * g.W + gx;
-      slot_parent[slot] = (int32_t)slot;
+      slot_label[slot] = gy * g.W + gx;  // (slot_parent[slot] == slot since k_frontier_prep)
       const long long sx = sz * tx0 + (zx & 0x3FFFFu);
       const long long sy = sz * ((long long)g.row0 + ty0) + ssy[c];
       slot_own[3 * slot + 0] = sz; slot_own[3 * slot + 1] = sx; slot_own[3 * slot + 2] = sy;
       slot_acc[3 * slot + 0] = sz; slot_acc[3 * slot + 1] = sx; slot_acc[3 * slot + 2] = sy;
     }
-    // border slots: [0] first row, [1] last row, [2] first col, [3] last col
+    // ---- 5. unions across the tile's edges -------------------------------------
+    // Wave w owns edge w ([0] first row, [1] last row, [2] first col, [3]
+    // last col; lane = position along it) and the slot of its lane's cell.
+    // For each neighbour relation (the edge, and for waves 0/1 the two
+    // corners of the row) the tile arrives at the pair's hand-off word
+    // (rel: stamp << 2 | arrived sides, one 64-bit atomic max per arrival);
+    // the tile that arrives second finds the other's side bit and performs
+    // the pair's unions, reading the first tile's published edge.  A tile
+    // arrives only at relations whose cells on its side hold frontier cells,
+    // so a pair without frontier cells on both sides is never united, and a
+    // pair is united by exactly one of its tiles (memory-side atomics
+    // serialise the two arrivals).  Publication (MI355X_MICROARCH.md,
+    // inter-workgroup visibility, hand-off row 1): the edge's slot ids are
+    // written with sc1 stores by the wave that then arrives, after its own
+    // s_waitcnt vmcnt(0); the second tile reads them with sc1 loads after its
+    // arrival returned.  Unions are keyed by slot index (dm_uf_unite_idx);
+    // k_frontier_resolve folds each set's min label into its root.
     {
-      const int side = tid >> 6, pos = tid & 63;
+      const int side = tid >> 6, pos = lane;
       const int y = side == 0 ? 0 : side == 1 ? 63 : pos;
       const int x = side == 0 || side == 1 ? pos : side == 2 ? 0 : 63;
-      long long sl = -1;
+      int32_t sl = -1;
       if ((s_F[y] >> x) & 1ull) {
-        sl = base + root_rank(s_root, s_rootpre, r_par[run_of(s_rbase, s_F, y, x)]);
-        sl = sl < g.slot_per ? sh0 + sl : -1;
+        const long long v = base + root_rank(s_root, s_rootpre, r_par[run_of(s_rbase, s_F, y, x)]);
+        sl = v < g.slot_per ? (int32_t)(sh0 + v) : -1;
       }
-      border[j * 256 + tid] = (int32_t)sl;
+      const uint64_t fb = __ballot(sl >= 0);
+      if (fb) {
+        __hip_atomic_store(&border[j * 256 + tid], sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int32_t tx = tile % g.TX, ty = tile / g.TX;
+        const bool up = ty > 0, down = ty + 1 < g.TY, left = tx > 0, right = tx + 1 < g.TX;
+        // this lane's relation: lane 0 the edge, lanes 1 / 2 the row's corners
+        // at x = 0 / x = 63; (pair word, my side bit, neighbour tile)
+        int64_t e = -1;
+        unsigned long long mine = 0;
+        int32_t nb = -1;
+        const int64_t NT = g.NT;
+        if (lane == 0) {
+          if (side == 0 && up) { e = NT + tile - g.TX; mine = 2; nb = tile - g.TX; }
+          if (side == 1 && down) { e = NT + tile; mine = 1; nb = tile + g.TX; }
+          if (side == 2 && left) { e = tile - 1; mine = 2; nb = tile - 1; }
+          if (side == 3 && right) { e = tile; mine = 1; nb = tile + 1; }
+        } else if (lane == 1 && (fb & 1ull)) {        // corner x = 0
+          if (side == 0 && up && left) { e = 2 * NT + tile - g.TX - 1; mine = 2; nb = tile - g.TX - 1; }
+          if (side == 1 && down && left) { e = 3 * NT + tile; mine = 1; nb = tile + g.TX - 1; }
+        } else if (lane == 2 && (fb >> 63)) {         // corner x = 63
+          if (side == 0 && up && right) { e = 3 * NT + tile - g.TX + 1; mine = 2; nb = tile - g.TX + 1; }
+          if (side == 1 && down && right) { e = 2 * NT + tile; mine = 1; nb = tile + g.TX + 1; }
+        }
+        bool second = false;
+        if (e >= 0) {
+          const unsigned long long old = __hip_atomic_fetch_max(&rel[e], (stamp << 2) | mine, __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT);
+          second = (old >> 2) == stamp && (old & (3ull ^ mine)) != 0ull;
+        }
+        const uint64_t sec = __ballot(second);
+        const int32_t nb0 = __shfl(nb, 0);
+        // the edge: cell pos against the neighbour's cells pos-1, pos, pos+1
+        // on its facing edge (first row <-> last row, first col <-> last col)
+        if (sec & 1ull) {
+          const int opp = side ^ 1;
+          const int32_t v = __hip_atomic_load(&border[(int64_t)nb0 * 256 + opp * 64 + pos], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+          int32_t sb[3];
+          sb[0] = __shfl_up(v, 1);
+          sb[1] = v;
+          sb[2] = __shfl_down(v, 1);
+          if (pos == 0) sb[0] = -1;
+          if (pos == 63) sb[2] = -1;
+          // skip the pairs the previous lane (previous edge cell) issues
+          const int32_t psl = __shfl_up(sl, 1);
+          int32_t psb[3];
+          for (int q = 0; q < 3; ++q) psb[q] = __shfl_up(sb[q], 1);
+          for (int q = 0; q < 3; ++q) {
+            const int32_t b = sb[q];
+            if (sl < 0 || b < 0) continue;
+            bool dup = false;
+            for (int r = 0; r < q; ++r) dup |= sb[r] == b;
+            if (pos > 0 && psl == sl) dup |= (psb[0] == b) | (psb[1] == b) | (psb[2] == b);
+            if (!dup) dm_uf_unite_idx(slot_parent, sl, b, &cnt[CNT_OVERFLOW], kOvUnionFind);
+          }
+        }
+        // the corners: lane 1 unites cell x = 0, lane 2 cell x = 63 of the
+        // row with the diagonal neighbour's facing corner cell
+        {
+          const int32_t c0 = __shfl(sl, 0), c63 = __shfl(sl, 63);
+          if (second && lane != 0) {
+            const int32_t me = lane == 1 ? c0 : c63;
+            // the neighbour's corner cell: upper tiles' last row, lower tiles'
+            // first row, at the column facing this one
+            const int nrow = side == 0 ? 1 : 0;
+            const int ncol = lane == 1 ? 63 : 0;
+            const int32_t b = __hip_atomic_load(&border[(int64_t)nb * 256 + nrow * 64 + ncol], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+            if (me >= 0 && b >= 0) dm_uf_unite_idx(slot_parent, me, b, &cnt[CNT_OVERFLOW], kOvUnionFind);
+          }
+        }
+      }
     }
     // band edge rows (cross-band merging) and optional dense outputs
     const bool dense = g.want_mask || g.want_labels;
@@ -472,64 +566,363 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile(
   DM_PH_FLUSH(dm_phase_acc_frontier);
 }
 
-// Unions across tile borders, one wave per (listed tile, edge) — edge 0: the
-// tile's last column against its right neighbour's first column; edge 1: its
-// last row against the next tile row's first row, plus the two corners
-// (lane 63: (63,63) vs the lower-right tile's (0,0); lane 0: (0,63) vs the
-// lower-left tile's (63,0)).  The waves are independent (no workgroup
-// barrier), so every (tile, edge) of the call is in flight at once and the
-// kernel takes about one unit's chain of dependent loads.  Consecutive
-// border cells of a frontier that crosses the border usually join the same
-// two slots; a lane skips every pair its predecessor lane (the previous
-// border cell) already issued, so repeated unions do not queue same-address
-// atomics behind each other.
-__global__ __launch_bounds__(256) void k_frontier_merge(FGeom g, const int32_t* __restrict__ ftiles,
-                                                        const unsigned long long* __restrict__ list_n,
-                                                        const int32_t* __restrict__ tile_free,
-                                                        const int32_t* __restrict__ border,
-                                                        const long long* __restrict__ slot_label,
-                                                        int32_t* slot_parent,
-                                                        unsigned long long* cnt) {
-  const int lane = __lane_id();
-  const int64_t nunits = 2 * (int64_t)*list_n;
-  const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  for (int64_t u = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); u < nunits; u += waves) {
-    const int32_t tile = __builtin_amdgcn_readfirstlane(ftiles[u >> 1]);
-    const bool right = (u & 1) == 0;
-    const int32_t tx = tile % g.TX, ty = tile / g.TX;
-    const int32_t* bA = border + (int64_t)tile * 256;
-    // this lane's border cell and the neighbour tile's (independent loads)
-    const int32_t nb = right ? (tx + 1 < g.TX ? ty * g.TX + tx + 1 : -1)
-                             : (ty + 1 < g.TY ? (ty + 1) * g.TX + tx : -1);
-    const int32_t sa = bA[(right ? 3 : 1) * 64 + lane];
-    const bool nb_ok = nb >= 0 && tile_free[nb] > 0;
-    // corners (edge 1 only): lane 63 -> the lower-right tile's (0,0),
-    // lane 0 -> the lower-left tile's (63,0)
-    int32_t nc = -1, cpos = 0;
-    if (!right && ty + 1 < g.TY) {
-      if (lane == 63 && tx + 1 < g.TX) { nc = (ty + 1) * g.TX + tx + 1; cpos = 0; }
-      if (lane == 0 && tx > 0) { nc = (ty + 1) * g.TX + tx - 1; cpos = 63; }
-    }
-    const bool nc_ok = nc >= 0 && tile_free[nc] > 0;
-    // candidate pairs of this lane: (sa, sb[0..3]); -1 = none
-    int32_t sb[4] = {-1, -1, -1, -1};
-    if (sa >= 0 && nb_ok) {
-      const int32_t* bB = border + (int64_t)nb * 256 + (right ? 2 * 64 : 0);
-      for (int d = -1; d <= 1; ++d)
-        if (lane + d >= 0 && lane + d < 64) sb[d + 1] = bB[lane + d];
-    }
-    if (sa >= 0 && nc_ok) sb[3] = border[(int64_t)nc * 256 + cpos];
-    // predecessor lane's pairs (lane 0 starts an edge: none)
-    const int32_t psa = __shfl_up(sa, 1);
-    int32_t psb[3];
-    for (int q = 0; q < 3; ++q) psb[q] = __shfl_up(sb[q], 1);
+// ---- one wave per tile ------------------------------------------------------
+// k_frontier_tile: each 64-lane wave of a workgroup takes its own listed
+// tile (no workgroup barrier anywhere: the four waves run independently),
+// lane y holding tile row y as two 64-bit words (free, unknown).  A tile
+// needs only a small LDS slice (kRunsFast runs: parent + packed sums), so
+// DM_FL_OCC workgroups = 4*DM_FL_OCC tiles per CU are in flight: a C3 pass's
+// ~3.3k listed tiles all at once, and an explored map's tiles without
+// frontier cells (load, 2 ballots, done) stream at the rate of their loads.
+// A tile with more runs than that (noise-like frontiers: random states,
+// checkerboards) is listed for k_frontier_tile_big, the 256-thread kernel
+// with a whole-tile LDS table, launched right after (same tile-edge
+// hand-off: it arrives later than every tile here, so it unites with them).
+constexpr int kFW = 4;            // tile-waves per workgroup
+constexpr int kRunsFast = 512;    // runs a tile-wave keeps in LDS
+#ifndef DM_FL_OCC
+#define DM_FL_OCC 6               // workgroups per CU (LDS 24.3 KB each, <= 80 VGPRs)
+#endif
+
+// Orders this wave's LDS accesses across lanes (LDS executes one wave's
+// instructions in order; this keeps the compiler from moving them).
+__device__ inline void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Row gy (band-local; -1 / R are the halo rows) as a pointer to its column 0,
+// or nullptr where there is no row ("not unknown").
+__device__ inline const int8_t* row_base(const FGeom& g, const int8_t* state, const int8_t* halo, int32_t gy) {
+  if (gy >= 0 && gy < g.R) return state + (int64_t)gy * g.W;
+  if (gy == -1 && g.has_before) return halo;
+  if (gy == g.R && g.has_after) return halo + g.W;
+  return nullptr;
+}
+
+// Bits of the 4 bytes of w that equal zero, at bit positions 0..3.
+__device__ inline uint32_t zero_byte_bits(uint32_t w) {
+  uint32_t t = (w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  t = ~(t | w | 0x7F7F7F7Fu);                   // 0x80 in each zero byte
+  return (((t >> 7) * 0x00204081u) >> 21) & 0xFu;
+}
+
+// Unknown (-1) and free (0) bits of cells tx0..tx0+63 of row gy, and the
+// unknown bits of its cells tx0-1 / tx0+64.  Free bits only for band rows.
+__device__ inline void row_bits(const FGeom& g, const int8_t* __restrict__ state, const int8_t* __restrict__ halo,
+                                int32_t tx0, int32_t gy, uint64_t& U, uint64_t& Fr, uint32_t& uL, uint32_t& uR) {
+  U = 0ull;
+  Fr = 0ull;
+  uL = 0u;
+  uR = 0u;
+  const int8_t* rb = row_base(g, state, halo, gy);
+  if (!rb) return;
+  const int8_t* p = rb + tx0;
+  if (tx0 + 64 <= g.W && (reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+    uint4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = reinterpret_cast<const uint4*>(p)[q];
+#pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int32_t b = sb[q];
-      if (sa < 0 || b < 0) continue;
-      bool dup = false;
-      for (int r = 0; r < q; ++r) dup |= sb[r] == b;
-      if (lane > 0 && psa == sa) dup |= (psb[0] == b) | (psb[1] == b) | (psb[2] == b);
-      if (!dup) dm_uf_unite(slot_parent, slot_label, sa, b, &cnt[CNT_OVERFLOW], kOvUnionFind);
+      const uint32_t wd[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int sh = 16 * q + 4 * k;
+        U |= (uint64_t)zero_byte_bits(~wd[k]) << sh;
+        Fr |= (uint64_t)zero_byte_bits(wd[k]) << sh;
+      }
+    }
+  } else {
+    for (int k = 0; k < 64 && tx0 + k < g.W; ++k) {
+      const int8_t b = p[k];
+      U |= (uint64_t)(b == -1) << k;
+      Fr |= (uint64_t)(b == 0) << k;
+    }
+  }
+  if (gy < 0 || gy >= g.R) Fr = 0ull;
+  if (tx0 > 0) uL = rb[tx0 - 1] == -1 ? 1u : 0u;
+  if (tx0 + 64 < g.W) uR = rb[tx0 + 64] == -1 ? 1u : 0u;
+}
+
+__device__ inline uint64_t dilate_row(uint64_t U, uint32_t uL, uint32_t uR) {
+  return U | (U << 1) | (U >> 1) | (uint64_t)uL | ((uint64_t)uR << 63);
+}
+
+// Unions of the cells of one of this tile's edges with the neighbour tile's
+// facing edge (published slot ids, sc1 loads): lane = position along the
+// edge, cell pos against the neighbour's cells pos-1, pos, pos+1.  A lane
+// skips the pairs the previous lane (previous edge cell) issues.
+__device__ inline void edge_unions(int32_t sl, const int32_t* border, int32_t nb, int opp, int lane,
+                                   int32_t* slot_parent, unsigned long long* flag) {
+  const int32_t v = __hip_atomic_load(&border[(int64_t)nb * 256 + opp * 64 + lane], __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+  int32_t sb[3];
+  sb[0] = __shfl_up(v, 1);
+  sb[1] = v;
+  sb[2] = __shfl_down(v, 1);
+  if (lane == 0) sb[0] = -1;
+  if (lane == 63) sb[2] = -1;
+  const int32_t psl = __shfl_up(sl, 1);
+  int32_t psb[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) psb[q] = __shfl_up(sb[q], 1);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int32_t b = sb[q];
+    if (sl < 0 || b < 0) continue;
+    bool dup = false;
+    for (int r = 0; r < q; ++r) dup |= sb[r] == b;
+    if (lane > 0 && psl == sl) dup |= (psb[0] == b) | (psb[1] == b) | (psb[2] == b);
+    if (!dup) dm_uf_unite_idx(slot_parent, sl, b, flag, kOvUnionFind);
+  }
+}
+
+__global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
+    FGeom g, const int8_t* __restrict__ state, const int8_t* __restrict__ halo,
+    const int32_t* __restrict__ ftiles, const unsigned long long* __restrict__ list_n,
+    int32_t* border, unsigned long long* rel, unsigned long long stamp,
+    long long* __restrict__ slot_label, int32_t* slot_parent,
+    long long* __restrict__ slot_own, long long* __restrict__ slot_acc,
+    uint8_t* __restrict__ mask, int32_t* __restrict__ cell_slot, int32_t* __restrict__ edge_slot,
+    unsigned long long* cnt, unsigned long long* fsh, int32_t* __restrict__ big_list) {
+  __shared__ int32_t s_par[kFW][kRunsFast];
+  __shared__ unsigned long long s_acc[kFW][kRunsFast];  // size << 40 | sum_x << 20 | sum_y (tile-local)
+  __shared__ uint64_t s_rootw[kFW][kRunsFast / 64];     // root-run bits
+  __shared__ int32_t s_rootpre[kFW][kRunsFast / 64];    // roots before each word
+  const int w = threadIdx.x >> 6, lane = __lane_id();
+  int32_t* par = s_par[w];
+  unsigned long long* acc = s_acc[w];
+  uint64_t* rootw = s_rootw[w];
+  int32_t* rootpre = s_rootpre[w];
+  const int64_t nft = (int64_t)*list_n;
+  const int64_t wid = (int64_t)blockIdx.x * kFW + w;
+  const int shard = (int)(wid % kShards);
+  const long long sh0 = (long long)shard * g.slot_per;
+  const bool dense = g.want_mask || g.want_labels;
+  for (int64_t jj = wid; jj < nft; jj += (int64_t)gridDim.x * kFW) {
+    const int32_t tile = __builtin_amdgcn_readfirstlane(ftiles[jj]);
+    const int32_t tx = tile % g.TX, ty = tile / g.TX;
+    const int32_t tx0 = tx * DM_TS, ty0 = ty * DM_TS;  // ty0 band-local
+    // ---- 1. rows: lane y = tile row y (lanes 0 / 63 also rows -1 / 64) --------
+    uint64_t U, Fr;
+    uint32_t uL, uR;
+    row_bits(g, state, halo, tx0, ty0 + lane, U, Fr, uL, uR);
+    uint64_t Ue = 0ull, Fe;
+    uint32_t eL = 0u, eR = 0u;
+    if (lane == 0 || lane == 63) row_bits(g, state, halo, tx0, lane == 0 ? ty0 - 1 : ty0 + DM_TS, Ue, Fe, eL, eR);
+    // ---- 2. frontier bits: free & 3x3 dilation of unknown -------------------
+    const uint64_t h = dilate_row(U, uL, uR);
+    const uint64_t he = dilate_row(Ue, eL, eR);
+    uint64_t hu = __shfl_up(h, 1);
+    uint64_t hd = __shfl_down(h, 1);
+    if (lane == 0) hu = he;
+    if (lane == 63) hd = he;
+    const uint64_t F = Fr & (h | hu | hd);
+    if (__ballot(F != 0ull) == 0ull) continue;  // no frontier cell: nothing to publish
+    // ---- 3. runs of set bits, numbered row-major ---------------------------
+    const uint64_t st = run_starts(F);
+    const int c = __popcll(st);
+    int incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(incl, d);
+      if (lane >= d) incl += v;
+    }
+    const int rbase = incl - c;
+    const int nruns = __shfl(incl, 63);
+    if (nruns > kRunsFast) {  // too many for this wave's LDS: the big kernel's
+      if (lane == 0) big_list[atomicAdd(&cnt[CNT_BIG], 1ull)] = tile;
+      continue;
+    }
+    for (int r = lane; r < nruns; r += 64) {
+      par[r] = r;
+      acc[r] = 0ull;
+    }
+    wave_lds_sync();
+    // ---- 4. union every run with the runs above it (extended by a cell) ------
+    const uint64_t Fa = __shfl_up(F, 1);
+    const uint64_t sta = __shfl_up(st, 1);
+    const int rba = __shfl_up(rbase, 1);
+    if (lane > 0 && Fa) {
+      uint64_t s_ = st;
+      int r = rbase;
+      while (s_) {
+        const int s0 = __ffsll((unsigned long long)s_) - 1;
+        const int e0 = run_end(F, s0);
+        const int lo = s0 > 0 ? s0 - 1 : 0, hi = e0 < 63 ? e0 + 1 : 63;
+        uint64_t P = Fa & upto_mask(hi) & ~(lo > 0 ? upto_mask(lo - 1) : 0ull);
+        while (P) {
+          const int q = __ffsll((unsigned long long)P) - 1;
+          lds_unite(par, r, rba + __popcll(sta & upto_mask(q)) - 1);
+          const uint64_t rest = ~(Fa >> q);
+          const int len = rest ? __ffsll((unsigned long long)rest) - 1 : 64 - q;
+          P &= ~upto_mask(q + len - 1);
+        }
+        ++r;
+        s_ &= s_ - 1;
+      }
+    }
+    wave_lds_sync();
+    // ---- 5. compress; root bits; component id = rank of the root run ---------
+    for (int r0 = 0; r0 < nruns; r0 += 64) {
+      const int r = r0 + lane;
+      int32_t x = r;
+      if (r < nruns) {
+        int32_t p = ((volatile int32_t*)par)[r];
+        while (p != x) {
+          x = p;
+          p = ((volatile int32_t*)par)[x];
+        }
+        par[r] = x;
+      }
+      const uint64_t rb = __ballot(r < nruns && x == r);
+      if (lane == 0) rootw[r0 >> 6] = rb;
+    }
+    wave_lds_sync();
+    const int nw = (nruns + 63) >> 6;
+    int ncomp;
+    {
+      const int pc = lane < nw ? __popcll(rootw[lane]) : 0;
+      int inc2 = pc;
+#pragma unroll
+      for (int d = 1; d < 8; d <<= 1) {
+        const int v = __shfl_up(inc2, d);
+        if (lane >= d) inc2 += v;
+      }
+      if (lane < nw) rootpre[lane] = inc2 - pc;
+      ncomp = __shfl(inc2, 7);
+    }
+    // ---- 6. per-component sums, in the root run's acc word -------------------
+    {
+      uint64_t s_ = st;
+      int r = rbase;
+      while (s_) {
+        const int s0 = __ffsll((unsigned long long)s_) - 1;
+        const int e0 = run_end(F, s0);
+        const unsigned long long len = (unsigned long long)(e0 - s0 + 1);
+        atomicAdd(&acc[par[r]], (len << 40) | ((unsigned long long)((s0 + e0) * (e0 - s0 + 1) / 2) << 20) |
+                                    (unsigned long long)(lane * (e0 - s0 + 1)));
+        ++r;
+        s_ &= s_ - 1;
+      }
+    }
+    wave_lds_sync();
+    // ---- 7. slots: one per component from this wave's shard region -----------
+    unsigned long long sb0 = 0ull;
+    if (lane == 0) sb0 = atomicAdd(&fsh[shard * kShardWords + SH_SLOT], (unsigned long long)ncomp);
+    const long long base = (long long)__shfl(sb0, 0);
+    auto slot_of_run = [&](int r) -> int32_t {
+      const int root = par[r];
+      const long long v = base + rootpre[root >> 6] + __popcll(rootw[root >> 6] & ((1ull << (root & 63)) - 1ull));
+      return v < g.slot_per ? (int32_t)(sh0 + v) : -1;
+    };
+    {
+      uint64_t s_ = st;
+      int r = rbase;
+      while (s_) {
+        const int s0 = __ffsll((unsigned long long)s_) - 1;
+        if (par[r] == r) {
+          const int32_t slot = slot_of_run(r);
+          if (slot < 0) {
+            atomicOr(&cnt[CNT_OVERFLOW], kOvSlots);
+          } else {
+            const unsigned long long a = acc[r];
+            const long long sz = (long long)(a >> 40);
+            const long long sx = sz * tx0 + (long long)((a >> 20) & 0xFFFFFull);
+            const long long sy = sz * ((long long)g.row0 + ty0) + (long long)(a & 0xFFFFFull);
+            slot_label[slot] = ((long long)g.row0 + ty0 + lane) * g.W + tx0 + s0;
+            slot_own[3 * (int64_t)slot + 0] = sz;
+            slot_own[3 * (int64_t)slot + 1] = sx;
+            slot_own[3 * (int64_t)slot + 2] = sy;
+            slot_acc[3 * (int64_t)slot + 0] = sz;
+            slot_acc[3 * (int64_t)slot + 1] = sx;
+            slot_acc[3 * (int64_t)slot + 2] = sy;
+          }
+        }
+        ++r;
+        s_ &= s_ - 1;
+      }
+    }
+    // ---- 8. edges: publish, arrive, unite -------------------
+    // sides [0] first row, [1] last row, [2] first col, [3] last col; lane =
+    // position along the side.  The published slot ids are sc1 stores drained
+    // by this wave before it arrives at any pair word (MI355X_MICROARCH.md,
+    // inter-workgroup visibility, hand-off row 1); the second tile of a pair
+    // reads them with sc1 loads after its own arrival returned.
+    int32_t sl[4];
+    {
+      const uint64_t F0 = __shfl(F, 0), F63 = __shfl(F, 63);
+      const uint64_t st0 = __shfl(st, 0), st63 = __shfl(st, 63);
+      const int rb0 = __shfl(rbase, 0), rb63 = __shfl(rbase, 63);
+      sl[0] = ((F0 >> lane) & 1ull) ? slot_of_run(rb0 + __popcll(st0 & upto_mask(lane)) - 1) : -1;
+      sl[1] = ((F63 >> lane) & 1ull) ? slot_of_run(rb63 + __popcll(st63 & upto_mask(lane)) - 1) : -1;
+      sl[2] = (F & 1ull) ? slot_of_run(rbase) : -1;  // column 0 of row `lane`: its first run
+      sl[3] = (F >> 63) ? slot_of_run(rbase + c - 1) : -1;  // column 63: its last run
+    }
+    uint64_t fb[4];
+#pragma unroll
+    for (int sd = 0; sd < 4; ++sd) fb[sd] = __ballot(sl[sd] >= 0);
+#pragma unroll
+    for (int sd = 0; sd < 4; ++sd)
+      if (fb[sd]) __hip_atomic_store(&border[(int64_t)tile * 256 + sd * 64 + lane], sl[sd], __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+    if (fb[0] | fb[1] | fb[2] | fb[3]) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const bool up = ty > 0, down = ty + 1 < g.TY, left = tx > 0, right = tx + 1 < g.TX;
+      const int64_t NT = g.NT;
+      // lane i arrives at relation i: 0 up, 1 down, 2 left, 3 right edge;
+      // 4 up-left, 5 up-right, 6 down-left, 7 down-right corner
+      int64_t e = -1;
+      unsigned long long mine = 0ull;
+      int32_t nb = -1;
+      if (lane == 0 && fb[0] && up) { e = NT + tile - g.TX; mine = 2; nb = tile - g.TX; }
+      if (lane == 1 && fb[1] && down) { e = NT + tile; mine = 1; nb = tile + g.TX; }
+      if (lane == 2 && fb[2] && left) { e = tile - 1; mine = 2; nb = tile - 1; }
+      if (lane == 3 && fb[3] && right) { e = tile; mine = 1; nb = tile + 1; }
+      if (lane == 4 && (fb[0] & 1ull) && up && left) { e = 2 * NT + tile - g.TX - 1; mine = 2; nb = tile - g.TX - 1; }
+      if (lane == 5 && (fb[0] >> 63) && up && right) { e = 3 * NT + tile - g.TX + 1; mine = 2; nb = tile - g.TX + 1; }
+      if (lane == 6 && (fb[1] & 1ull) && down && left) { e = 3 * NT + tile; mine = 1; nb = tile + g.TX - 1; }
+      if (lane == 7 && (fb[1] >> 63) && down && right) { e = 2 * NT + tile; mine = 1; nb = tile + g.TX + 1; }
+      bool second = false;
+      if (e >= 0) {
+        const unsigned long long old = __hip_atomic_fetch_max(&rel[e], (stamp << 2) | mine, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT);
+        second = (old >> 2) == stamp && (old & (3ull ^ mine)) != 0ull;
+      }
+      const uint64_t sec = __ballot(second);
+      unsigned long long* uflag = &cnt[CNT_OVERFLOW];
+#pragma unroll
+      for (int sd = 0; sd < 4; ++sd)
+        if ((sec >> sd) & 1ull) edge_unions(sl[sd], border, __shfl(nb, sd), sd ^ 1, lane, slot_parent, uflag);
+      // corners: the diagonal neighbour's facing corner cell (upper tiles:
+      // its last row, lower tiles: its first row)
+      const int32_t c00 = __shfl(sl[0], 0), c630 = __shfl(sl[0], 63);
+      const int32_t c063 = __shfl(sl[1], 0), c6363 = __shfl(sl[1], 63);
+      if (second && lane >= 4) {
+        const int32_t me = lane == 4 ? c00 : lane == 5 ? c630 : lane == 6 ? c063 : c6363;
+        const int nrow = lane < 6 ? 1 : 0;
+        const int ncol = (lane == 4 || lane == 6) ? 63 : 0;
+        const int32_t b = __hip_atomic_load(&border[(int64_t)nb * 256 + nrow * 64 + ncol], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        if (b >= 0) dm_uf_unite_idx(slot_parent, me, b, uflag, kOvUnionFind);
+      }
+    }
+    // ---- 9. band edge rows (cross-band merging) and optional dense outputs ---
+    const int32_t gy = ty0 + lane;
+    if (gy < g.R && (dense || gy == 0 || gy == g.R - 1)) {
+      uint64_t s_ = F;
+      while (s_) {
+        const int x = __ffsll((unsigned long long)s_) - 1;
+        s_ &= s_ - 1;
+        const int32_t gx = tx0 + x;
+        const int32_t sv = slot_of_run(rbase + __popcll(st & upto_mask(x)) - 1);
+        const int64_t gi = (int64_t)gy * g.W + gx;
+        if (g.want_mask) mask[gi] = 1;
+        if (g.want_labels) cell_slot[gi] = sv;
+        if (gy == 0) edge_slot[gx] = sv;
+        if (gy == g.R - 1) edge_slot[g.W + gx] = sv;
+      }
     }
   }
 }
@@ -546,19 +939,25 @@ __device__ inline bool slot_used(const FGeom& g, const int64_t* s_n, int64_t s) 
   return s < g.slot_cap && (s % g.slot_per) < s_n[s / g.slot_per];
 }
 
-// Roots, and every non-root slot's sums added into its root.  A component
-// spread over many tiles (a robot's star of long thin rays on a 1 cm map)
-// has thousands of slots: one global atomic each would queue them on the
-// same three addresses.  The sums are first combined per workgroup in an LDS
-// table keyed by root (64-bit LDS atomics), then flushed with one global
-// atomic per (workgroup, root, field); a root that finds no LDS entry within
-// kRootProbe probes goes straight to global memory.
+// Roots, and every non-root slot's sums and label folded into its root: the
+// set's size / sum_x / sum_y add up, its label is the min over its slots
+// (SPEC a9: the tile-edge unions hook by slot index, so the root slot is not
+// the min-label one).  A component spread over many tiles (a robot's star of
+// long thin rays on a 1 cm map) has thousands of slots: one global atomic
+// each would queue them on the same four addresses.  The values are first
+// combined per workgroup in an LDS table keyed by root (64-bit LDS atomics),
+// then flushed with one global atomic per (workgroup, root, field); a root
+// that finds no LDS entry within kRootProbe probes goes straight to global
+// memory.  The min label lands in slot_label[root] (only roots' entries are
+// written; a non-root's own label is read once, never changed).
 constexpr int kRootHash = 512;
 constexpr int kRootProbe = 8;
 
-__device__ inline void add_to_root(long long* slot_acc, int32_t r, const long long* v) {
+__device__ inline void add_to_root(long long* slot_acc, long long* slot_label, int32_t r, const long long* v,
+                                   long long lab) {
   for (int f = 0; f < 3; ++f)
     atomicAdd((unsigned long long*)&slot_acc[3 * (int64_t)r + f], (unsigned long long)v[f]);
+  atomicMin(&slot_label[r], lab);
 }
 
 __global__ __launch_bounds__(256) void k_frontier_resolve(FGeom g, const int32_t* __restrict__ slot_parent,
@@ -566,16 +965,18 @@ __global__ __launch_bounds__(256) void k_frontier_resolve(FGeom g, const int32_t
                                                           const long long* __restrict__ slot_own,
                                                           long long* slot_acc,
                                                           const unsigned long long* fsh, int fuse,
-                                                          const long long* __restrict__ slot_label,
+                                                          long long* slot_label,
                                                           long long* __restrict__ clusters,
                                                           int32_t* __restrict__ slot_k,
                                                           unsigned long long* cnt) {
   __shared__ int64_t s_n[kShards];
   __shared__ int32_t hkey[kRootHash];
   __shared__ unsigned long long hacc[3][kRootHash];
+  __shared__ long long hmin[kRootHash];
   for (int e = threadIdx.x; e < kRootHash; e += blockDim.x) {
     hkey[e] = -1;
     hacc[0][e] = hacc[1][e] = hacc[2][e] = 0;
+    hmin[e] = 0x7FFFFFFFFFFFFFFFll;
   }
   load_shard_counts(g, fsh, s_n);  // (its barrier also orders the table init)
   const int lane = __lane_id();
@@ -588,9 +989,9 @@ __global__ __launch_bounds__(256) void k_frontier_resolve(FGeom g, const int32_t
     if (used) slot_root[s] = r;
     if (fuse) {
       // min_size <= 1: every root is a cluster, so k_frontier_compact's
-      // work happens here; its sums are not final yet (other workgroups
-      // still add into the root), so the record holds -(slot + 1) and the
-      // sort kernel reads the sums (put_sorted)
+      // work happens here; its label and sums are not final yet (other
+      // workgroups still fold into the root), so the record holds -(slot + 1)
+      // and the sort kernel reads them by slot (record_vals)
       const bool root = used && r == (int32_t)s;
       const unsigned long long bal = __ballot(root);
       if (bal) {
@@ -601,30 +1002,32 @@ __global__ __launch_bounds__(256) void k_frontier_resolve(FGeom g, const int32_t
         const unsigned long long k = k0 + __popcll(bal & ((1ull << lane) - 1));
         if (root && (int64_t)k < g.clu_cap) {
           slot_k[s] = (int32_t)k;
-          clusters[4 * k + 0] = slot_label[s];
+          clusters[4 * k + 0] = -1;
           clusters[4 * k + 1] = -(long long)s - 1;
         }
       }
     }
     if (!used || r == (int32_t)s) continue;
     const long long v[3] = {slot_own[3 * s + 0], slot_own[3 * s + 1], slot_own[3 * s + 2]};
+    const long long lab = slot_label[s];
     uint32_t h = ((uint32_t)r * 2654435761u) >> 23;  // 9 bits
     bool done = false;
     for (int p = 0; p < kRootProbe && !done; ++p, h = (h + 1) & (kRootHash - 1)) {
       const int32_t k = atomicCAS(&hkey[h], -1, r);
       if (k == -1 || k == r) {
         for (int f = 0; f < 3; ++f) atomicAdd(&hacc[f][h], (unsigned long long)v[f]);
+        atomicMin(&hmin[h], lab);
         done = true;
       }
     }
-    if (!done) add_to_root(slot_acc, r, v);
+    if (!done) add_to_root(slot_acc, slot_label, r, v, lab);
   }
   __syncthreads();
   for (int e = threadIdx.x; e < kRootHash; e += blockDim.x) {
     const int32_t r = hkey[e];
     if (r < 0) continue;
     const long long v[3] = {(long long)hacc[0][e], (long long)hacc[1][e], (long long)hacc[2][e]};
-    add_to_root(slot_acc, r, v);
+    add_to_root(slot_acc, slot_label, r, v, hmin[e]);
   }
 }
 
@@ -683,46 +1086,64 @@ __device__ inline void write_rb_header(int64_t K, int64_t cap, unsigned long lon
 }
 
 // A record written by the fused compaction (k_frontier_resolve, min_size
-// <= 1) holds -(slot + 1) instead of its sums: read them from slot_acc
-// (final after resolve) and write them into the raw record too (the host
-// sort fallback reads raw records).  One writer per record.
-__device__ inline void record_sums(long long* clusters, const long long* sums, int64_t i, long long* sz,
-                                   long long* sx, long long* sy) {
-  *sz = clusters[4 * i + 1];
-  if (sums && *sz < 0) {
-    const int64_t sl = -*sz - 1;
+// <= 1) holds -(slot + 1) instead of its size: its label and sums are read
+// by slot (final after the resolve kernel).  Records are only read here,
+// never rewritten (other workgroups read the keys concurrently); the raw
+// records of a pass the device does not sort are completed by
+// fix_raw_records.
+__device__ inline void record_vals(const long long* clusters, const long long* sums, const long long* labels,
+                                   int64_t i, long long* lab, long long* sz, long long* sx, long long* sy) {
+  const long long m = clusters[4 * i + 1];
+  if (sums && m < 0) {
+    const int64_t sl = -m - 1;
+    *lab = labels[sl];
     *sz = sums[3 * sl];
     *sx = sums[3 * sl + 1];
     *sy = sums[3 * sl + 2];
-    clusters[4 * i + 1] = *sz;
-    clusters[4 * i + 2] = *sx;
-    clusters[4 * i + 3] = *sy;
   } else {
+    *lab = clusters[4 * i];
+    *sz = m;
     *sx = clusters[4 * i + 2];
     *sy = clusters[4 * i + 3];
   }
 }
 
-// Raw records of a pass the device does not sort (K > cap): sums in place.
-__device__ inline void fix_raw_records(long long* clusters, const long long* sums, int64_t K) {
+// Sort key (label) of record i.
+__device__ inline long long record_key(const long long* clusters, const long long* labels, int64_t i) {
+  if (labels) {
+    const long long m = clusters[4 * i + 1];
+    if (m < 0) return labels[-m - 1];
+  }
+  return clusters[4 * i];
+}
+
+// Raw records of a pass the device does not sort (K > cap): values in place
+// (the host sorts them).  One writer per record, no concurrent key readers.
+__device__ inline void fix_raw_records(long long* clusters, const long long* sums, const long long* labels,
+                                       int64_t K) {
   if (!sums) return;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < K; i += (int64_t)gridDim.x * blockDim.x) {
-    long long sz, sx, sy;
-    record_sums(clusters, sums, i, &sz, &sx, &sy);
+    long long lab, sz, sx, sy;
+    record_vals(clusters, sums, labels, i, &lab, &sz, &sx, &sy);
+    clusters[4 * i + 0] = lab;
+    clusters[4 * i + 1] = sz;
+    clusters[4 * i + 2] = sx;
+    clusters[4 * i + 3] = sy;
   }
 }
 
 // Raw record i ([4] int64 label, size, sum_x, sum_y) -> dm_cluster at its
 // sorted position, centroid cx_m = ox + ((double)sum_x / (double)size + 0.5)
 // * res (SPEC a10: one IEEE division, then add; no FMA contraction).
-__device__ inline void put_sorted(double ox, double oy, double res, long long* clusters, const long long* sums,
+__device__ inline void put_sorted(double ox, double oy, double res, const long long* clusters,
+                                  const long long* sums, const long long* labels,
                                   int64_t i, int64_t rank, dm_cluster* __restrict__ out,
                                   int32_t* __restrict__ rank_of, dm_cluster* __restrict__ host_out,
                                   int64_t host_cap) {
   dm_cluster c;
-  c.label = clusters[4 * i];
-  long long sz, sx, sy;
-  record_sums(clusters, sums, i, &sz, &sx, &sy);
+  long long lab, sz, sx, sy;
+  record_vals(clusters, sums, labels, i, &lab, &sz, &sx, &sy);
+  c.label = lab;
   c.size = sz;
   c.sum_x = sx;
   c.sum_y = sy;
@@ -755,6 +1176,7 @@ constexpr int64_t kRankSortCap = 1 << 16;
 
 __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy, double res,
                                                             long long* clusters, const long long* sums,
+                                                            const long long* labels,
                                                             const unsigned long long* __restrict__ count,
                                                             int64_t cap, dm_cluster* __restrict__ out,
                                                             int32_t* __restrict__ rank_of,
@@ -770,14 +1192,14 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
   const int64_t K = (int64_t)*count;
   if (blockIdx.x == 0) write_rb_header(K, cap, sorted, cnt, ncnt, sorted_idx, fsh, host_out);
   if (K > cap) {
-    fix_raw_records(clusters, sums, K);
+    fix_raw_records(clusters, sums, labels, K);
     return;
   }
   // grid-stride over groups of 64 records (the grid is sized from the
   // expected count; the loop bound is uniform within a workgroup)
   for (int64_t g0 = (int64_t)blockIdx.x * 64; g0 < K; g0 += (int64_t)gridDim.x * 64) {
     const int64_t i = g0 + lane;
-    const long long key = i < K ? clusters[4 * i] : 0;
+    const long long key = i < K ? record_key(clusters, labels, i) : 0;
     int32_t r = 0;
     for (int64_t c0 = 0; c0 < K; c0 += kSortChunk) {
       const int n = (int)min((int64_t)kSortChunk, K - c0);
@@ -787,7 +1209,7 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
 #pragma unroll
         for (int q = 0; q < kSortChunk / kSortThreads; ++q) {
           const int e = tid + q * kSortThreads;
-          v[q] = e < n ? clusters[4 * (c0 + e)] : 0;
+          v[q] = e < n ? record_key(clusters, labels, c0 + e) : 0;
         }
 #pragma unroll
         for (int q = 0; q < kSortChunk / kSortThreads; ++q) {
@@ -809,7 +1231,7 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
       int32_t rank = 0;
 #pragma unroll
       for (int q = 0; q < kSortWaves; ++q) rank += part[q][lane];
-      put_sorted(ox, oy, res, clusters, sums, i, rank, out, rank_of, host_out, host_cap);
+      put_sorted(ox, oy, res, clusters, sums, labels, i, rank, out, rank_of, host_out, host_cap);
     }
   }
 }
@@ -830,13 +1252,14 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
 // Every kernel reads the device-side count; K > cap leaves the result
 // unsorted (flag 0), as the rank sort does.
 __global__ __launch_bounds__(256) void k_bs_count(const long long* __restrict__ clusters,
+                                                  const long long* __restrict__ labels,
                                                   const unsigned long long* __restrict__ count, int64_t cap,
                                                   long long base, int shift,
                                                   int32_t* __restrict__ rcnt) {
   const int64_t K = (int64_t)*count;
   if (K > cap) return;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < K; i += (int64_t)gridDim.x * blockDim.x)
-    atomicAdd(&rcnt[(clusters[4 * i] - base) >> shift], 1);
+    atomicAdd(&rcnt[(record_key(clusters, labels, i) - base) >> shift], 1);
 }
 
 constexpr int kScanThreads = 1024;
@@ -878,6 +1301,7 @@ __global__ __launch_bounds__(kScanThreads) void k_bs_scan(const unsigned long lo
 }
 
 __global__ __launch_bounds__(256) void k_bs_place(const long long* __restrict__ clusters,
+                                                  const long long* __restrict__ labels,
                                                   const unsigned long long* __restrict__ count, int64_t cap,
                                                   long long base, int shift,
                                                   int32_t* __restrict__ rcur, long long* __restrict__ bkey,
@@ -885,7 +1309,7 @@ __global__ __launch_bounds__(256) void k_bs_place(const long long* __restrict__ 
   const int64_t K = (int64_t)*count;
   if (K > cap) return;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < K; i += (int64_t)gridDim.x * blockDim.x) {
-    const long long key = clusters[4 * i];
+    const long long key = record_key(clusters, labels, i);
     const int32_t p = atomicAdd(&rcur[(key - base) >> shift], 1);
     bkey[p] = key;
     bidx[p] = (int32_t)i;
@@ -894,6 +1318,7 @@ __global__ __launch_bounds__(256) void k_bs_place(const long long* __restrict__ 
 
 __global__ __launch_bounds__(256) void k_bs_rank(double ox, double oy, double res,
                                                  long long* clusters, const long long* sums,
+                                                 const long long* labels,
                                                  const unsigned long long* __restrict__ count, int64_t cap,
                                                  long long base, int shift,
                                                  const int32_t* __restrict__ roff,
@@ -906,7 +1331,7 @@ __global__ __launch_bounds__(256) void k_bs_rank(double ox, double oy, double re
   const int64_t K = (int64_t)*count;
   if (blockIdx.x == 0) write_rb_header(K, cap, sorted, cnt, ncnt, sorted_idx, fsh, host_out);
   if (K > cap) {
-    fix_raw_records(clusters, sums, K);
+    fix_raw_records(clusters, sums, labels, K);
     return;
   }
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < K; p += (int64_t)gridDim.x * blockDim.x) {
@@ -915,7 +1340,7 @@ __global__ __launch_bounds__(256) void k_bs_rank(double ox, double oy, double re
     const int32_t lo = roff[b], hi = roff[b + 1];
     int64_t rank = lo;
     for (int32_t j = lo; j < hi; ++j) rank += bkey[j] < key;
-    put_sorted(ox, oy, res, clusters, sums, bidx[p], rank, out, rank_of, host_out, host_cap);
+    put_sorted(ox, oy, res, clusters, sums, labels, bidx[p], rank, out, rank_of, host_out, host_cap);
   }
 }
 
@@ -972,7 +1397,7 @@ int dm_launch_edge_labels(dm_grid* g) {
 }
 
 int dm_launch_rank_sort(hipStream_t stream, long long* clusters, const long long* sums,
-                        const unsigned long long* d_count,
+                        const long long* labels, const unsigned long long* d_count,
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
                         int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
                         int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
@@ -982,14 +1407,14 @@ int dm_launch_rank_sort(hipStream_t stream, long long* clusters, const long long
   // least 2048): a thousand idle 1024-thread workgroups cost microseconds
   const int64_t want = std::max<int64_t>(2 * expect, 2048);
   hipLaunchKernelGGL(k_rank_sort, dim3(grid_for(std::min(cap, want), 64, 1 << 20)), dim3(kSortThreads), 0, stream,
-                     ox, oy, res, clusters, sums, d_count, cap, out, rank_of, d_sorted, cnt, ncnt, sorted_idx,
+                     ox, oy, res, clusters, sums, labels, d_count, cap, out, rank_of, d_sorted, cnt, ncnt, sorted_idx,
                      fsh, host_out, host_cap);
   DM_HIP(hipGetLastError());
   return DM_OK;
 }
 
 int dm_launch_bucket_sort(dm_grid* g, long long* clusters, const long long* sums,
-                          const unsigned long long* d_count,
+                          const long long* labels, const unsigned long long* d_count,
                           int64_t max_records, int64_t row_base, int64_t rows, dm_cluster* out,
                           int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
                           int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
@@ -1007,17 +1432,17 @@ int dm_launch_bucket_sort(dm_grid* g, long long* clusters, const long long* sums
   int32_t* roff = rcnt + (kBuckets + 1);
   int32_t* rcur = roff + (kBuckets + 1);
   const int eg = grid_for(max_records, 256, 2048);
-  hipLaunchKernelGGL(k_bs_count, dim3(eg), dim3(256), 0, g->stream, clusters, d_count, max_records, base,
+  hipLaunchKernelGGL(k_bs_count, dim3(eg), dim3(256), 0, g->stream, clusters, labels, d_count, max_records, base,
                      shift, rcnt);
   DM_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_bs_scan, dim3(1), dim3(kScanThreads), 0, g->stream, d_count, max_records, nbk, rcnt,
                      roff, rcur);
   DM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_bs_place, dim3(eg), dim3(256), 0, g->stream, clusters, d_count, max_records, base,
-                     shift, rcur, g->bs_key, g->bs_idx);
+  hipLaunchKernelGGL(k_bs_place, dim3(eg), dim3(256), 0, g->stream, clusters, labels, d_count, max_records,
+                     base, shift, rcur, g->bs_key, g->bs_idx);
   DM_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_bs_rank, dim3(eg), dim3(256), 0, g->stream, g->p.origin_x, g->p.origin_y,
-                     g->p.resolution, clusters, sums, d_count, max_records, base, shift, roff, g->bs_key,
+                     g->p.resolution, clusters, sums, labels, d_count, max_records, base, shift, roff, g->bs_key,
                      g->bs_idx, out, rank_of, d_sorted, cnt, ncnt, sorted_idx, fsh, host_out, host_cap);
   DM_HIP(hipGetLastError());
   return DM_OK;
@@ -1037,7 +1462,7 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   dm_timer_begin(g, "frontier_prep", &t);
   hipLaunchKernelGGL(k_frontier_prep, dim3(grid_for(std::max<int64_t>(std::max<int64_t>(g->NT, 2 * g->W), kShards * kShardWords), 256, 1024)), dim3(256), 0,
                      g->stream, g->NT, g->tile_free, g->ftiles, list_n, other_n, 2 * g->W, g->cnt, g->fsh,
-                     g->edge_slot);
+                     g->edge_slot, g->slot_parent, g->slot_cap);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   // the last integrate call's tile workspace is free once the map update
@@ -1046,18 +1471,20 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   DM_HIP(dm_mark_tiles(g));
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));
-  const int nft_grid = grid_for(g->NT, 1, 2048);
-  // k_frontier_tile: one listed tile per workgroup (the dispatcher balances)
-  const int ftile_grid = grid_for(g->NT, 1, 8192);
+  // k_frontier_tile: one listed tile per wave (the dispatcher balances);
+  // k_frontier_tile_big: the tiles it left (more runs than a wave holds)
   dm_timer_begin(g, "frontier_tile", &t);
-  hipLaunchKernelGGL(k_frontier_tile, dim3(ftile_grid), dim3(kFT), 0, g->stream, fg, g->state,
-                     g->halo, g->ftiles, list_n, g->border, g->slot_label, g->slot_parent, g->slot_own,
-                     g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh);
+  hipLaunchKernelGGL(k_frontier_tile, dim3(grid_for(g->NT, kFW, 8192)), dim3(kFW * 64), 0, g->stream, fg, g->state,
+                     g->halo, g->ftiles, list_n, g->border, g->rel, (unsigned long long)g->fr_pass,
+                     g->slot_label, g->slot_parent, g->slot_own, g->slot_acc, g->mask, g->cell_slot, g->edge_slot,
+                     g->cnt, g->fsh, g->big_tiles);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
-  dm_timer_begin(g, "frontier_merge", &t);
-  hipLaunchKernelGGL(k_frontier_merge, dim3(nft_grid), dim3(256), 0, g->stream, fg, g->ftiles, list_n, g->tile_free,
-                     g->border, g->slot_label, g->slot_parent, g->cnt);
+  dm_timer_begin(g, "frontier_big", &t);
+  hipLaunchKernelGGL(k_frontier_tile_big, dim3(grid_for(g->NT, 1, 512)), dim3(kFT), 0, g->stream, fg, g->state,
+                     g->halo, g->big_tiles, g->cnt + CNT_BIG, g->border, g->rel, (unsigned long long)g->fr_pass,
+                     g->slot_label, g->slot_parent, g->slot_own,
+                     g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   const int sgrid = grid_for(g->slot_cap, 256, 1024);
@@ -1087,10 +1514,12 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   // the last collected pass predicts this one's cluster count (either sort
   // is exact for any count; only their speed differs)
   const int rc = g->sort_hint > kBucketSortMin
-      ? dm_launch_bucket_sort(g, g->clusters, fuse ? g->slot_acc : nullptr, g->cnt + CNT_CLUSTERS, g->slot_cap, g->row0, g->R, g->out_clu,
+      ? dm_launch_bucket_sort(g, g->clusters, fuse ? g->slot_acc : nullptr, fuse ? g->slot_label : nullptr,
+                              g->cnt + CNT_CLUSTERS, g->slot_cap, g->row0, g->R, g->out_clu,
                               g->rank_of, g->cnt + CNT_SORTED, g->cnt, CNT_N, CNT_SORTED, g->fsh,
                               g->h_out_dev, g->h_out_cap)
-      : dm_launch_rank_sort(g->stream, g->clusters, fuse ? g->slot_acc : nullptr, g->cnt + CNT_CLUSTERS, g->slot_cap, g->p.origin_x,
+      : dm_launch_rank_sort(g->stream, g->clusters, fuse ? g->slot_acc : nullptr, fuse ? g->slot_label : nullptr,
+                            g->cnt + CNT_CLUSTERS, g->slot_cap, g->p.origin_x,
                             g->p.origin_y, g->p.resolution, g->out_clu, g->rank_of, g->cnt + CNT_SORTED,
                             g->cnt, CNT_N, CNT_SORTED, g->fsh, g->h_out_dev, g->h_out_cap, g->sort_hint);
   dm_timer_end(g, &t);

@@ -40,8 +40,9 @@ enum {
   CNT_FL0 = 12,     // frontier tile-list length, even calls (zeroed by the odd calls)
   CNT_FL1 = 13,     // frontier tile-list length, odd calls (zeroed by the even calls)
   CNT_LITEMS = 14,  // light work items (= light tiles)
-  CNT_IOVERFLOW = 15,  // integrate capacity overflow flags (1 first-touch list, 2 pieces)
-  CNT_N = 16
+  CNT_IOVERFLOW = 15,  // integrate capacity overflow flags (1 first-touch list, 2 pieces, 4 work lists)
+  CNT_BIG = 16,     // frontier tiles with more runs than a tile-wave holds (big-tile list length)
+  CNT_N = 17
 };
 // CNT_OVERFLOW bits of a frontier pass
 constexpr unsigned long long kOvSlots = 4ull;      // a slot shard region overflowed
@@ -185,7 +186,12 @@ struct dm_grid {
 
   // frontier workspace
   int32_t* ftiles = nullptr;   // tiles with free cells (built by k_frontier_prep)
-  int32_t* border = nullptr;   // [tile][4][64] slot ids (listed tiles)
+  int32_t* big_tiles = nullptr;  // [NT] tiles left to k_frontier_tile_big (too many runs for a tile-wave)
+  int32_t* border = nullptr;   // [tile][4][64] slot ids of a tile's edges (published sides only)
+  // tile-edge hand-off words of k_frontier_tile, [4][NT]: horizontal (t, t+1),
+  // vertical (t, t+TX), diagonal (t, t+TX+1), anti-diagonal (t, t+TX-1) pairs,
+  // each (pass stamp << 2 | arrived sides); never reset (stamped)
+  unsigned long long* rel = nullptr;
   int32_t fparity = 0;         // which CNT_FL* counter the last frontier call used
   int64_t border_cap = 0;      // in tiles
   int64_t slot_cap = 0;
@@ -277,10 +283,11 @@ int dm_launch_edge_labels(dm_grid* g);
 int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied);
 int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters,
                         int64_t* copied);
-// sums: slot sums (slot_acc) when the records were written by the fused
-// compaction (-(slot + 1) in place of the size), else nullptr.
+// sums / labels: slot sums (slot_acc) and slot labels when the records were
+// written by the fused compaction (-(slot + 1) in place of the size), else
+// nullptr.
 int dm_launch_rank_sort(hipStream_t stream, long long* clusters, const long long* sums,
-                        const unsigned long long* d_count,
+                        const long long* labels, const unsigned long long* d_count,
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
                         int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
                         int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
@@ -292,7 +299,7 @@ int dm_grow_bucket_sort(dm_grid* g, int64_t n);
 // Row-bucket sort of the raw records (labels of rows [row_base, row_base +
 // rows)): same outputs, readback header and flags as dm_launch_rank_sort.
 int dm_launch_bucket_sort(dm_grid* g, long long* clusters, const long long* sums,
-                          const unsigned long long* d_count,
+                          const long long* labels, const unsigned long long* d_count,
                           int64_t max_records, int64_t row_base, int64_t rows, dm_cluster* out,
                           int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
                           int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,

@@ -78,3 +78,24 @@ __device__ inline int32_t dm_uf_root(const int32_t* par, int32_t x, unsigned lon
   dm_uf_flag(flag, bit);
   return x;
 }
+
+// Union keyed by node index instead of label: hook the root with the larger
+// index under the other.  Used where the labels are not known yet when the
+// unions run (the in-kernel tile-edge unions of k_frontier_tile: a
+// neighbour's slot labels are still being written); the set's label (its
+// min) is folded into the root afterwards (k_frontier_resolve).  Same
+// stale-read argument as dm_uf_unite: parents only ever point to a smaller
+// index, so the forest stays acyclic whatever order the CASes land in.
+__device__ inline void dm_uf_unite_idx(int32_t* par, int32_t a, int32_t b, unsigned long long* flag,
+                                       unsigned long long bit) {
+  for (int it = 0; it < kUfUniteBound; ++it) {
+    a = dm_uf_find(par, a, flag, bit);
+    b = dm_uf_find(par, b, flag, bit);
+    if (a == b) return;
+    if (a < b) { const int32_t t = a; a = b; b = t; }
+    const int32_t old = atomicCAS(&par[a], a, b);
+    if (old == a) return;
+    a = old;  // hooked meanwhile: climb from its real parent
+  }
+  dm_uf_flag(flag, bit);
+}
