@@ -407,6 +407,8 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   {
     const char* sep = getenv("DM_HEAVY_SEPARATE");
     g->fuse_heavy = !(sep && sep[0] == '1');
+    const char* fk = getenv("DM_FRONTIER_KERNEL");
+    g->frontier_kernel = fk && !strcmp(fk, "wave") ? 1 : (fk && !strcmp(fk, "wg") ? 2 : 0);
   }
   if ((rc = dev_alloc(&g->cnt, CNT_N, "counters"))) return fail(rc);
   if ((rc = dev_alloc(&g->ish, 2 * kShards * kShardWords, "shard counters"))) return fail(rc);

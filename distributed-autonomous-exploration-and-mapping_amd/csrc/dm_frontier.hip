@@ -31,6 +31,7 @@
 #include <algorithm>
 
 DM_PH_DECL(frontier)
+DM_PH_DECL(ftile)
 
 namespace {
 
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
     long long* __restrict__ slot_label, int32_t* slot_parent,
     long long* __restrict__ slot_own, long long* __restrict__ slot_acc,
     uint8_t* __restrict__ mask, int32_t* __restrict__ cell_slot, int32_t* __restrict__ edge_slot,
-    unsigned long long* cnt, unsigned long long* fsh) {
+    unsigned long long* cnt, unsigned long long* fsh, int count_stats) {
   __shared__ uint64_t s_unk[DM_TS + 2];    // row y at index y+1, bit c = column c
   __shared__ uint8_t s_unkL[DM_TS + 2];    // column -1
   __shared__ uint8_t s_unkR[DM_TS + 2];    // column 64
@@ -352,6 +353,10 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
     for (int r = tid; r < kMaxRoots; r += kFT) { szx[r] = 0; ssy[r] = 0; }
     __syncthreads();
     const int nruns = s_rbase[DM_TS];
+    if (count_stats && tid == 0) {
+      atomicAdd(&fsh[(blockIdx.x % kShards) * kShardWords + SH_RUNS], (unsigned long long)nruns);
+      atomicAdd(&fsh[(blockIdx.x % kShards) * kShardWords + SH_FTF], 1ull);
+    }
     DM_PH(dm_phase_acc_frontier, 2);
     DM_PH_COUNT(dm_phase_acc_frontier, 17, nruns);
     DM_PH_COUNT(dm_phase_acc_frontier, 18, 1);
@@ -579,7 +584,14 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
 // with a whole-tile LDS table, launched right after (same tile-edge
 // hand-off: it arrives later than every tile here, so it unites with them).
 constexpr int kFW = 4;            // tile-waves per workgroup
-constexpr int kRunsFast = 512;    // runs a tile-wave keeps in LDS
+constexpr int64_t kDenseRuns = 48;  // runs per frontier tile above which a pass is "dense"
+#ifndef DM_FL_RUNS
+#define DM_FL_RUNS 512
+#endif
+constexpr int kRunsFast = DM_FL_RUNS;  // runs a tile-wave keeps in LDS
+#ifndef DM_FL_STRIDED
+#define DM_FL_STRIDED 0
+#endif
 #ifndef DM_FL_OCC
 #define DM_FL_OCC 6               // workgroups per CU (LDS 24.3 KB each, <= 80 VGPRs)
 #endif
@@ -608,45 +620,83 @@ __device__ inline uint32_t zero_byte_bits(uint32_t w) {
   return (((t >> 7) * 0x00204081u) >> 21) & 0xFu;
 }
 
-// Unknown (-1) and free (0) bits of cells tx0..tx0+63 of row gy, and the
-// unknown bits of its cells tx0-1 / tx0+64.  Free bits only for band rows.
-__device__ inline void row_bits(const FGeom& g, const int8_t* __restrict__ state, const int8_t* __restrict__ halo,
-                                int32_t tx0, int32_t gy, uint64_t& U, uint64_t& Fr, uint32_t& uL, uint32_t& uR) {
-  U = 0ull;
-  Fr = 0ull;
-  uL = 0u;
-  uR = 0u;
-  const int8_t* rb = row_base(g, state, halo, gy);
-  if (!rb) return;
-  const int8_t* p = rb + tx0;
-  if (tx0 + 64 <= g.W && (reinterpret_cast<uintptr_t>(p) & 15) == 0) {
-    uint4 v[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = reinterpret_cast<const uint4*>(p)[q];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t wd[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int sh = 16 * q + 4 * k;
-        U |= (uint64_t)zero_byte_bits(~wd[k]) << sh;
-        Fr |= (uint64_t)zero_byte_bits(wd[k]) << sh;
-      }
-    }
-  } else {
-    for (int k = 0; k < 64 && tx0 + k < g.W; ++k) {
-      const int8_t b = p[k];
-      U |= (uint64_t)(b == -1) << k;
-      Fr |= (uint64_t)(b == 0) << k;
-    }
-  }
-  if (gy < 0 || gy >= g.R) Fr = 0ull;
-  if (tx0 > 0) uL = rb[tx0 - 1] == -1 ? 1u : 0u;
-  if (tx0 + 64 < g.W) uR = rb[tx0 + 64] == -1 ? 1u : 0u;
-}
-
 __device__ inline uint64_t dilate_row(uint64_t U, uint32_t uL, uint32_t uR) {
   return U | (U << 1) | (U >> 1) | (uint64_t)uL | ((uint64_t)uR << 63);
+}
+
+// 16 cells (16-B chunk k of tile row gy) as unknown bits | free bits << 16.
+__device__ inline uint32_t chunk_bits(const FGeom& g, const int8_t* __restrict__ state,
+                                      const int8_t* __restrict__ halo, int32_t tx0, int32_t gy, int k) {
+  const int8_t* rb = row_base(g, state, halo, gy);
+  if (!rb) return 0u;
+  const int32_t x0 = tx0 + 16 * k;
+  const int8_t* p = rb + x0;
+  uint32_t u = 0u, f = 0u;
+  if (x0 + 16 <= g.W && (reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      u |= zero_byte_bits(~wd[j]) << (4 * j);
+      f |= zero_byte_bits(wd[j]) << (4 * j);
+    }
+  } else {
+    for (int j = 0; j < 16 && x0 + j < g.W; ++j) {
+      u |= (uint32_t)(p[j] == -1) << j;
+      f |= (uint32_t)(p[j] == 0) << j;
+    }
+  }
+  if (gy < 0 || gy >= g.R) f = 0u;  // halo rows hold no band cells
+  return u | (f << 16);
+}
+
+// Unknown bit of cell (x, gy) (0 outside the grid / band + halos).
+__device__ inline uint32_t unknown_at(const FGeom& g, const int8_t* __restrict__ state,
+                                      const int8_t* __restrict__ halo, int32_t x, int32_t gy) {
+  if (x < 0 || x >= g.W) return 0u;
+  const int8_t* rb = row_base(g, state, halo, gy);
+  return rb && rb[x] == -1 ? 1u : 0u;
+}
+
+// The tile's rows, one per lane (lane y: U / Fr = unknown / free bits of tile
+// row y, uL / uR = unknown bits of its cells at x = -1 / 64), and for lane 0 /
+// lane 63 the unknown bits of rows -1 / 64 (Ue, eL, eR).  The interior loads
+// are coalesced: load q, lane l reads the 16-B chunk l % 4 of row 16q + l / 4
+// (16 rows x 64 B per wave instruction), then each lane gathers its row's four
+// chunks with shuffles.
+__device__ inline void tile_rows(const FGeom& g, const int8_t* __restrict__ state, const int8_t* __restrict__ halo,
+                                 int32_t tx0, int32_t ty0, int lane, uint64_t& U, uint64_t& Fr, uint32_t& uL,
+                                 uint32_t& uR, uint64_t& Ue, uint32_t& eL, uint32_t& eR) {
+  uint32_t wq[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) wq[q] = chunk_bits(g, state, halo, tx0, ty0 + 16 * q + (lane >> 2), lane & 3);
+  // rows -1 (lanes 0-3) and 64 (lanes 4-7), unknown bits only
+  const uint32_t we = lane < 8 ? chunk_bits(g, state, halo, tx0, lane < 4 ? ty0 - 1 : ty0 + DM_TS, lane & 3) : 0u;
+  // column halos of this lane's row; lanes 0 / 63 also the corners
+  uL = unknown_at(g, state, halo, tx0 - 1, ty0 + lane);
+  uR = unknown_at(g, state, halo, tx0 + DM_TS, ty0 + lane);
+  eL = 0u;
+  eR = 0u;
+  if (lane == 0 || lane == 63) {
+    const int32_t ey = lane == 0 ? ty0 - 1 : ty0 + DM_TS;
+    eL = unknown_at(g, state, halo, tx0 - 1, ey);
+    eR = unknown_at(g, state, halo, tx0 + DM_TS, ey);
+  }
+  U = 0ull;
+  Fr = 0ull;
+  Ue = 0ull;
+  const int src = (lane & 15) << 2, qsel = lane >> 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t t[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = __shfl(wq[q], src + k);
+    const uint32_t sel = qsel == 0 ? t[0] : qsel == 1 ? t[1] : qsel == 2 ? t[2] : t[3];
+    U |= (uint64_t)(sel & 0xFFFFu) << (16 * k);
+    Fr |= (uint64_t)(sel >> 16) << (16 * k);
+    const uint32_t te = __shfl(we, (lane == 63 ? 4 : 0) + k);
+    Ue |= (uint64_t)(te & 0xFFFFu) << (16 * k);
+  }
 }
 
 // Unions of the cells of one of this tile's edges with the neighbour tile's
@@ -696,21 +746,29 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
   uint64_t* rootw = s_rootw[w];
   int32_t* rootpre = s_rootpre[w];
   const int64_t nft = (int64_t)*list_n;
+  // list position of this wave's first tile: the four waves of a workgroup
+  // take four consecutive listed tiles (horizontal neighbours share the
+  // 128-byte lines of their rows and their halo columns: measured 129 vs
+  // 190 us on the explored C3 map against tiles a quarter list apart)
+#if DM_FL_STRIDED
+  const int64_t wid = (int64_t)w * gridDim.x + blockIdx.x;
+#else
   const int64_t wid = (int64_t)blockIdx.x * kFW + w;
+#endif
   const int shard = (int)(wid % kShards);
   const long long sh0 = (long long)shard * g.slot_per;
   const bool dense = g.want_mask || g.want_labels;
+  DM_PH_INIT();
   for (int64_t jj = wid; jj < nft; jj += (int64_t)gridDim.x * kFW) {
+    DM_PH(dm_phase_acc_ftile, 9);
     const int32_t tile = __builtin_amdgcn_readfirstlane(ftiles[jj]);
+    DM_PH_COUNT(dm_phase_acc_ftile, 16, 1);
     const int32_t tx = tile % g.TX, ty = tile / g.TX;
     const int32_t tx0 = tx * DM_TS, ty0 = ty * DM_TS;  // ty0 band-local
     // ---- 1. rows: lane y = tile row y (lanes 0 / 63 also rows -1 / 64) --------
-    uint64_t U, Fr;
-    uint32_t uL, uR;
-    row_bits(g, state, halo, tx0, ty0 + lane, U, Fr, uL, uR);
-    uint64_t Ue = 0ull, Fe;
-    uint32_t eL = 0u, eR = 0u;
-    if (lane == 0 || lane == 63) row_bits(g, state, halo, tx0, lane == 0 ? ty0 - 1 : ty0 + DM_TS, Ue, Fe, eL, eR);
+    uint64_t U, Fr, Ue;
+    uint32_t uL, uR, eL, eR;
+    tile_rows(g, state, halo, tx0, ty0, lane, U, Fr, uL, uR, Ue, eL, eR);
     // ---- 2. frontier bits: free & 3x3 dilation of unknown -------------------
     const uint64_t h = dilate_row(U, uL, uR);
     const uint64_t he = dilate_row(Ue, eL, eR);
@@ -719,6 +777,7 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
     if (lane == 0) hu = he;
     if (lane == 63) hd = he;
     const uint64_t F = Fr & (h | hu | hd);
+    DM_PH(dm_phase_acc_ftile, 0);
     if (__ballot(F != 0ull) == 0ull) continue;  // no frontier cell: nothing to publish
     // ---- 3. runs of set bits, numbered row-major ---------------------------
     const uint64_t st = run_starts(F);
@@ -731,6 +790,10 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
     }
     const int rbase = incl - c;
     const int nruns = __shfl(incl, 63);
+    if (lane == 0) {  // statistics for the next pass's kernel choice (shard sums)
+      atomicAdd(&fsh[shard * kShardWords + SH_RUNS], (unsigned long long)nruns);
+      atomicAdd(&fsh[shard * kShardWords + SH_FTF], 1ull);
+    }
     if (nruns > kRunsFast) {  // too many for this wave's LDS: the big kernel's
       if (lane == 0) big_list[atomicAdd(&cnt[CNT_BIG], 1ull)] = tile;
       continue;
@@ -740,6 +803,9 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
       acc[r] = 0ull;
     }
     wave_lds_sync();
+    DM_PH(dm_phase_acc_ftile, 1);
+    DM_PH_COUNT(dm_phase_acc_ftile, 17, 1);
+    DM_PH_COUNT(dm_phase_acc_ftile, 18, nruns);
     // ---- 4. union every run with the runs above it (extended by a cell) ------
     const uint64_t Fa = __shfl_up(F, 1);
     const uint64_t sta = __shfl_up(st, 1);
@@ -764,6 +830,7 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
       }
     }
     wave_lds_sync();
+    DM_PH(dm_phase_acc_ftile, 2);
     // ---- 5. compress; root bits; component id = rank of the root run ---------
     for (int r0 = 0; r0 < nruns; r0 += 64) {
       const int r = r0 + lane;
@@ -793,6 +860,7 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
       if (lane < nw) rootpre[lane] = inc2 - pc;
       ncomp = __shfl(inc2, 7);
     }
+    DM_PH(dm_phase_acc_ftile, 3);
     // ---- 6. per-component sums, in the root run's acc word -------------------
     {
       uint64_t s_ = st;
@@ -808,6 +876,7 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
       }
     }
     wave_lds_sync();
+    DM_PH(dm_phase_acc_ftile, 4);
     // ---- 7. slots: one per component from this wave's shard region -----------
     unsigned long long sb0 = 0ull;
     if (lane == 0) sb0 = atomicAdd(&fsh[shard * kShardWords + SH_SLOT], (unsigned long long)ncomp);
@@ -844,6 +913,7 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
         s_ &= s_ - 1;
       }
     }
+    DM_PH(dm_phase_acc_ftile, 5);
     // ---- 8. edges: publish, arrive, unite -------------------
     // sides [0] first row, [1] last row, [2] first col, [3] last col; lane =
     // position along the side.  The published slot ids are sc1 stores drained
@@ -869,6 +939,7 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
                                      __HIP_MEMORY_SCOPE_AGENT);
     if (fb[0] | fb[1] | fb[2] | fb[3]) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      DM_PH(dm_phase_acc_ftile, 6);
       const bool up = ty > 0, down = ty + 1 < g.TY, left = tx > 0, right = tx + 1 < g.TX;
       const int64_t NT = g.NT;
       // lane i arrives at relation i: 0 up, 1 down, 2 left, 3 right edge;
@@ -891,6 +962,7 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
         second = (old >> 2) == stamp && (old & (3ull ^ mine)) != 0ull;
       }
       const uint64_t sec = __ballot(second);
+      DM_PH(dm_phase_acc_ftile, 7);
       unsigned long long* uflag = &cnt[CNT_OVERFLOW];
 #pragma unroll
       for (int sd = 0; sd < 4; ++sd)
@@ -907,6 +979,7 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
                                             __HIP_MEMORY_SCOPE_AGENT);
         if (b >= 0) dm_uf_unite_idx(slot_parent, me, b, uflag, kOvUnionFind);
       }
+      DM_PH(dm_phase_acc_ftile, 8);
     }
     // ---- 9. band edge rows (cross-band merging) and optional dense outputs ---
     const int32_t gy = ty0 + lane;
@@ -924,7 +997,9 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
         if (gy == g.R - 1) edge_slot[g.W + gx] = sv;
       }
     }
+    DM_PH(dm_phase_acc_ftile, 10);
   }
+  DM_PHW_FLUSH(dm_phase_acc_ftile);
 }
 
 // Slot s is in use iff its offset inside its shard region is below that
@@ -1079,9 +1154,15 @@ __device__ inline void write_rb_header(int64_t K, int64_t cap, unsigned long lon
   unsigned long long* header = dm_rb_header(host_out);
   if (tid < ncnt) header[tid] = tid == sorted_idx ? (K <= cap ? 1ull : 0ull) : cnt[tid];
   if (tid == ncnt && fsh) {
-    unsigned long long most = 0;
-    for (int i = 0; i < kShards; ++i) most = max(most, fsh[i * kShardWords + SH_SLOT]);
+    unsigned long long most = 0, runs = 0, ftf = 0;
+    for (int i = 0; i < kShards; ++i) {
+      most = max(most, fsh[i * kShardWords + SH_SLOT]);
+      runs += fsh[i * kShardWords + SH_RUNS];
+      ftf += fsh[i * kShardWords + SH_FTF];
+    }
     header[ncnt] = most;
+    header[ncnt + 1] = runs;
+    header[ncnt + 2] = ftf;
   }
 }
 
@@ -1386,6 +1467,7 @@ static FGeom make_fgeom(const dm_grid* g, bool want_mask, bool want_labels) {
 }
 
 DM_PH_READER(frontier)
+DM_PH_READER(ftile)
 
 // Band edge-row labels (dm_get_edge_labels; only the host-side band merge
 // reads them), from the last frontier call's slots.
@@ -1471,20 +1553,35 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
   DM_HIP(dm_mark_tiles(g));
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));
-  // k_frontier_tile: one listed tile per wave (the dispatcher balances);
-  // k_frontier_tile_big: the tiles it left (more runs than a wave holds)
-  dm_timer_begin(g, "frontier_tile", &t);
-  hipLaunchKernelGGL(k_frontier_tile, dim3(grid_for(g->NT, kFW, 8192)), dim3(kFW * 64), 0, g->stream, fg, g->state,
-                     g->halo, g->ftiles, list_n, g->border, g->rel, (unsigned long long)g->fr_pass,
-                     g->slot_label, g->slot_parent, g->slot_own, g->slot_acc, g->mask, g->cell_slot, g->edge_slot,
-                     g->cnt, g->fsh, g->big_tiles);
-  dm_timer_end(g, &t);
-  DM_HIP(hipGetLastError());
-  dm_timer_begin(g, "frontier_big", &t);
-  hipLaunchKernelGGL(k_frontier_tile_big, dim3(grid_for(g->NT, 1, 512)), dim3(kFT), 0, g->stream, fg, g->state,
-                     g->halo, g->big_tiles, g->cnt + CNT_BIG, g->border, g->rel, (unsigned long long)g->fr_pass,
+  // Tile kernel, chosen from the last collected pass (both are exact for any
+  // map; they differ in speed): tiles whose frontiers are dense (more than
+  // kDenseRuns runs per tile with frontier cells on average, e.g. C3's ray
+  // fans, ~100) take the 256-thread kernel, one tile per workgroup; sparse
+  // ones (an explored map's few frontier tiles among many listed tiles, a
+  // 1 cm map's thin rays) the wave-per-tile kernel, which also screens the
+  // listed tiles without frontier cells at the rate of their loads and
+  // leaves tiles with more than kRunsFast runs to the 256-thread kernel.
+  const bool dense = g->frontier_kernel == 2 ||
+                     (g->frontier_kernel == 0 && g->ftf_hint > 0 && g->runs_hint > kDenseRuns * g->ftf_hint);
+  if (!dense) {
+    // one wave per listed tile: the grid follows the last collected pass's
+    // list length (+25 %; the kernel grid-strides, so any count is covered)
+    const int64_t want_waves = g->ftile_hint > 0 ? g->ftile_hint + g->ftile_hint / 4 + 64 : g->NT;
+    const int light_grid = grid_for(std::min<int64_t>(want_waves, g->NT), kFW, 8192);
+    dm_timer_begin(g, "frontier_tile", &t);
+    hipLaunchKernelGGL(k_frontier_tile, dim3(light_grid), dim3(kFW * 64), 0, g->stream, fg, g->state,
+                       g->halo, g->ftiles, list_n, g->border, g->rel, (unsigned long long)g->fr_pass,
+                       g->slot_label, g->slot_parent, g->slot_own, g->slot_acc, g->mask, g->cell_slot,
+                       g->edge_slot, g->cnt, g->fsh, g->big_tiles);
+    dm_timer_end(g, &t);
+    DM_HIP(hipGetLastError());
+  }
+  dm_timer_begin(g, dense ? "frontier_tile" : "frontier_big", &t);
+  hipLaunchKernelGGL(k_frontier_tile_big, dim3(dense ? grid_for(g->NT, 1, 8192) : grid_for(g->NT, 1, 512)),
+                     dim3(kFT), 0, g->stream, fg, g->state, g->halo, dense ? g->ftiles : g->big_tiles,
+                     dense ? list_n : g->cnt + CNT_BIG, g->border, g->rel, (unsigned long long)g->fr_pass,
                      g->slot_label, g->slot_parent, g->slot_own,
-                     g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh);
+                     g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh, dense ? 1 : 0);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   const int sgrid = grid_for(g->slot_cap, 256, 1024);
@@ -1546,6 +1643,10 @@ int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied) {
                                            "(dm_uf.h): this pass has no result");
   *n_clusters = (int64_t)g->h_cnt[CNT_CLUSTERS];
   g->sort_hint = *n_clusters;
+  // this pass's tile-list length (the other parity's counter is 0 or smaller)
+  g->ftile_hint = (int64_t)std::max(g->h_cnt[CNT_FL0], g->h_cnt[CNT_FL1]);
+  g->runs_hint = (int64_t)hdr[CNT_N + 1];
+  g->ftf_hint = (int64_t)hdr[CNT_N + 2];
   return DM_OK;
 }
 

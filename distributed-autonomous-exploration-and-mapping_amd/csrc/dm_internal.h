@@ -61,14 +61,18 @@ constexpr int kShards = 32;
 constexpr int kShardWords = 16;  // 128 B per shard
 static_assert(kShards * kShardWords == 512, "k_integrate_reset covers 512 shard words");
 enum { SH_U = 0, SH_T = 1, SH_TH = 2, SH_ACT = 3 };  // integrate shard fields
-enum { SH_SLOT = 0 };                                 // frontier shard fields
+// frontier shard fields: slots allocated, runs and tiles with frontier
+// cells (the next pass picks its tile kernel from their ratio)
+enum { SH_SLOT = 0, SH_RUNS = 1, SH_FTF = 2 };
 
 // Readback header in front of the sorted cluster records (device out_clu and
 // pinned h_out both point kRbRecords records into their allocation): the
 // frontier counters [CNT_N] and the fullest slot shard [CNT_N], written by
 // k_rank_sort into the mapped host buffer together with the first records.
-constexpr int kRbRecords = 6;  // 6 * 48 B = 288 B >= (CNT_N + 1) * 8 B
-static_assert(kRbRecords * sizeof(dm_cluster) >= (CNT_N + 1) * sizeof(unsigned long long), "readback header");
+// header words: [0, CNT_N) counters, [CNT_N] fullest slot shard, [CNT_N + 1]
+// runs, [CNT_N + 2] tiles with frontier cells (shard sums)
+constexpr int kRbRecords = 6;  // 6 * 48 B = 288 B >= (CNT_N + 3) * 8 B
+static_assert(kRbRecords * sizeof(dm_cluster) >= (CNT_N + 3) * sizeof(unsigned long long), "readback header");
 __host__ __device__ inline unsigned long long* dm_rb_header(dm_cluster* records) {
   return reinterpret_cast<unsigned long long*>(records - kRbRecords);
 }
@@ -223,6 +227,12 @@ struct dm_grid {
   int32_t* bs_idx = nullptr;      // [bs_cap] their record indices
   int64_t bs_cap = 0;
   int64_t sort_hint = 0, msort_hint = 0;  // clusters of the last band / merge readback
+  int64_t ftile_hint = 0;                 // listed tiles of the last collected frontier pass
+  int64_t runs_hint = 0, ftf_hint = 0;    // its runs and tiles with frontier cells
+  // tile kernel choice: 0 from those statistics, 1 always the wave-per-tile
+  // kernel, 2 always the 256-thread kernel (DM_FRONTIER_KERNEL=auto|wave|wg,
+  // read at dm_create, for A/B measurements; all three are exact)
+  int frontier_kernel = 0;
 
   // cross-band merge workspace (dm_merge.hip), sized nranks * rec_cap
   int64_t m_cap = 0;

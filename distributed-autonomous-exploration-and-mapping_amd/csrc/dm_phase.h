@@ -30,6 +30,15 @@
         if (_dm_acc[_k])                                                       \
           atomicAdd(&acc[(blockIdx.x % DM_PH_SHARDS) * DM_PH_SLOTS + _k], _dm_acc[_k]); \
   } while (0)
+// wave-level variant (kernels whose waves run independently): lane 0 of
+// every wave flushes its own accumulators
+#define DM_PHW_FLUSH(acc)                                                      \
+  do {                                                                         \
+    if (__lane_id() == 0)                                                      \
+      for (int _k = 0; _k < DM_PH_SLOTS; ++_k)                                 \
+        if (_dm_acc[_k])                                                       \
+          atomicAdd(&acc[((blockIdx.x * 4 + (threadIdx.x >> 6)) % DM_PH_SHARDS) * DM_PH_SLOTS + _k], _dm_acc[_k]); \
+  } while (0)
 #define DM_PH_READER(tu)                                                       \
   extern "C" int dm_debug_phases_##tu(unsigned long long* out, int n, int reset) { \
     static unsigned long long h[DM_PH_SHARDS * DM_PH_SLOTS];                   \
@@ -50,5 +59,6 @@
 #define DM_PH(acc, k) do {} while (0)
 #define DM_PH_COUNT(acc, k, v) do {} while (0)
 #define DM_PH_FLUSH(acc) do {} while (0)
+#define DM_PHW_FLUSH(acc) do {} while (0)
 #define DM_PH_READER(tu)
 #endif

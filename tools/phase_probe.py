@@ -24,6 +24,10 @@ NAMES = {
     "frontier": {0: "load+bitrows", 1: "F+run scan", 2: "enum runs", 3: "unions", 4: "compress",
                  5: "roots", 6: "sums+slot atomic", 7: "slot/border/edge writes", 8: "empty tile exit",
                  16: "#tiles", 17: "#runs", 18: "#tiles with F"},
+    "ftile": {9: "tile index load", 0: "loads + frontier bits", 1: "run scan + LDS init", 2: "row unions",
+              3: "compress + root ranks", 4: "sums", 5: "slot atomic + slot writes", 6: "border publish + drain",
+              7: "pair arrivals", 8: "edge unions", 10: "dense / band-edge writes",
+              16: "#tiles", 17: "#tiles with F", 18: "#runs"},
     "integrate": {0: "item setup (pieces, prefetch)", 1: "heavy accum", 2: "heavy slab flush",
                   3: "light accum", 5: "light: wait for cell loads", 4: "light apply", 8: "heavy_apply loads", 9: "heavy_apply apply", 10: "heavy_apply finish", 11: "plan: shard offsets",
                   12: "plan: list loads", 13: "plan: scans", 14: "plan: writes", 16: "#light items",
@@ -66,7 +70,7 @@ def main():
             if k >= 16:
                 print(f"  {name:28s} {v:12.1f} per step")
             else:
-                print(f"  {name:28s} {v * 0.01:12.1f} workgroup-us per step")
+                print(f"  {name:28s} {v * 0.01:12.1f} {'wave' if tu == 'ftile' else 'workgroup'}-us per step")
     m.close()
 
 
