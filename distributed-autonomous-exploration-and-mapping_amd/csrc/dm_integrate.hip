@@ -636,6 +636,9 @@ __device__ inline void heavy_quarter(const Geom& g, const ApplyArgs& p, int64_t 
 #ifndef DM_ACCUM_OCC
 #define DM_ACCUM_OCC 7
 #endif
+#ifndef DM_TICKET_RELEASE
+#define DM_TICKET_RELEASE 0
+#endif
 constexpr int kAccumPerCu = DM_ACCUM_OCC;  // resident k_tile_accum workgroups per CU (4 waves each)
 __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     Geom g, ApplyArgs p, const int4* __restrict__ list_a, int cnt_a, const int4* __restrict__ list_b,
@@ -710,19 +713,39 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
         }
       }
       DM_PH(dm_phase_acc_integrate, 2);
-      // the tile's last item to finish applies the merged slab.  Slab adds,
-      // ticket and the finisher's slab exchanges are all agent-scope atomics,
-      // performed at the memory side (MI355X_MICROARCH.md, global atomics):
-      // every wave waits for its adds (vmcnt 0) before the barrier behind
-      // which one lane takes the ticket, so the last ticket sees every add —
-      // no release fence (an L2 write-back per heavy item: C3's tile_accum
-      // 42 -> 172 us with __threadfence)
+      // The tile's last item to finish applies the merged slab.  Why no
+      // release / acquire fence is needed: every access to a slab word in a
+      // call is an agent-scope atomic RMW (the items' adds, the finisher's
+      // exchanges), and on gfx950 such an RMW is performed at the memory
+      // side, past the XCD's L2 (MI355X_MICROARCH.md §Global float atomics;
+      // atomics drop the L2 line, §Workgroup dispatch table), so there is no
+      // cached copy a release would have to write back or an acquire to
+      // invalidate.  What remains is ordering: a wave's non-returning RMW is
+      // counted in vmcnt until the memory side acknowledges it as performed,
+      // so after every wave's s_waitcnt vmcnt(0) and the barrier, all of this
+      // item's adds are performed before the ticket RMW is issued (the wait
+      // is what an agent-scope release does after its L2 write-back: LLVM
+      // AMDGPUUsage, GFX942 memory model, release = buffer_wbl2 sc1 +
+      // s_waitcnt vmcnt(0)).  The ticket RMWs are totally ordered on their
+      // address, so the item whose ticket returns n_it - 1 comes after every
+      // other item's adds, and its exchanges read their sums.  A release
+      // fence here (the L2 write-back of the items' other, plain stores)
+      // measured 42 -> 172 us per call with __threadfence (round 1) and
+      // DM_TICKET_RELEASE=1 builds that form for A/B; DM_HEAVY_SEPARATE=1
+      // (read at dm_create) applies the slabs in a separate k_heavy_apply
+      // launch instead — the kernel boundary orders everything.
       if (heavy_done) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
           const int32_t n_it = (tile_count[tile] + kChunk - 1) / kChunk;  // k_plan's item count
+#if DM_TICKET_RELEASE
+          s_last = __hip_atomic_fetch_add(&heavy_done[heavy >> 1], 1, __ATOMIC_RELEASE,
+                                          __HIP_MEMORY_SCOPE_AGENT) == n_it - 1;
+          if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#else
           s_last = atomicAdd(&heavy_done[heavy >> 1], 1) == n_it - 1;
+#endif
         }
         __syncthreads();
         if (s_last) {

@@ -384,3 +384,34 @@ def test_heavy_apply_fused_and_separate(oracle_lib, monkeypatch, S, separate):
             assert m.last_stats()["heavy_tiles"] >= (1 if S >= 17 else 3)
         assert_map_equal(m, om)
         assert_frontiers_equal(m.frontiers(want_mask=True, want_labels=True), *om.frontiers())
+
+
+def test_heavy_ticket_under_uneven_load(oracle_lib):
+    """The fused heavy apply's ticket hand-off (csrc/dm_integrate.hip,
+    k_tile_accum) while another stream keeps CUs busy with long GEMMs, so
+    the heavy items of one tile run on different XCDs at very different
+    times: 12 calls, each bit-exact against the oracle (17 co-located scans:
+    wide slabs; one sensor tile split into 272 items)."""
+    import torch
+
+    p = cases.make_params(600, 500)
+    rng = np.random.Generator(np.random.PCG64(2024))
+    N = 4096
+    amin, inc = 0.0, float(np.float32(2 * np.pi / (N - 1)))
+    om = oracle_lib.OracleMap(p)
+    side = torch.cuda.Stream()
+    a = torch.randn(4096, 4096, device="cuda")
+    with dm.OccupancyMapper(p) as m:
+        for k in range(12):
+            with torch.cuda.stream(side):
+                for _ in range(3 + k % 4):
+                    a = torch.tanh(a @ a * 1e-3)
+            S = 17 if k % 2 == 0 else 9
+            poses = np.tile(np.array([[0.013 + 0.3 * k, -0.021, 0.3]]), (S, 1))
+            poses[:, 2] += rng.uniform(-0.01, 0.01, S)
+            ranges = (np.round(rng.uniform(0.05, 8.0, (S, N)) * 1000) / 1000).astype(np.float32)
+            assert m.integrate(poses, ranges, amin, inc) == om.integrate(poses, ranges, amin, inc)
+            assert m.last_stats()["heavy_tiles"] >= 1
+            np.testing.assert_array_equal(m.logodds().view(np.uint32), om.L.view(np.uint32))
+        torch.cuda.synchronize()
+        assert_map_equal(m, om)

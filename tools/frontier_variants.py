@@ -56,6 +56,23 @@ def child():
     for p4, r in dpool:
         m.integrate_device(p4.data_ptr(), S, r.data_ptr(), N, amin, inc)
     m.synchronize()
+    # integrate alone (the pool replayed), then frontier passes on that map
+    ti = []
+    for k in range(20):
+        p4, r = dpool[k % len(dpool)]
+        a = time.perf_counter()
+        m.integrate_device(p4.data_ptr(), S, r.data_ptr(), N, amin, inc)
+        m.synchronize()
+        ti.append(time.perf_counter() - a)
+    m.profile(True)
+    m.profile_reset()
+    for k in range(12):
+        p4, r = dpool[k % len(dpool)]
+        m.integrate_device(p4.data_ptr(), S, r.data_ptr(), N, amin, inc)
+    k = m.profile_read()
+    m.profile(False)
+    out["integrate"] = {"wall_ms": float(np.median(ti)) * 1e3,
+                        "kernels_us": {n_: round(t / max(1, c) * 1e3, 1) for n_, (c, t) in k.items()}}
     passes("c3")
     m.set_state(synth.explored_state(world, G, G, res, -half, -half, seed=77))
     passes("explored")

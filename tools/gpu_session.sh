@@ -19,8 +19,8 @@ ok() { [ "$1" -eq 0 ]; }
 for s in "$@"; do
   case $s in
     tests|tests:*)
-      k=""; [ "$s" != tests ] && k="-k ${s#tests:}"
-      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v $k --timeout 400 --timeout-method thread \
+      k=(); [ "$s" != tests ] && k=(-k "${s#tests:}")
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v "${k[@]}" --timeout 400 --timeout-method thread \
         > $OUT/pytest_gpu.log 2>&1
       rc=$?; echo "tests rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $OUT/pytest_gpu.log | tail -8
       ok $rc || exit $rc ;;
