@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="budget for the CPU-oracle baseline sample (0 disables)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--depth", type=int, default=1,
+                    help="frontier passes in flight in the pipelined steps (1 or 2; libdm keeps 2 readback slots)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the steps back to back without overlapping step k+1's integrate "
                          "front-end with step k's frontier pass")
@@ -197,13 +199,18 @@ def main():
                 integ(k0 + k)
                 fr = mapper.frontiers()
             return fr
-        integ(k0)
-        mapper.frontiers_begin()
-        for k in range(1, n):
+        # up to `depth` frontier passes in flight: pass k is collected after
+        # batch k + depth was enqueued, so the host never waits for the pass
+        # it just started before enqueuing the next batch's front-end
+        depth = max(1, min(args.depth, n))
+        fr = None
+        for k in range(n):
             integ(k0 + k)
-            mapper.frontiers_end()
+            if k >= depth:
+                mapper.frontiers_end()
             mapper.frontiers_begin()
-        fr = mapper.frontiers_end()
+        for _ in range(min(depth, n)):
+            fr = mapper.frontiers_end()
         # None: the pass overflowed a capacity (grown now); rerun on this map
         return fr if fr is not None else mapper.frontiers()
 
@@ -396,8 +403,9 @@ def main():
             "exchange": ("device: RCCL all-gather of halo rows + export records, dm_merge_bands"
                          if world_size > 1 else None),
             "exchange_fallbacks": getattr(mapper, "fallbacks", 0),
-            "pipelined": ("step k+1's integrate front-end overlaps step k's frontier pass "
-                          "(dm_set_overlap + dm_frontiers_begin/_end)") if pipelined else None,
+            "pipelined": (f"step k+1's integrate front-end overlaps step k's frontier pass "
+                          f"(dm_set_overlap + dm_frontiers_begin/_end), {min(args.depth, 2)} passes in flight")
+            if pipelined else None,
             "cpu_baseline": cpu,
             "gen_seconds": t_gen,
         }

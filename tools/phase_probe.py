@@ -22,7 +22,7 @@ from dm import synth  # noqa: E402
 
 NAMES = {
     "frontier": {0: "load+bitrows", 1: "F+run scan", 2: "enum runs", 3: "unions", 4: "compress",
-                 5: "roots", 6: "sums+slot atomic", 7: "slot/border/edge writes", 8: "empty tile exit",
+                 5: "roots", 6: "sums+slot atomic", 7: "slot writes + edge unions + band rows", 8: "empty tile exit",
                  16: "#tiles", 17: "#runs", 18: "#tiles with F"},
     "ftile": {9: "tile index load", 0: "loads + frontier bits", 1: "run scan + LDS init", 2: "row unions",
               3: "compress + root ranks", 4: "sums", 5: "slot atomic + slot writes", 6: "border publish + drain",

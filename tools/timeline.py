@@ -41,7 +41,7 @@ def gaps(a, b):
 
 
 for a, b in (("k_rank_sort", "k_tile_accum"), ("k_heavy_apply", "k_frontier_prep"),
-             ("k_frontier_prep", "k_frontier_tile"), ("k_scatter", "k_tile_accum")):
+             ("k_frontier_prep", "k_frontier_tile_big"), ("k_frontier_tile_big", "k_frontier_resolve"), ("k_frontier_resolve", "k_rank_sort"), ("k_tile_accum", "k_frontier_prep"), ("k_scatter", "k_tile_accum")):
     g = gaps(a, b)[5:30]
     if g:
         print(f"gap {a} -> {b}: median {statistics.median(g):.1f} us, min {min(g):.1f}")
