@@ -40,8 +40,8 @@ TILE_APPLY_BYTES_PER_TOUCHED = 25.0  # read h,m,L; write L, st
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--grid", type=int, default=16384, help="cells per side of each GPU's band")
     ap.add_argument("--robots", type=int, default=64)
     ap.add_argument("--beams", type=int, default=4096)

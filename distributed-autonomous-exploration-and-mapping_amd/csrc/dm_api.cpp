@@ -20,12 +20,20 @@
 #include <stdlib.h>
 
 hipError_t dm_copy_shards(dm_grid* g) {
-  return hipMemcpyAsync(g->h_sh, g->ish, sizeof(unsigned long long) * 2 * kShards * kShardWords,
-                        hipMemcpyDeviceToHost, g->stream);
+  const size_t bytes = sizeof(unsigned long long) * kShards * kShardWords;
+  hipError_t e = hipMemcpyAsync(g->h_sh, g->iw[g->iw_cur].sh, bytes, hipMemcpyDeviceToHost, g->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(g->h_sh + kShards * kShardWords, g->fsh, bytes, hipMemcpyDeviceToHost, g->stream);
+  return e;
 }
 
 namespace {
 thread_local std::string t_err;
+
+bool dm_env_off(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] == '0';
+}
 
 struct HostCluster {
   long long label, size, sum_x, sum_y;
@@ -101,8 +109,10 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   }
   const int64_t segs = nb * per_beam;
   if (segs > g->segs_cap) {
-    int rc = dev_alloc(&g->pieces, segs, "ray pieces");
-    if (rc) return rc;
+    for (auto& w : g->iw) {
+      int rc = dev_alloc(&w.pieces, segs, "ray pieces");
+      if (rc) { g->segs_cap = 0; return rc; }
+    }
     g->segs_cap = segs;
   }
   const int64_t side = ceil_div(2 * (int64_t)g->nmax + 1, DM_TILE) + 1;
@@ -110,27 +120,33 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   if (act < 1) act = 1;
   if (act > g->act_cap) {
     int rc = dev_alloc(&g->act_raw, act * kShards, "first-touch lists");
-    if (!rc) rc = dev_alloc(&g->litems, act, "light work items");
-    if (rc) return rc;
+    for (auto& w : g->iw)
+      if (!rc) rc = dev_alloc(&w.litems, act, "light work items");
+    if (rc) { g->act_cap = 0; return rc; }
     g->act_cap = act;
   }
-  // heavy work items / heavy tiles (exact bounds: a heavy tile has > 256
-  // pieces, its items ceil(pieces / 256) <= pieces / 256 + 1)
-  const int64_t chunk = 256;
-  const int64_t heavy = std::max<int64_t>(1, std::min<int64_t>(g->act_cap, segs / (chunk + 1) + 1));
-  const int64_t hitems = segs / chunk + heavy + 1;
+  // work items of medium and heavy tiles (exact bounds: such a tile has
+  // more than kIntegrateChunk pieces, its items ceil(pieces / chunk) <=
+  // pieces / chunk + 1), heavy tiles (more than kIntegrateMedium pieces)
+  const int64_t chunk = kIntegrateChunk;
+  const int64_t heavy = std::max<int64_t>(1, std::min<int64_t>(g->act_cap, segs / (kIntegrateMedium + 1) + 1));
+  const int64_t hitems = segs / chunk + segs / (chunk + 1) + 2;
   if (hitems > g->hitem_cap) {
-    int rc = dev_alloc(&g->hitems, hitems, "heavy work items");
-    if (rc) return rc;
+    for (auto& w : g->iw) {
+      int rc = dev_alloc(&w.hitems, hitems, "heavy work items");
+      if (rc) { g->hitem_cap = 0; return rc; }
+    }
     g->hitem_cap = hitems;
   }
   if (heavy > g->heavy_cap) {
-    int rc = dev_alloc(&g->heavy_list, heavy, "heavy tiles");
-    if (!rc) rc = dev_alloc(&g->slabs, heavy * 2 * DM_TILE * DM_TILE, "heavy-tile slabs");
-    if (!rc) rc = dev_alloc(&g->heavy_done, heavy, "heavy-tile item tickets");
-    if (rc) return rc;
-    DM_HIP(hipMemset(g->slabs, 0, sizeof(uint32_t) * (size_t)(heavy * 2 * DM_TILE * DM_TILE)));
-    DM_HIP(hipMemset(g->heavy_done, 0, sizeof(int32_t) * (size_t)heavy));
+    for (auto& w : g->iw) {
+      int rc = dev_alloc(&w.heavy_list, heavy, "heavy tiles");
+      if (!rc) rc = dev_alloc(&w.slabs, heavy * 2 * DM_TILE * DM_TILE, "heavy-tile slabs");
+      if (!rc) rc = dev_alloc(&w.heavy_done, heavy, "heavy-tile item tickets");
+      if (rc) { g->heavy_cap = 0; return rc; }
+      DM_HIP(hipMemset(w.slabs, 0, sizeof(uint32_t) * (size_t)(heavy * 2 * DM_TILE * DM_TILE)));
+      DM_HIP(hipMemset(w.heavy_done, 0, sizeof(int32_t) * (size_t)heavy));
+    }
     g->heavy_cap = heavy;
   }
   if (2 * (int64_t)N > g->trig_cap) {
@@ -290,16 +306,28 @@ int check_integrate_args(int32_t S, int32_t N, const void* poses, const void* ra
   return DM_OK;
 }
 
-int finish_counts(dm_grid* g, uint64_t* U, uint64_t* T) {
+// Copies both counter blocks (frontier, then the last integrate call's) and
+// both shard blocks into the pinned mirrors and waits for them.
+int read_counters(dm_grid* g) {
   DM_HIP(hipMemcpyAsync(g->h_cnt, g->cnt, sizeof(unsigned long long) * CNT_N,
+                        hipMemcpyDeviceToHost, g->stream));
+  DM_HIP(hipMemcpyAsync(g->h_cnt + CNT_N, g->iw[g->iw_cur].cnt, sizeof(unsigned long long) * CNT_N,
                         hipMemcpyDeviceToHost, g->stream));
   DM_HIP(dm_copy_shards(g));
   DM_HIP(hipStreamSynchronize(g->stream));
-  if (g->h_cnt[CNT_IOVERFLOW]) {
+  return DM_OK;
+}
+
+int finish_counts(dm_grid* g, uint64_t* U, uint64_t* T) {
+  int rc = read_counters(g);
+  if (rc) return rc;
+  const unsigned long long* ic = g->h_cnt + CNT_N;
+  if (ic[CNT_IOVERFLOW]) {
     // cannot happen with the bounds in grow_integrate; keep the map consistent anyway
-    (void)hipMemset(g->tile_count, 0, sizeof(int32_t) * (size_t)g->NT);
-    return dm_set_error(DM_ERR_CAPACITY, "integrate workspace overflow (flags %llu)",
-                        (unsigned long long)g->h_cnt[CNT_IOVERFLOW]);
+    (void)hipMemset(g->iw[g->iw_cur].tile_count, 0, sizeof(int32_t) * (size_t)g->NT);
+    return dm_set_error(DM_ERR_CAPACITY, "integrate workspace overflow (flags %llu: 1 first-touch "
+                        "list, 2 pieces, 4 work lists, 8 front-end hand-off timed out)",
+                        (unsigned long long)ic[CNT_IOVERFLOW]);
   }
   if (U) *U = dm_shard_sum(g->h_sh, SH_U);
   if (T) *T = dm_shard_sum(g->h_sh, SH_T);
@@ -401,18 +429,27 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   };
   if ((rc = dev_alloc(&g->L, cells, "log-odds"))) return fail(rc);
   if ((rc = dev_alloc(&g->state, cells, "state"))) return fail(rc);
-  if ((rc = dev_alloc(&g->tile_count, g->NT, "tile counts"))) return fail(rc);
-  if ((rc = dev_alloc(&g->tile_cur, g->NT, "tile bin cursors"))) return fail(rc);
+  for (auto& w : g->iw) {
+    if ((rc = dev_alloc(&w.tile_count, g->NT, "tile counts"))) return fail(rc);
+    if ((rc = dev_alloc(&w.tile_cur, g->NT, "tile bin cursors"))) return fail(rc);
+    if ((rc = dev_alloc(&w.cnt, CNT_N, "integrate counters"))) return fail(rc);
+    if ((rc = dev_alloc(&w.sh, kShards * kShardWords, "integrate shard counters"))) return fail(rc);
+    DM_HIP(hipMemset(w.cnt, 0, sizeof(unsigned long long) * CNT_N));
+    DM_HIP(hipMemset(w.sh, 0, sizeof(unsigned long long) * kShards * kShardWords));
+  }
   if ((rc = dev_alloc(&g->tile_free, g->NT, "tile free counts"))) return fail(rc);
   {
     const char* sep = getenv("DM_HEAVY_SEPARATE");
     g->fuse_heavy = !(sep && sep[0] == '1');
+    g->fe_gate = !dm_env_off("DM_FE_GATE");
     const char* fk = getenv("DM_FRONTIER_KERNEL");
     g->frontier_kernel = fk && !strcmp(fk, "wave") ? 1 : (fk && !strcmp(fk, "wg") ? 2 : 0);
   }
   if ((rc = dev_alloc(&g->cnt, CNT_N, "counters"))) return fail(rc);
-  if ((rc = dev_alloc(&g->ish, 2 * kShards * kShardWords, "shard counters"))) return fail(rc);
-  g->fsh = g->ish + kShards * kShardWords;
+  if ((rc = dev_alloc(&g->fe_flag, 16, "front-end completion word"))) return fail(rc);
+  DM_HIP(hipMemset(g->fe_flag, 0, sizeof(unsigned long long) * 16));
+  if ((rc = dev_alloc(&g->fsh, kShards * kShardWords, "frontier shard counters"))) return fail(rc);
+  DM_HIP(hipMemset(g->fsh, 0, sizeof(unsigned long long) * kShards * kShardWords));
   if ((rc = dev_alloc(&g->ftiles, g->NT, "frontier tiles"))) return fail(rc);
   if ((rc = dev_alloc(&g->big_tiles, g->NT, "frontier big tiles"))) return fail(rc);
   if ((rc = dev_alloc(&g->border, g->NT * 256, "frontier borders"))) return fail(rc);
@@ -427,7 +464,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   for (int sl = 0; sl <= dm_grid::kRbSlots; ++sl)
     if ((rc = grow_host_out(g, sl, 1 << 14))) return fail(rc);
   dm_select_slot(g, 0);
-  e = hipHostMalloc((void**)&g->h_cnt, sizeof(unsigned long long) * CNT_N, hipHostMallocDefault);
+  e = hipHostMalloc((void**)&g->h_cnt, sizeof(unsigned long long) * 2 * CNT_N, hipHostMallocDefault);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipHostMalloc(counters)"));
   e = hipHostMalloc((void**)&g->h_sh, sizeof(unsigned long long) * 2 * kShards * kShardWords,
                     hipHostMallocDefault);
@@ -437,16 +474,25 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipHostMalloc(merge counters)"));
   e = hipDeviceGetAttribute(&g->n_cu, hipDeviceAttributeMultiprocessorCount, device);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipDeviceGetAttribute(multiprocessor count)"));
-  e = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking);
+  // Stream priorities (DM_STREAM_PRIO=0 turns them off, for A/B): the map
+  // chain (accumulation, frontier pass) high, the integrate front-end low,
+  // so a front-end enqueued early fills what the map chain leaves idle
+  // instead of competing with the accumulation for its CUs.
+  int prio_lo = 0, prio_hi = 0;
+  {
+    const char* sp = getenv("DM_STREAM_PRIO");
+    if (!(sp && sp[0] == '0')) (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  }
+  e = hipStreamCreateWithPriority(&g->stream, hipStreamNonBlocking, prio_hi);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate"));
   g->own_stream = true;
-  e = hipStreamCreateWithFlags(&g->fe_stream, hipStreamNonBlocking);
+  e = hipStreamCreateWithPriority(&g->fe_stream, hipStreamNonBlocking, prio_lo);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(front-end)"));
-  // ev_fe / ev_tiles only order the two streams on the device: no system-
+  // ev_fe / ev_free only order the two streams on the device: no system-
   // scope fence (no host-visible cache writeback at every step).  The host
   // waits on a readback slot's event and then reads mapped host memory:
   // default fences.
-  for (hipEvent_t* ev : {&g->ev_fe, &g->ev_tiles}) {
+  for (hipEvent_t* ev : {&g->ev_fe, &g->iw[0].ev_free, &g->iw[1].ev_free}) {
     e = hipEventCreateWithFlags(ev, hipEventDisableTiming | hipEventDisableSystemFence);
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
   }
@@ -469,7 +515,7 @@ int dm_destroy(dm_grid* g) {
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   if (g->fe_stream) (void)hipStreamSynchronize(g->fe_stream);
   for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
-  for (hipEvent_t ev : {g->ev_fe, g->ev_tiles})
+  for (hipEvent_t ev : {g->ev_fe, g->iw[0].ev_free, g->iw[1].ev_free})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& r : g->rb) {
     if (r.ev) (void)hipEventDestroy(r.ev);
@@ -478,16 +524,19 @@ int dm_destroy(dm_grid* g) {
     dev_free(r.m_out);
   }
   if (g->fe_stream) (void)hipStreamDestroy(g->fe_stream);
-  dev_free(g->L); dev_free(g->state); dev_free(g->tile_count); dev_free(g->tile_cur);
-  dev_free(g->tile_free); dev_free(g->cnt); dev_free(g->beams); dev_free(g->blk_hist); dev_free(g->blk_n); dev_free(g->pieces);
+  for (auto& w : g->iw) {
+    dev_free(w.pieces); dev_free(w.hitems); dev_free(w.litems); dev_free(w.heavy_list); dev_free(w.slabs);
+    dev_free(w.heavy_done); dev_free(w.tile_count); dev_free(w.tile_cur); dev_free(w.cnt); dev_free(w.sh);
+  }
+  dev_free(g->L); dev_free(g->state);
+  dev_free(g->tile_free); dev_free(g->cnt); dev_free(g->beams); dev_free(g->blk_hist); dev_free(g->blk_n);
   dev_free(g->trig);
-  dev_free(g->hitems); dev_free(g->litems); dev_free(g->heavy_list); dev_free(g->slabs); dev_free(g->heavy_done);
   dev_free(g->pose4); dev_free(g->ranges); 
   dev_free(g->bs_rows); dev_free(g->bs_key); dev_free(g->bs_idx);
   dev_free(g->border); dev_free(g->rel); dev_free(g->ftiles); dev_free(g->big_tiles); dev_free(g->slot_label); dev_free(g->slot_parent); dev_free(g->slot_root);
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
   dev_free(g->edge_slot); dev_free(g->edge_label); dev_free(g->mask); dev_free(g->labels);
-  dev_free(g->halo); dev_free(g->ish); dev_free(g->act_raw);
+  dev_free(g->halo); dev_free(g->fsh); dev_free(g->fe_flag); dev_free(g->act_raw);
   dev_free(g->slot_k); dev_free(g->rank_of); dev_free(g->m_parent); dev_free(g->m_label);
   dev_free(g->m_acc); dev_free(g->m_clu); dev_free(g->m_cnt);
   if (g->h_mcnt) (void)hipHostFree(g->h_mcnt);
@@ -508,7 +557,9 @@ int dm_reset(dm_grid* g) {
   const int64_t cells = g->W * g->R;
   DM_HIP(hipMemsetAsync(g->L, 0, sizeof(float) * (size_t)cells, g->stream));
   DM_HIP(hipMemsetAsync(g->state, 0xFF, (size_t)cells, g->stream));
-  DM_HIP(hipMemsetAsync(g->tile_count, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
+  DM_HIP(hipStreamSynchronize(g->fe_stream));
+  for (auto& w : g->iw)
+    DM_HIP(hipMemsetAsync(w.tile_count, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
   DM_HIP(hipMemsetAsync(g->tile_free, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
   DM_HIP(hipMemsetAsync(g->cnt, 0, sizeof(unsigned long long) * CNT_N, g->stream));
   DM_HIP(hipStreamSynchronize(g->stream));
@@ -575,10 +626,8 @@ int enqueue_host_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N
     hp[4 * s + 2] = cos(yaw);  // C library, as the oracle
     hp[4 * s + 3] = sin(yaw);
   }
-  if (g->overlap) {  // pose4 / ranges of the last call read
-    DM_HIP(dm_mark_tiles(g));
-    DM_HIP(hipStreamWaitEvent(fs, g->ev_tiles, 0));
-  }
+  // pose4 / ranges are read by the front-end only, which runs on fs: the
+  // last call's reads are ahead of these copies in stream order
   if (S > 0)
     DM_HIP(hipMemcpyAsync(g->pose4, hp, sizeof(double) * 4 * (size_t)S, hipMemcpyHostToDevice, fs));
   DM_HIP(hipEventRecord(g->ev_pose[slot], fs));
@@ -637,16 +686,14 @@ int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out) {
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (cap > 0 && !out) return dm_set_error(DM_ERR_INVALID_ARG, "out is NULL");
-  DM_HIP(hipMemcpyAsync(g->h_cnt, g->cnt, sizeof(unsigned long long) * CNT_N,
-                        hipMemcpyDeviceToHost, g->stream));
-  DM_HIP(dm_copy_shards(g));
-  DM_HIP(hipStreamSynchronize(g->stream));
+  if ((rc = read_counters(g))) return rc;
   const unsigned long long* fs = g->h_sh + kShards * kShardWords;
-  const uint64_t items = g->h_cnt[CNT_ITEMS] + g->h_cnt[CNT_LITEMS];  // heavy + light work items
+  const unsigned long long* ic = g->h_cnt + CNT_N;  // the last integrate call's counters
+  const uint64_t items = ic[CNT_ITEMS] + ic[CNT_LITEMS];  // heavy + light work items
   const uint64_t v[10] = {dm_shard_sum(g->h_sh, SH_U),  dm_shard_sum(g->h_sh, SH_T),
-                          dm_shard_sum(g->h_sh, SH_TH), g->h_cnt[CNT_SEGS],
-                          g->h_cnt[CNT_ACTIVE],         items,
-                          g->h_cnt[CNT_HEAVY],          g->h_cnt[g->fparity ? CNT_FL1 : CNT_FL0],
+                          dm_shard_sum(g->h_sh, SH_TH), ic[CNT_SEGS],
+                          ic[CNT_ACTIVE],               items,
+                          ic[CNT_HEAVY],                g->h_cnt[g->fparity ? CNT_FL1 : CNT_FL0],
                           dm_shard_sum(fs, SH_SLOT),    g->h_cnt[CNT_CLUSTERS]};
   for (int32_t i = 0; i < cap && i < 10; ++i) out[i] = v[i];
   if (n_out) *n_out = 10;
@@ -762,6 +809,7 @@ int dm_frontiers_export_device(dm_grid* g, void* d_export, int64_t rec_cap) {
   dm_select_slot(g, (g->rb_head + g->rb_count) % dm_grid::kRbSlots);
   if ((rc = dm_enqueue_frontiers(g, false, false))) return rc;
   if ((rc = dm_launch_export(g, d_export, rec_cap))) return rc;
+  DM_HIP(dm_mark_ws_free(g));
   g->frontier_valid = true;
   return DM_OK;
 }
@@ -882,6 +930,10 @@ int dm_frontiers_begin(dm_grid* g) {
   if ((rc = dm_enqueue_frontiers(g, false, false))) return rc;
   dm_grid::RbSlot& r = g->rb[slot];
   DM_HIP(hipEventRecord(r.ev, g->stream));
+  // the integrate workspaces' accumulations are ahead of this event: it
+  // frees them (a marker right behind the write-heavy map update would cost
+  // the stream several microseconds)
+  DM_HIP(dm_mark_ws_free(g, r.ev));
   r.kind = 1;
   r.seq = g->integrate_seq;
   r.gen = g->rb_gen;
@@ -936,7 +988,10 @@ int dm_set_overlap(dm_grid* g, int32_t on) {
   DM_HIP(hipStreamSynchronize(g->stream));
   DM_HIP(hipStreamSynchronize(g->fe_stream));
   g->overlap = on != 0;
-  g->tiles_mark_pending = false;
+  for (auto& w : g->iw) {
+    w.free_owed = false;
+    w.free_wait = nullptr;
+  }
   return DM_OK;
 }
 

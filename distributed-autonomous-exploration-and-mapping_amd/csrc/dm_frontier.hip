@@ -1547,10 +1547,6 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
                      g->edge_slot, g->slot_parent, g->slot_cap);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
-  // the last integrate call's tile workspace is free once the map update
-  // (ahead of the prep in stream order) is done: the next call's front-end
-  // may start now, beside the rest of this pass
-  DM_HIP(dm_mark_tiles(g));
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));
   // Tile kernel, chosen from the last collected pass (both are exact for any

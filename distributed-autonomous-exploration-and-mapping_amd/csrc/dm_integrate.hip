@@ -196,12 +196,12 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
 // pieces, exclusive scans of: c_j (bin offsets), heavy items, light items,
 // heavy ordinals.  Heavy items are listed first (they are the long ones).
 // Item = {tile, first piece, pieces, slab code or -1 (light / medium)}.
-constexpr int kChunk = 256;
+constexpr int kChunk = kIntegrateChunk;
 // Tiles with more pieces than kChunk but at most kMedium (the ring around a
 // sensor: rays fan out, so a per-thread walk does not pile onto one cell) are
 // one item walked in rounds; only tiles beyond kMedium (the sensor's own)
 // are split over workgroups and merged in a slab.
-constexpr int kMedium = 1024;
+constexpr int kMedium = kIntegrateMedium;
 static_assert(kMedium < 65536, "packed 16-bit LDS counts of medium tiles");
 constexpr int kTileWords = DM_TS * kLdsPitch;
 constexpr int kQuarter = 256;  // threads of an apply workgroup (= kChunk)
@@ -864,6 +864,36 @@ __global__ __launch_bounds__(256) void k_integrate_reset(unsigned long long* cnt
   if (i < kShards * kShardWords) ish[i] = 0ull;
 }
 
+// Front-end -> accumulation hand-off across the two streams (dm_set_overlap)
+// without a cross-queue event wait, which holds the map stream ~10 us even
+// when the front-end finished long before.  k_fe_signal runs on the
+// front-end stream after k_scatter (the kernel boundary has written its
+// outputs back) and stores the call's sequence number; k_fe_gate, one lane
+// on the map stream right before k_tile_accum, polls that word and exits;
+// k_tile_accum's own kernel-boundary acquire then sees the front-end's
+// outputs.  No deadlock: the gate holds one workgroup slot, and everything
+// the front-end waits for is ahead of the gate on the map stream.  Bounded:
+// after kFeGateTicks of the 100 MHz wall clock the gate sets flag 8 in the
+// call's CNT_IOVERFLOW (DM_ERR_CAPACITY at dm_last_counts) and exits.
+constexpr unsigned long long kFeGateTicks = 500000000ull;  // 5 s
+
+__global__ __launch_bounds__(64) void k_fe_signal(unsigned long long* flag, unsigned long long seq) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(64) void k_fe_gate(const unsigned long long* flag, unsigned long long seq,
+                                                unsigned long long* cnt) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = wall_clock64();
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < seq) {
+    __builtin_amdgcn_s_sleep(2);
+    if (wall_clock64() - t0 > kFeGateTicks) {
+      atomicOr(&cnt[CNT_IOVERFLOW], 8ull);
+      return;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_recount(Geom g, const int8_t* __restrict__ state,
                                                  int32_t* __restrict__ tile_free) {
   const int64_t tile = blockIdx.x;
@@ -956,22 +986,26 @@ DM_PH_READER(integrate)
 int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                         const float* d_ranges, const double* d_trig) {
   const int64_t nb = (int64_t)S * N;
-  // front-end stream: with overlap, its own stream after the previous call's
-  // accumulation (ev_tiles: the tile workspace is free again), so it runs
-  // beside a frontier pass still in flight on g->stream
+  // calls alternate between the two workspace sets; this one was last used
+  // two calls ago
+  g->iw_cur ^= 1;
+  dm_grid::IntWs& w = g->iw[g->iw_cur];
+  // front-end stream: with overlap, its own stream, after the accumulation
+  // that last used this set (ev_free), so it runs beside the previous call's
+  // accumulation and a frontier pass still in flight on g->stream
   hipStream_t fs = g->stream;
   if (g->overlap) {
     fs = g->fe_stream;
-    DM_HIP(dm_mark_tiles(g));
-    DM_HIP(hipStreamWaitEvent(fs, g->ev_tiles, 0));
+    DM_HIP(dm_mark_ws_free(g));  // still owed when no frontier pass came in between
+    DM_HIP(hipStreamWaitEvent(fs, w.free_wait ? w.free_wait : w.ev_free, 0));
   }
-  hipLaunchKernelGGL(k_integrate_reset, dim3(2), dim3(256), 0, fs, g->cnt, g->ish);
+  hipLaunchKernelGGL(k_integrate_reset, dim3(2), dim3(256), 0, fs, w.cnt, w.sh);
   DM_HIP(hipGetLastError());
   if (nb == 0) {
     if (g->overlap) {  // keep the stream order of the calls
       DM_HIP(hipEventRecord(g->ev_fe, fs));
       DM_HIP(hipStreamWaitEvent(g->stream, g->ev_fe, 0));
-      g->tiles_mark_pending = true;
+      w.free_owed = true;
     }
     return DM_OK;
   }
@@ -991,23 +1025,29 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   KernelTimer t;
   dm_timer_begin(g, "beam_prep", &t, fs);
   hipLaunchKernelGGL(k_beam_prep, dim3(nblk), dim3(256), 0, fs, a, ge, d_pose4, d_ranges,
-                     d_trig, g->beams, g->tile_count, g->act_raw, g->ish, g->blk_hist, g->blk_n, g->cnt);
+                     d_trig, g->beams, w.tile_count, g->act_raw, w.sh, g->blk_hist, g->blk_n, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "plan", &t, fs);
   hipLaunchKernelGGL(k_plan, dim3(grid_for(g->act_cap, kPlanThreads, 256)), dim3(kPlanThreads), 0, fs,
-                     ge, g->act_raw, g->ish, g->tile_cur, g->tile_count, g->hitems, g->litems,
-                     g->heavy_list, g->cnt);
+                     ge, g->act_raw, w.sh, w.tile_cur, w.tile_count, w.hitems, w.litems,
+                     w.heavy_list, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "scatter", &t, fs);
   hipLaunchKernelGGL(k_scatter, dim3(nblk), dim3(256), 0, fs, a, ge, g->beams,
-                     g->tile_cur, g->blk_hist, g->blk_n, g->pieces, g->cnt);
+                     w.tile_cur, g->blk_hist, g->blk_n, w.pieces, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
-  if (g->overlap) {
+  if (g->overlap && !g->fe_gate) {
     DM_HIP(hipEventRecord(g->ev_fe, fs));
     DM_HIP(hipStreamWaitEvent(g->stream, g->ev_fe, 0));
+  } else if (g->overlap) {
+    const unsigned long long seq = ++g->fe_seq;
+    hipLaunchKernelGGL(k_fe_signal, dim3(1), dim3(64), 0, fs, g->fe_flag, seq);
+    DM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_fe_gate, dim3(1), dim3(64), 0, g->stream, g->fe_flag, seq, w.cnt);
+    DM_HIP(hipGetLastError());
   }
   const int vec_ok = (g->W % 4 == 0) ? 1 : 0;
   // heavy chunks and medium tiles first (the long items), then the light
@@ -1015,27 +1055,24 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   dm_timer_begin(g, "tile_accum", &t);
   hipLaunchKernelGGL(k_tile_accum, dim3(grid_for(g->hitem_cap + g->act_cap, 1, 16384)),
                      dim3(kQuarter), 0,
-                     g->stream, ge, make_apply(g), g->hitems, (int)CNT_ITEMS, g->litems, (int)CNT_LITEMS,
-                     g->pieces, g->tile_count, g->tile_free, g->slabs, g->L, g->state, g->cnt, g->ish, vec_ok,
-                     g->heavy_list, g->fuse_heavy ? g->heavy_done : nullptr);
+                     g->stream, ge, make_apply(g), w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS,
+                     w.pieces, w.tile_count, g->tile_free, w.slabs, g->L, g->state, w.cnt, w.sh, vec_ok,
+                     w.heavy_list, g->fuse_heavy ? w.heavy_done : nullptr);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
+  if (g->overlap) w.free_owed = true;
   // A beam meets a (convex) tile in one k-range of <= 64 steps, and chunks
   // are >= 64 steps long, so a tile gets at most 1 piece per beam (2 when
   // beams are chunked).  Calls that cannot reach kMedium pieces in any tile
   // (one 360-beam scan: C1 / C2) have no heavy tile: no k_heavy_apply.
   const int64_t max_tile_pieces = nb * (ge.chunks > 1 ? 2 : 1);
-  if (max_tile_pieces <= kMedium || g->fuse_heavy) {
-    if (g->overlap) g->tiles_mark_pending = true;
-    return DM_OK;
-  }
+  if (max_tile_pieces <= kMedium || g->fuse_heavy) return DM_OK;
   dm_timer_begin(g, "heavy_apply", &t);
   hipLaunchKernelGGL(k_heavy_apply, dim3(grid_for(4 * g->heavy_cap, 1, 1024)), dim3(kQuarter), 0, g->stream, ge,
-                     make_apply(g), g->heavy_list, g->tile_count, g->tile_free, g->slabs, g->L, g->state,
-                     g->cnt, g->ish);
+                     make_apply(g), w.heavy_list, w.tile_count, g->tile_free, w.slabs, g->L, g->state,
+                     w.cnt, w.sh);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
-  if (g->overlap) g->tiles_mark_pending = true;
   return DM_OK;
 }
 

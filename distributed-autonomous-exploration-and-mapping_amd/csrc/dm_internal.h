@@ -53,6 +53,12 @@ constexpr unsigned long long kOvUnionFind = 8ull;  // a union-find loop hit its 
 constexpr int kIntegrateCounters[] = {CNT_ACTIVE, CNT_U, CNT_T, CNT_SEGS, CNT_ITEMS,
                                       CNT_HEAVY, CNT_TH, CNT_LITEMS, CNT_IOVERFLOW};
 
+// k_plan's work-item classes (dm_integrate.hip): tiles with more pieces than
+// kIntegrateChunk are split into items of kIntegrateChunk pieces, tiles with
+// more than kIntegrateMedium are heavy (merged in a slab)
+constexpr int kIntegrateChunk = 256;
+constexpr int kIntegrateMedium = 1024;
+
 // Sharded counters: same-address device atomics serialise at the memory side
 // (~12 ns each, MI355X_MICROARCH.md price list "fanin"), so per-workgroup
 // totals go to one of kShards counters, each on its own 128-B line
@@ -102,16 +108,20 @@ struct dm_grid {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   // dm_set_overlap: the integrate front-end (reset, beam_prep, plan, scatter)
-  // runs on fe_stream and waits only for the previous call's accumulation
-  // (ev_tiles), so it overlaps a frontier pass still running on `stream`;
-  // the accumulation waits for it (ev_fe).
+  // runs on fe_stream, so it overlaps a frontier pass still running on
+  // `stream`; the accumulation waits for it (ev_fe).  The workspace the
+  // front-end hands to the accumulation is double-buffered (iw[2], calls
+  // alternate): call k+1's front-end only waits for call k-1's accumulation
+  // (iw[p].ev_free), which is long done when the steps are pipelined, so no
+  // marker sits behind the accumulation of call k.
   bool overlap = false;
   hipStream_t fe_stream = nullptr;
-  hipEvent_t ev_fe = nullptr, ev_tiles = nullptr;
-  // ev_tiles is recorded lazily: after the next frontier pass's first
-  // kernel (an event marker right behind the write-heavy map update costs
-  // the stream several microseconds), or at the next integrate call
-  bool tiles_mark_pending = false;
+  hipEvent_t ev_fe = nullptr;
+  // front-end completion word (k_fe_signal / k_fe_gate, dm_integrate.hip):
+  // the sequence number of the last call whose front-end finished
+  unsigned long long* fe_flag = nullptr;
+  unsigned long long fe_seq = 0;
+  bool fe_gate = true;  // DM_FE_GATE=0: cross-stream event wait instead (A/B)
   uint64_t integrate_seq = 0;  // map changes so far
   // Asynchronous passes (dm_frontiers_begin / dm_merge_bands_begin) use a
   // ring of kRbSlots readback slots, so a pass can be started before the
@@ -147,30 +157,45 @@ struct dm_grid {
 
   float* L = nullptr;
   int8_t* state = nullptr;
-  int32_t* tile_count = nullptr;
-  int32_t* tile_cur = nullptr;   // [NT] k_scatter's bin cursor per active tile (k_plan)
   int32_t* tile_free = nullptr;
-  unsigned long long* cnt = nullptr;  // CNT_N device counters
-  unsigned long long* h_cnt = nullptr;  // pinned mirror
-  unsigned long long* ish = nullptr;    // [kShards][kShardWords] integrate shards
+  unsigned long long* cnt = nullptr;    // CNT_N device counters (frontier fields)
+  unsigned long long* h_cnt = nullptr;  // pinned mirror: [CNT_N] frontier counters, [CNT_N] integrate counters
   unsigned long long* fsh = nullptr;    // [kShards][kShardWords] frontier shards
-  unsigned long long* h_sh = nullptr;   // pinned mirror of ish then fsh
+  unsigned long long* h_sh = nullptr;   // pinned mirror of the last call's integrate shards, then fsh
 
   // integrate workspace
   Beam* beams = nullptr; int64_t beams_cap = 0;
   int64_t blk_cap = 0;            // workgroups blk_hist / blk_n hold
   int2* blk_hist = nullptr;       // [beam blocks][1024] k_beam_prep's (tile, pieces) histogram
   int32_t* blk_n = nullptr;       // [beam blocks] its entries
-  PackedPiece* pieces = nullptr; int64_t segs_cap = 0;  // ray pieces binned by tile
+  int64_t segs_cap = 0;           // pieces per workspace
   int32_t* act_raw = nullptr;    // [kShards][act_cap] first-touch lists per shard
   int64_t act_cap = 0;
-  int4* hitems = nullptr;        // heavy work items {tile, first piece, pieces, heavy ordinal}
   int64_t hitem_cap = 0;
-  int4* litems = nullptr;        // light work items {tile, first piece, pieces, -1} [act_cap]
-  int32_t* heavy_list = nullptr; // heavy ordinal -> tile
   int64_t heavy_cap = 0;
-  uint32_t* slabs = nullptr;     // [heavy][2][64*64] merged hit / miss counts
-  int32_t* heavy_done = nullptr; // [heavy] items finished this call (the last one applies the slab)
+  // what the front-end hands to the accumulation, one set per call parity
+  struct IntWs {
+    PackedPiece* pieces = nullptr;    // [segs_cap] ray pieces binned by tile
+    int4* hitems = nullptr;           // heavy work items {tile, first piece, pieces, heavy ordinal}
+    int4* litems = nullptr;           // light work items {tile, first piece, pieces, -1} [act_cap]
+    int32_t* heavy_list = nullptr;    // heavy ordinal -> tile
+    uint32_t* slabs = nullptr;        // [heavy][2][64*64] merged hit / miss counts
+    int32_t* heavy_done = nullptr;    // [heavy] items finished this call (the last one applies the slab)
+    int32_t* tile_count = nullptr;    // [NT] pieces per tile (zeroed again by the accumulation)
+    int32_t* tile_cur = nullptr;      // [NT] k_scatter's bin cursor per active tile (k_plan)
+    unsigned long long* cnt = nullptr;  // [CNT_N] the integrate counters (kIntegrateCounters)
+    unsigned long long* sh = nullptr;   // [kShards][kShardWords] integrate shards
+    // the next front-end using this set waits for free_wait: an event on
+    // `stream` after the set's last accumulation, recorded lazily (at the next
+    // frontier pass or integrate call) -- ev_free, or the readback-slot event
+    // of an asynchronous frontier pass enqueued after that accumulation
+    // (dm_frontiers_begin records one anyway: no extra marker)
+    hipEvent_t ev_free = nullptr;
+    hipEvent_t free_wait = nullptr;
+    bool free_owed = false;
+  };
+  IntWs iw[2];
+  int iw_cur = 0;                // set of the last integrate call
   // heavy tiles applied by their last k_tile_accum item (default) instead of
   // a separate k_heavy_apply launch (DM_HEAVY_SEPARATE=1, A/B measurement)
   bool fuse_heavy = true;
@@ -261,12 +286,19 @@ inline void dm_select_slot(dm_grid* g, int slot) {
   g->m_out = r.m_out;
 }
 
-// Record ev_tiles (the tile workspace of the last integrate call is free
-// once the work enqueued so far on g->stream is done) if it is still owed.
-inline hipError_t dm_mark_tiles(dm_grid* g) {
-  if (!g->overlap || !g->tiles_mark_pending) return hipSuccess;
-  g->tiles_mark_pending = false;
-  return hipEventRecord(g->ev_tiles, g->stream);
+// Settle the free events owed by the integrate workspaces (their last
+// accumulation is enqueued on g->stream before this point): `recorded`, an
+// event just recorded on g->stream, or each set's own ev_free recorded now.
+inline hipError_t dm_mark_ws_free(dm_grid* g, hipEvent_t recorded = nullptr) {
+  for (auto& w : g->iw) {
+    if (!w.free_owed) continue;
+    w.free_owed = false;
+    w.free_wait = recorded ? recorded : w.ev_free;
+    if (recorded) continue;
+    const hipError_t e = hipEventRecord(w.ev_free, g->stream);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 // A call with too few beams to fill the chip enumerates each beam's pieces
