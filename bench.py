@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="budget for the CPU-oracle baseline sample (0 disables)")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--depth", type=int, default=1,
+    ap.add_argument("--depth", type=int, default=2,
                     help="frontier passes in flight in the pipelined steps (1 or 2; libdm keeps 2 readback slots)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the steps back to back without overlapping step k+1's integrate "

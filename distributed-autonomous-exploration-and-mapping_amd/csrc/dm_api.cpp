@@ -19,6 +19,18 @@
 
 #include <stdlib.h>
 
+// Wait for all three streams; nothing of this handle is in flight afterwards.
+hipError_t dm_sync_all(dm_grid* g) {
+  for (hipStream_t s : {g->stream, g->fe_stream, g->pass_stream}) {
+    if (!s) continue;
+    const hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+  }
+  g->p_pending = false;
+  for (auto& f : g->fw) f.busy_pending = false;
+  return hipSuccess;
+}
+
 hipError_t dm_copy_shards(dm_grid* g) {
   const size_t bytes = sizeof(unsigned long long) * kShards * kShardWords;
   hipError_t e = hipMemcpyAsync(g->h_sh, g->iw[g->iw_cur].sh, bytes, hipMemcpyDeviceToHost, g->stream);
@@ -161,8 +173,7 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
 int ensure_trig(dm_grid* g, int32_t N, float amin, float inc) {
   if (N == g->trig_n && amin == g->trig_amin && inc == g->trig_inc) return DM_OK;
   // the table may still be read by an in-flight call
-  DM_HIP(hipStreamSynchronize(g->stream));
-  if (g->fe_stream) DM_HIP(hipStreamSynchronize(g->fe_stream));
+  DM_HIP(dm_sync_all(g));
   std::vector<double> t(2 * (size_t)std::max(N, 1));
   for (int32_t i = 0; i < N; ++i) {
     const double phi = (double)amin + (double)i * (double)inc;
@@ -196,7 +207,9 @@ int grow_slots(dm_grid* g, int64_t need) {
   if (cap < (1 << 16)) cap = 1 << 16;
   cap = ceil_div(cap, kShards) * kShards;  // kShards equal regions (k_frontier_tile)
   int rc = dev_alloc(&g->slot_label, cap, "slot labels");
-  if (!rc) rc = dev_alloc(&g->slot_parent, cap, "slot parents");
+  for (auto& f : g->fw)
+    if (!rc) rc = dev_alloc(&f.slot_parent, cap, "slot parents");
+  g->slot_parent = g->fw[g->fparity].slot_parent;
   if (!rc) rc = dev_alloc(&g->slot_root, cap, "slot roots");
   if (!rc) rc = dev_alloc(&g->slot_own, 3 * cap, "slot sums");
   if (!rc) rc = dev_alloc(&g->slot_acc, 3 * cap, "slot totals");
@@ -309,6 +322,7 @@ int check_integrate_args(int32_t S, int32_t N, const void* poses, const void* ra
 // Copies both counter blocks (frontier, then the last integrate call's) and
 // both shard blocks into the pinned mirrors and waits for them.
 int read_counters(dm_grid* g) {
+  DM_HIP(dm_join_pass_stream(g));
   DM_HIP(hipMemcpyAsync(g->h_cnt, g->cnt, sizeof(unsigned long long) * CNT_N,
                         hipMemcpyDeviceToHost, g->stream));
   DM_HIP(hipMemcpyAsync(g->h_cnt + CNT_N, g->iw[g->iw_cur].cnt, sizeof(unsigned long long) * CNT_N,
@@ -445,22 +459,31 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     const char* fk = getenv("DM_FRONTIER_KERNEL");
     g->frontier_kernel = fk && !strcmp(fk, "wave") ? 1 : (fk && !strcmp(fk, "wg") ? 2 : 0);
   }
-  if ((rc = dev_alloc(&g->cnt, CNT_N, "counters"))) return fail(rc);
+  for (auto& f : g->fw) {
+    if ((rc = dev_alloc(&f.cnt, CNT_N, "frontier counters"))) return fail(rc);
+    DM_HIP(hipMemset(f.cnt, 0, sizeof(unsigned long long) * CNT_N));
+    if ((rc = dev_alloc(&f.fsh, kShards * kShardWords, "frontier shard counters"))) return fail(rc);
+    DM_HIP(hipMemset(f.fsh, 0, sizeof(unsigned long long) * kShards * kShardWords));
+    if ((rc = dev_alloc(&f.ftiles, g->NT, "frontier tiles"))) return fail(rc);
+    if ((rc = dev_alloc(&f.big_tiles, g->NT, "frontier big tiles"))) return fail(rc);
+    if ((rc = dev_alloc(&f.fbits, g->NT * DM_TILE, "frontier bit rows"))) return fail(rc);
+    if ((rc = dev_alloc(&f.edge_slot, 2 * g->W, "edge slots"))) return fail(rc);
+  }
+  if ((rc = dev_alloc(&g->fl_n, 48, "frontier list lengths"))) return fail(rc);
+  DM_HIP(hipMemset(g->fl_n, 0, sizeof(unsigned long long) * 48));
+  if ((rc = dev_alloc(&g->bits_flag, 16, "bit-row hand-off word"))) return fail(rc);
+  DM_HIP(hipMemset(g->bits_flag, 0, sizeof(unsigned long long) * 16));
   if ((rc = dev_alloc(&g->fe_flag, 16, "front-end completion word"))) return fail(rc);
   DM_HIP(hipMemset(g->fe_flag, 0, sizeof(unsigned long long) * 16));
-  if ((rc = dev_alloc(&g->fsh, kShards * kShardWords, "frontier shard counters"))) return fail(rc);
-  DM_HIP(hipMemset(g->fsh, 0, sizeof(unsigned long long) * kShards * kShardWords));
-  if ((rc = dev_alloc(&g->ftiles, g->NT, "frontier tiles"))) return fail(rc);
-  if ((rc = dev_alloc(&g->big_tiles, g->NT, "frontier big tiles"))) return fail(rc);
   if ((rc = dev_alloc(&g->border, g->NT * 256, "frontier borders"))) return fail(rc);
   if ((rc = dev_alloc(&g->rel, 4 * g->NT, "tile-edge hand-off words"))) return fail(rc);
   DM_HIP(hipMemset(g->rel, 0, sizeof(unsigned long long) * 4 * (size_t)g->NT));
-  if ((rc = dev_alloc(&g->edge_slot, 2 * g->W, "edge slots"))) return fail(rc);
   if ((rc = dev_alloc(&g->edge_label, 2 * g->W, "edge labels"))) return fail(rc);
   if ((rc = dev_alloc(&g->halo, 2 * g->W, "halo rows"))) return fail(rc);
   if ((rc = dev_alloc(&g->bs_rows, 3 * (kBuckets + 1), "bucket-sort buckets"))) return fail(rc);
   DM_HIP(hipMemset(g->bs_rows, 0, sizeof(int32_t) * 3 * (kBuckets + 1)));  // counts start at zero
   if ((rc = grow_slots(g, 1 << 16))) return fail(rc);
+  dm_select_fw(g, g->fparity);
   for (int sl = 0; sl <= dm_grid::kRbSlots; ++sl)
     if ((rc = grow_host_out(g, sl, 1 << 14))) return fail(rc);
   dm_select_slot(g, 0);
@@ -488,6 +511,8 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   g->own_stream = true;
   e = hipStreamCreateWithPriority(&g->fe_stream, hipStreamNonBlocking, prio_lo);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(front-end)"));
+  e = hipStreamCreateWithPriority(&g->pass_stream, hipStreamNonBlocking, prio_hi);
+  if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(pass)"));
   // ev_fe / ev_free only order the two streams on the device: no system-
   // scope fence (no host-visible cache writeback at every step).  The host
   // waits on a readback slot's event and then reads mapped host memory:
@@ -512,8 +537,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
 int dm_destroy(dm_grid* g) {
   if (!g) return DM_OK;
   (void)hipSetDevice(g->device);
-  if (g->stream) (void)hipStreamSynchronize(g->stream);
-  if (g->fe_stream) (void)hipStreamSynchronize(g->fe_stream);
+  (void)dm_sync_all(g);
   for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
   for (hipEvent_t ev : {g->ev_fe, g->iw[0].ev_free, g->iw[1].ev_free})
     if (ev) (void)hipEventDestroy(ev);
@@ -524,19 +548,25 @@ int dm_destroy(dm_grid* g) {
     dev_free(r.m_out);
   }
   if (g->fe_stream) (void)hipStreamDestroy(g->fe_stream);
+  if (g->pass_stream) (void)hipStreamDestroy(g->pass_stream);
+  for (auto& f : g->fw) {
+    dev_free(f.cnt); dev_free(f.fsh); dev_free(f.ftiles); dev_free(f.big_tiles); dev_free(f.fbits);
+    dev_free(f.edge_slot); dev_free(f.slot_parent);
+  }
+  dev_free(g->fl_n); dev_free(g->bits_flag);
   for (auto& w : g->iw) {
     dev_free(w.pieces); dev_free(w.hitems); dev_free(w.litems); dev_free(w.heavy_list); dev_free(w.slabs);
     dev_free(w.heavy_done); dev_free(w.tile_count); dev_free(w.tile_cur); dev_free(w.cnt); dev_free(w.sh);
   }
   dev_free(g->L); dev_free(g->state);
-  dev_free(g->tile_free); dev_free(g->cnt); dev_free(g->beams); dev_free(g->blk_hist); dev_free(g->blk_n);
+  dev_free(g->tile_free); dev_free(g->beams); dev_free(g->blk_hist); dev_free(g->blk_n);
   dev_free(g->trig);
   dev_free(g->pose4); dev_free(g->ranges); 
   dev_free(g->bs_rows); dev_free(g->bs_key); dev_free(g->bs_idx);
-  dev_free(g->border); dev_free(g->rel); dev_free(g->ftiles); dev_free(g->big_tiles); dev_free(g->slot_label); dev_free(g->slot_parent); dev_free(g->slot_root);
+  dev_free(g->border); dev_free(g->rel); dev_free(g->slot_label); dev_free(g->slot_root);
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
-  dev_free(g->edge_slot); dev_free(g->edge_label); dev_free(g->mask); dev_free(g->labels);
-  dev_free(g->halo); dev_free(g->fsh); dev_free(g->fe_flag); dev_free(g->act_raw);
+  dev_free(g->edge_label); dev_free(g->mask); dev_free(g->labels);
+  dev_free(g->halo); dev_free(g->fe_flag); dev_free(g->act_raw);
   dev_free(g->slot_k); dev_free(g->rank_of); dev_free(g->m_parent); dev_free(g->m_label);
   dev_free(g->m_acc); dev_free(g->m_clu); dev_free(g->m_cnt);
   if (g->h_mcnt) (void)hipHostFree(g->h_mcnt);
@@ -557,11 +587,11 @@ int dm_reset(dm_grid* g) {
   const int64_t cells = g->W * g->R;
   DM_HIP(hipMemsetAsync(g->L, 0, sizeof(float) * (size_t)cells, g->stream));
   DM_HIP(hipMemsetAsync(g->state, 0xFF, (size_t)cells, g->stream));
-  DM_HIP(hipStreamSynchronize(g->fe_stream));
+  DM_HIP(dm_sync_all(g));
   for (auto& w : g->iw)
     DM_HIP(hipMemsetAsync(w.tile_count, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
   DM_HIP(hipMemsetAsync(g->tile_free, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
-  DM_HIP(hipMemsetAsync(g->cnt, 0, sizeof(unsigned long long) * CNT_N, g->stream));
+  for (auto& f : g->fw) DM_HIP(hipMemsetAsync(f.cnt, 0, sizeof(unsigned long long) * CNT_N, g->stream));
   DM_HIP(hipStreamSynchronize(g->stream));
   return DM_OK;
 }
@@ -593,8 +623,7 @@ int enqueue_host_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N
   hipStream_t fs = g->overlap ? g->fe_stream : g->stream;
   if ((int64_t)S * 4 > g->pose_cap || nb > g->ranges_cap || (int64_t)S * 4 > g->h_pose_cap) {
     // the device buffers may still feed an in-flight call
-    DM_HIP(hipStreamSynchronize(g->stream));
-    DM_HIP(hipStreamSynchronize(g->fe_stream));
+    DM_HIP(dm_sync_all(g));
   }
   if ((int64_t)S * 4 > g->pose_cap) {
     if ((rc = dev_alloc(&g->pose4, (int64_t)S * 4, "poses"))) return rc;
@@ -693,7 +722,7 @@ int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out) {
   const uint64_t v[10] = {dm_shard_sum(g->h_sh, SH_U),  dm_shard_sum(g->h_sh, SH_T),
                           dm_shard_sum(g->h_sh, SH_TH), ic[CNT_SEGS],
                           ic[CNT_ACTIVE],               items,
-                          ic[CNT_HEAVY],                g->h_cnt[g->fparity ? CNT_FL1 : CNT_FL0],
+                          ic[CNT_HEAVY],                g->h_cnt[CNT_FL0],
                           dm_shard_sum(fs, SH_SLOT),    g->h_cnt[CNT_CLUSTERS]};
   for (int32_t i = 0; i < cap && i < 10; ++i) out[i] = v[i];
   if (n_out) *n_out = 10;
@@ -831,6 +860,12 @@ int wait_oldest(dm_grid* g, int kind, const char* what) {
   if (!g->rb_count || g->rb[g->rb_head].kind != kind)
     return dm_set_error(DM_ERR_INVALID_ARG, "the oldest pass in flight is not a %s pass", what);
   DM_HIP(hipEventSynchronize(g->rb[g->rb_head].ev));
+  if (kind == 1) {  // passes end in order: this one and every earlier one are done
+    const uint64_t pass = g->rb[g->rb_head].pass;
+    for (auto& f : g->fw)
+      if (f.busy_pending && f.busy_pass <= pass) f.busy_pending = false;
+    if (g->p_pending && g->p_tail_pass <= pass) g->p_pending = false;
+  }
   dm_select_slot(g, g->rb_head);
   return DM_OK;
 }
@@ -884,6 +919,7 @@ int dm_merge_bands_begin(dm_grid* g, const void* d_gathered, int32_t nranks, int
   if (n >= (1ll << 31)) return dm_set_error(DM_ERR_SHAPE, "nranks * rec_cap must be < 2^31");
   int slot = 0;
   if ((rc = grow_merge(g, n)) || (rc = claim_slot(g, &slot))) return rc;
+  DM_HIP(dm_join_pass_stream(g));  // the sort workspace is shared with the frontier passes
   if ((rc = dm_launch_merge(g, d_gathered, nranks, rec_cap, min_size))) return rc;
   dm_grid::RbSlot& r = g->rb[slot];
   DM_HIP(hipEventRecord(r.ev, g->stream));
@@ -917,6 +953,7 @@ int dm_merge_bands(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t r
   if (n >= (1ll << 31)) return dm_set_error(DM_ERR_SHAPE, "nranks * rec_cap must be < 2^31");
   if ((rc = grow_merge(g, n))) return rc;
   dm_select_slot(g, dm_grid::kRbSync);  // its own slot: asynchronous passes may be in flight
+  DM_HIP(dm_join_pass_stream(g));  // the sort workspace is shared with the frontier passes
   if ((rc = dm_launch_merge(g, d_gathered, nranks, rec_cap, min_size))) return rc;
   DM_HIP(hipStreamSynchronize(g->stream));
   return merge_readback(g, dm_grid::kRbSync, n, out, cap, n_out);
@@ -927,9 +964,21 @@ int dm_frontiers_begin(dm_grid* g) {
   if (rc || (rc = use_device(g))) return rc;
   int slot = 0;
   if ((rc = claim_slot(g, &slot))) return rc;
-  if ((rc = dm_enqueue_frontiers(g, false, false))) return rc;
+  // with overlap, the pass's labelling half runs on the pass stream, beside
+  // the next batch's map update (dm_enqueue_frontiers)
+  hipStream_t es = g->stream;
+  if ((rc = dm_enqueue_frontiers(g, false, false, g->overlap, &es))) return rc;
   dm_grid::RbSlot& r = g->rb[slot];
-  DM_HIP(hipEventRecord(r.ev, g->stream));
+  DM_HIP(hipEventRecord(r.ev, es));
+  dm_grid::FrWs& f = g->fw[g->fparity];
+  f.busy = r.ev;  // the set is free again once this pass ended
+  f.busy_pending = true;
+  f.busy_pass = g->fr_pass;
+  if (es != g->stream) {
+    g->p_tail = r.ev;
+    g->p_pending = true;
+    g->p_tail_pass = g->fr_pass;
+  }
   // the integrate workspaces' accumulations are ahead of this event: it
   // frees them (a marker right behind the write-heavy map update would cost
   // the stream several microseconds)
@@ -985,8 +1034,7 @@ int dm_frontiers_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out) {
 int dm_set_overlap(dm_grid* g, int32_t on) {
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
-  DM_HIP(hipStreamSynchronize(g->stream));
-  DM_HIP(hipStreamSynchronize(g->fe_stream));
+  DM_HIP(dm_sync_all(g));
   g->overlap = on != 0;
   for (auto& w : g->iw) {
     w.free_owed = false;
@@ -1049,6 +1097,7 @@ int dm_get_edge_labels(dm_grid* g, int64_t* first_row, int64_t* last_row) {
   if (rc || (rc = use_device(g))) return rc;
   if (!g->frontier_valid)
     return dm_set_error(DM_ERR_STATE, "call dm_frontiers first (map or halo changed since)");
+  DM_HIP(dm_join_pass_stream(g));
   if ((rc = dm_launch_edge_labels(g))) return rc;
   DM_HIP(hipStreamSynchronize(g->stream));
   if (first_row)
@@ -1155,8 +1204,7 @@ int dm_load(dm_grid* g, const char* path) {
 int dm_set_stream(dm_grid* g, void* stream) {
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
-  DM_HIP(hipStreamSynchronize(g->fe_stream));
-  DM_HIP(hipStreamSynchronize(g->stream));
+  DM_HIP(dm_sync_all(g));
   if (stream) {
     if (g->own_stream && g->stream) (void)hipStreamDestroy(g->stream);
     g->stream = (hipStream_t)stream;
@@ -1171,8 +1219,7 @@ int dm_set_stream(dm_grid* g, void* stream) {
 int dm_synchronize(dm_grid* g) {
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
-  DM_HIP(hipStreamSynchronize(g->fe_stream));
-  DM_HIP(hipStreamSynchronize(g->stream));
+  DM_HIP(dm_sync_all(g));
   return DM_OK;
 }
 

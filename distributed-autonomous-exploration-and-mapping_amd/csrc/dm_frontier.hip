@@ -164,72 +164,27 @@ __device__ inline int root_rank(const uint64_t* s_root, const int32_t* pre, int 
   return pre[r >> 6] + __popcll(s_root[r >> 6] & ((1ull << (r & 63)) - 1ull));
 }
 
-// State byte of one halo cell (global column x, band-local row y), or
-// nullptr for out-of-grid cells and missing halos ("not unknown").
-__device__ inline const int8_t* halo_ptr(const FGeom& g, const int8_t* state, const int8_t* halo, int32_t x,
-                                         int32_t y) {
-  if (x < 0 || x >= g.W) return nullptr;
-  if (y >= 0 && y < g.R) return state + (int64_t)y * g.W + x;
-  if (y == -1 && g.has_before) return halo + x;
-  if (y == g.R && g.has_after) return halo + g.W + x;
-  return nullptr;
-}
-
-// The global loads of one tile, issued one tile ahead by k_frontier_tile so
-// that they are in flight while the previous tile is labelled: this
-// thread's 16 interior cells (one uint4 when the row segment is whole and
-// aligned; ragged tiles read byte-wise when consumed) and its halo cell
-// (waves 0/1: the rows above / below; threads 128..255: the columns left /
-// right) and corner cell (threads 0..3).  A missing cell reads as 0 (free:
-// "not unknown").
-struct TileLoads {
-  uint4 v;
-  int8_t hb, cb;
-};
-
-__device__ inline void tile_issue(const FGeom& g, const int8_t* __restrict__ state,
-                                  const int8_t* __restrict__ halo, int32_t tile, int tid, TileLoads& t) {
-  const int32_t tx0 = (tile % g.TX) * DM_TS, ty0 = (tile / g.TX) * DM_TS;
-  const int y = tid >> 2, q = tid & 3;
-  const int32_t gy = ty0 + y, x0 = tx0 + q * 16;
-  const int64_t off = (int64_t)gy * g.W + x0;
-  t.v = make_uint4(0u, 0u, 0u, 0u);
-  if (gy < g.R && x0 + 16 <= g.W && (off & 15) == 0) t.v = *reinterpret_cast<const uint4*>(state + off);
-  const int lane = tid & 63, hr = (tid - 128) & 63;
-  const bool left = tid < 192;
-  const int8_t* hp = tid < 128 ? halo_ptr(g, state, halo, tx0 + lane, tid < 64 ? ty0 - 1 : ty0 + DM_TS)
-                               : halo_ptr(g, state, halo, left ? tx0 - 1 : tx0 + DM_TS, ty0 + hr);
-  t.hb = hp ? *hp : (int8_t)0;
-  t.cb = 0;
-  if (tid < 4) {
-    const int8_t* cp = halo_ptr(g, state, halo, tx0 + ((tid & 1) ? DM_TS : -1),
-                                (tid & 2) ? ty0 + DM_TS : ty0 - 1);
-    t.cb = cp ? *cp : (int8_t)0;
-  }
-}
-
 // One workgroup per listed tile.  Each 64-cell tile row is a 64-bit word:
-//  1. state -> bit rows: interior 16 B per thread (one uint4 load), the 260
-//     halo cells one load per thread, all issued together;
-//  2. frontier row y = free[y] & dilate(unknown[y-1] | unknown[y] | unknown[y+1]);
-//  3. 8-connected CCL on runs of set bits: runs numbered row-major, a run is
-//     joined with every run of the row above that overlaps it extended by one
-//     cell each side (LDS union-find, atomicMin hooking: a root is its set's
-//     first run, whose first cell is the component's min linear index);
-//  4. per-component sums from run lengths, one slot per component, border
-//     slot ids for k_frontier_merge.
+//  1. the tile's frontier bit rows (k_frontier_bits), one 8-byte load per
+//     thread of wave 0;
+//  2. runs of set bits, numbered row-major;
+//  3. 8-connected CCL on the runs: a run is joined with every run of the row
+//     above that overlaps it extended by one cell each side (LDS union-find,
+//     atomicMin hooking: a root is its set's first run, whose first cell is
+//     the component's min linear index);
+//  4. per-component sums from run lengths, one slot per component;
+//  5. unions across the tile's edges (below).
+// Tiles come from the pass's list (jlist == nullptr: list position kk), or
+// from jlist, the list positions k_frontier_tile left over.
 __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
-    FGeom g, const int8_t* __restrict__ state, const int8_t* __restrict__ halo,
+    FGeom g, const uint64_t* __restrict__ fbits, const int32_t* __restrict__ jlist,
     const int32_t* __restrict__ ftiles, const unsigned long long* __restrict__ list_n,
     int32_t* border, unsigned long long* rel, unsigned long long stamp,
     long long* __restrict__ slot_label, int32_t* slot_parent,
     long long* __restrict__ slot_own, long long* __restrict__ slot_acc,
     uint8_t* __restrict__ mask, int32_t* __restrict__ cell_slot, int32_t* __restrict__ edge_slot,
     unsigned long long* cnt, unsigned long long* fsh, int count_stats) {
-  __shared__ uint64_t s_unk[DM_TS + 2];    // row y at index y+1, bit c = column c
-  __shared__ uint8_t s_unkL[DM_TS + 2];    // column -1
-  __shared__ uint8_t s_unkR[DM_TS + 2];    // column 64
-  __shared__ uint64_t s_F[DM_TS];          // free bits (step 1), then frontier bits (step 2)
+  __shared__ uint64_t s_F[DM_TS];          // frontier bit rows
   __shared__ int32_t s_rbase[DM_TS + 1];
   __shared__ int32_t r_par[kMaxRuns];
   __shared__ uint8_t r_s[kMaxRuns], r_y[kMaxRuns];  // run end: run_end(s_F[y], s)
@@ -244,78 +199,19 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
   const int64_t nft = (int64_t)*list_n;
   const int64_t G = gridDim.x;
   DM_PH_INIT();
-  for (int64_t jj = blockIdx.x; jj < nft; jj += G) {  // one tile per workgroup at C3
+  for (int64_t kk = blockIdx.x; kk < nft; kk += G) {  // one tile per workgroup at C3
+    const int64_t jj = jlist ? (int64_t)jlist[kk] : kk;
     const int32_t tile = ftiles[jj];
-    TileLoads cur;
-    tile_issue(g, state, halo, tile, tid, cur);
+    const uint64_t F = tid < DM_TS ? fbits[jj * DM_TS + tid] : 0ull;
     const int64_t j = tile;  // border records are indexed by tile
     DM_PH_COUNT(dm_phase_acc_frontier, 16, 1);
     const int32_t tx0 = (tile % g.TX) * DM_TS;
     const int32_t ty0 = (tile / g.TX) * DM_TS;  // band-local
-    // ---- 1. bit rows ------------------------------------------------------
-    {
-      const int y = tid >> 2, q = tid & 3;
-      const int32_t gy = ty0 + y;
-      uint32_t unk = 0u, fre = 0u;
-      if (gy < g.R) {
-        const int32_t x0 = tx0 + q * 16;
-        const int64_t off = (int64_t)gy * g.W + x0;
-        if (x0 + 16 <= g.W && (off & 15) == 0) {
-          const uint4 v = cur.v;
-          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-          for (int k = 0; k < 16; ++k) {
-            const uint32_t b = (w[k >> 2] >> ((k & 3) * 8)) & 0xFFu;
-            unk |= (b == 0xFFu ? 1u : 0u) << k;
-            fre |= (b == 0u ? 1u : 0u) << k;
-          }
-        } else {
-          for (int k = 0; k < 16; ++k) {
-            if (x0 + k >= g.W) break;
-            const int8_t b = state[off + k];
-            unk |= (b == -1 ? 1u : 0u) << k;
-            fre |= (b == 0 ? 1u : 0u) << k;
-          }
-        }
-      } else if (gy == g.R && g.has_after) {  // ragged band: the halo row falls inside the tile
-        const int32_t x0 = tx0 + q * 16;
-        for (int k = 0; k < 16; ++k) {
-          if (x0 + k >= g.W) break;
-          unk |= (halo[g.W + x0 + k] == -1 ? 1u : 0u) << k;
-        }
-      }
-      reinterpret_cast<uint16_t*>(&s_unk[y + 1])[q] = (uint16_t)unk;
-      reinterpret_cast<uint16_t*>(&s_F[y])[q] = (uint16_t)fre;
-      // halo (loaded with the interior, a tile ahead): waves 0/1 the row
-      // above / below (one ballot each), threads 128..255 the columns left /
-      // right, threads 0..3 the four corners
-      const int hr = (tid - 128) & 63;
-      const bool left = tid < 192;
-      const uint32_t hu = (tid < 128 && cur.hb == -1) ? 1u : 0u;
-      const uint32_t su = (tid >= 128 && cur.hb == -1) ? 1u : 0u;
-      const uint32_t cu = (tid < 4 && cur.cb == -1) ? 1u : 0u;
-      const uint64_t hm = __ballot(hu != 0u);
-      if (tid == 0) s_unk[0] = hm;
-      if (tid == 64) s_unk[DM_TS + 1] = hm;
-      if (tid >= 128) {
-        if (left) s_unkL[hr + 1] = (uint8_t)su; else s_unkR[hr + 1] = (uint8_t)su;
-      }
-      if (tid < 4) {
-        const int idx = (tid & 2) ? DM_TS + 1 : 0;
-        if (tid & 1) s_unkR[idx] = (uint8_t)cu; else s_unkL[idx] = (uint8_t)cu;
-      }
-    }
-    __syncthreads();
     DM_PH(dm_phase_acc_frontier, 0);
-    // ---- 2. frontier bits + runs -------------------------------------------
+    // ---- 2. runs ----------------------------------------------------------------
     int any = 0;
     if (tid < DM_TS) {
       const int y = tid;
-      uint64_t D = 0;
-      for (int d = 0; d < 3; ++d) {
-        const uint64_t ui = s_unk[y + d];
-        D |= ui | (ui << 1) | (uint64_t)s_unkL[y + d] | (ui >> 1) | ((uint64_t)s_unkR[y + d] << 63);
-      }
-      const uint64_t F = s_F[y] & D;  // only this thread reads row y's free bits
       const uint64_t st = run_starts(F);
       s_F[y] = F;
       any = F != 0ull;
@@ -728,8 +624,41 @@ __device__ inline void edge_unions(int32_t sl, const int32_t* border, int32_t nb
   }
 }
 
+// Frontier bit rows of the listed tiles, one wave per tile (lane y = tile
+// row y): F = free & 3x3 dilation of unknown (out-of-grid / missing halo
+// cells are "not unknown").  The only kernel of a pass that reads the map:
+// with dm_set_overlap the next batch's map update may start right after it,
+// while the labelling kernels below (which read only these rows) run on the
+// pass stream.  Also copies the list length into the pass's counters.
+__global__ __launch_bounds__(kFW * 64) void k_frontier_bits(FGeom g, const int8_t* __restrict__ state,
+                                                            const int8_t* __restrict__ halo,
+                                                            const int32_t* __restrict__ ftiles,
+                                                            const unsigned long long* __restrict__ list_n,
+                                                            uint64_t* __restrict__ fbits,
+                                                            unsigned long long* cnt) {
+  const int w = threadIdx.x >> 6, lane = __lane_id();
+  const int64_t nft = (int64_t)*list_n;
+  if (blockIdx.x == 0 && threadIdx.x == 0) cnt[CNT_FL0] = (unsigned long long)nft;
+  // four consecutive listed tiles per workgroup: horizontal neighbours share
+  // the 128-byte lines of their rows and halo columns
+  for (int64_t jj = (int64_t)blockIdx.x * kFW + w; jj < nft; jj += (int64_t)gridDim.x * kFW) {
+    const int32_t tile = __builtin_amdgcn_readfirstlane(ftiles[jj]);
+    const int32_t tx0 = (tile % g.TX) * DM_TS, ty0 = (tile / g.TX) * DM_TS;  // ty0 band-local
+    uint64_t U, Fr, Ue;
+    uint32_t uL, uR, eL, eR;
+    tile_rows(g, state, halo, tx0, ty0, lane, U, Fr, uL, uR, Ue, eL, eR);
+    const uint64_t h = dilate_row(U, uL, uR);
+    const uint64_t he = dilate_row(Ue, eL, eR);
+    uint64_t hu = __shfl_up(h, 1);
+    uint64_t hd = __shfl_down(h, 1);
+    if (lane == 0) hu = he;
+    if (lane == 63) hd = he;
+    fbits[jj * DM_TS + lane] = Fr & (h | hu | hd);
+  }
+}
+
 __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
-    FGeom g, const int8_t* __restrict__ state, const int8_t* __restrict__ halo,
+    FGeom g, const uint64_t* __restrict__ fbits,
     const int32_t* __restrict__ ftiles, const unsigned long long* __restrict__ list_n,
     int32_t* border, unsigned long long* rel, unsigned long long stamp,
     long long* __restrict__ slot_label, int32_t* slot_parent,
@@ -762,21 +691,11 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
   for (int64_t jj = wid; jj < nft; jj += (int64_t)gridDim.x * kFW) {
     DM_PH(dm_phase_acc_ftile, 9);
     const int32_t tile = __builtin_amdgcn_readfirstlane(ftiles[jj]);
+    // ---- 1-2. frontier bit rows (k_frontier_bits): lane y = tile row y ----------
+    const uint64_t F = fbits[jj * DM_TS + lane];
     DM_PH_COUNT(dm_phase_acc_ftile, 16, 1);
     const int32_t tx = tile % g.TX, ty = tile / g.TX;
     const int32_t tx0 = tx * DM_TS, ty0 = ty * DM_TS;  // ty0 band-local
-    // ---- 1. rows: lane y = tile row y (lanes 0 / 63 also rows -1 / 64) --------
-    uint64_t U, Fr, Ue;
-    uint32_t uL, uR, eL, eR;
-    tile_rows(g, state, halo, tx0, ty0, lane, U, Fr, uL, uR, Ue, eL, eR);
-    // ---- 2. frontier bits: free & 3x3 dilation of unknown -------------------
-    const uint64_t h = dilate_row(U, uL, uR);
-    const uint64_t he = dilate_row(Ue, eL, eR);
-    uint64_t hu = __shfl_up(h, 1);
-    uint64_t hd = __shfl_down(h, 1);
-    if (lane == 0) hu = he;
-    if (lane == 63) hd = he;
-    const uint64_t F = Fr & (h | hu | hd);
     DM_PH(dm_phase_acc_ftile, 0);
     if (__ballot(F != 0ull) == 0ull) continue;  // no frontier cell: nothing to publish
     // ---- 3. runs of set bits, numbered row-major ---------------------------
@@ -795,7 +714,7 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
       atomicAdd(&fsh[shard * kShardWords + SH_FTF], 1ull);
     }
     if (nruns > kRunsFast) {  // too many for this wave's LDS: the big kernel's
-      if (lane == 0) big_list[atomicAdd(&cnt[CNT_BIG], 1ull)] = tile;
+      if (lane == 0) big_list[atomicAdd(&cnt[CNT_BIG], 1ull)] = (int32_t)jj;
       continue;
     }
     for (int r = lane; r < nruns; r += 64) {
@@ -1495,7 +1414,7 @@ int dm_launch_rank_sort(hipStream_t stream, long long* clusters, const long long
   return DM_OK;
 }
 
-int dm_launch_bucket_sort(dm_grid* g, long long* clusters, const long long* sums,
+int dm_launch_bucket_sort(dm_grid* g, hipStream_t stream, long long* clusters, const long long* sums,
                           const long long* labels, const unsigned long long* d_count,
                           int64_t max_records, int64_t row_base, int64_t rows, dm_cluster* out,
                           int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
@@ -1514,16 +1433,16 @@ int dm_launch_bucket_sort(dm_grid* g, long long* clusters, const long long* sums
   int32_t* roff = rcnt + (kBuckets + 1);
   int32_t* rcur = roff + (kBuckets + 1);
   const int eg = grid_for(max_records, 256, 2048);
-  hipLaunchKernelGGL(k_bs_count, dim3(eg), dim3(256), 0, g->stream, clusters, labels, d_count, max_records, base,
+  hipLaunchKernelGGL(k_bs_count, dim3(eg), dim3(256), 0, stream, clusters, labels, d_count, max_records, base,
                      shift, rcnt);
   DM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_bs_scan, dim3(1), dim3(kScanThreads), 0, g->stream, d_count, max_records, nbk, rcnt,
+  hipLaunchKernelGGL(k_bs_scan, dim3(1), dim3(kScanThreads), 0, stream, d_count, max_records, nbk, rcnt,
                      roff, rcur);
   DM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_bs_place, dim3(eg), dim3(256), 0, g->stream, clusters, labels, d_count, max_records,
+  hipLaunchKernelGGL(k_bs_place, dim3(eg), dim3(256), 0, stream, clusters, labels, d_count, max_records,
                      base, shift, rcur, g->bs_key, g->bs_idx);
   DM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_bs_rank, dim3(eg), dim3(256), 0, g->stream, g->p.origin_x, g->p.origin_y,
+  hipLaunchKernelGGL(k_bs_rank, dim3(eg), dim3(256), 0, stream, g->p.origin_x, g->p.origin_y,
                      g->p.resolution, clusters, sums, labels, d_count, max_records, base, shift, roff, g->bs_key,
                      g->bs_idx, out, rank_of, d_sorted, cnt, ncnt, sorted_idx, fsh, host_out, host_cap);
   DM_HIP(hipGetLastError());
@@ -1533,85 +1452,111 @@ int dm_launch_bucket_sort(dm_grid* g, long long* clusters, const long long* sums
 // Enqueues the band pipeline (no synchronisation): tile list, tile CCL,
 // border merge, roots, compaction, sort.  Shared by dm_launch_frontiers and
 // the cross-band export (dm_merge.hip).
-int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels) {
+int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool split, hipStream_t* end_stream) {
   const FGeom fg = make_fgeom(g, want_mask, want_labels);
   const int64_t cells = g->R * g->W;
+  // the prep and the bit rows run on g->stream after everything shared with
+  // the pass stream (labelling of earlier passes) -- except for split passes,
+  // which keep that order on the pass stream itself
+  if (!split) DM_HIP(dm_join_pass_stream(g));
   ++g->fr_pass;
   g->fparity ^= 1;
-  unsigned long long* list_n = g->cnt + (g->fparity ? CNT_FL1 : CNT_FL0);
-  unsigned long long* other_n = g->cnt + (g->fparity ? CNT_FL0 : CNT_FL1);
+  dm_grid::FrWs& fw = g->fw[g->fparity];
+  if (fw.busy_pending) {  // the set's previous pass (two passes ago) may still run
+    DM_HIP(hipStreamWaitEvent(g->stream, fw.busy, 0));
+    fw.busy_pending = false;
+  }
+  dm_select_fw(g, g->fparity);
+  unsigned long long* list_n = g->fl_n + 16 * (g->fr_pass % 3);
+  unsigned long long* zero_n = g->fl_n + 16 * ((g->fr_pass + 1) % 3);  // last used by pass fr_pass - 2
   KernelTimer t;
   dm_timer_begin(g, "frontier_prep", &t);
   hipLaunchKernelGGL(k_frontier_prep, dim3(grid_for(std::max<int64_t>(std::max<int64_t>(g->NT, 2 * g->W), kShards * kShardWords), 256, 1024)), dim3(256), 0,
-                     g->stream, g->NT, g->tile_free, g->ftiles, list_n, other_n, 2 * g->W, g->cnt, g->fsh,
+                     g->stream, g->NT, g->tile_free, g->ftiles, list_n, zero_n, 2 * g->W, g->cnt, g->fsh,
                      g->edge_slot, g->slot_parent, g->slot_cap);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));
+  // one wave per listed tile; the grid follows the last collected pass's
+  // list length (+25 %; the kernels grid-stride, so any count is covered)
+  const int64_t want_waves = g->ftile_hint > 0 ? g->ftile_hint + g->ftile_hint / 4 + 64 : g->NT;
+  const int wave_grid = grid_for(std::min<int64_t>(want_waves, g->NT), kFW, 8192);
+  dm_timer_begin(g, "frontier_bits", &t);
+  hipLaunchKernelGGL(k_frontier_bits, dim3(wave_grid), dim3(kFW * 64), 0, g->stream, fg, g->state, g->halo,
+                     g->ftiles, list_n, g->fbits, g->cnt);
+  dm_timer_end(g, &t);
+  DM_HIP(hipGetLastError());
+  // the map has been read: with split, the rest runs on the pass stream,
+  // after the bit rows' hand-off
+  hipStream_t ps = g->stream;
+  if (split) {
+    ps = g->pass_stream;
+    const unsigned long long seq = ++g->bits_seq;
+    if (int rc = dm_launch_signal(g->stream, g->bits_flag, seq)) return rc;
+    if (int rc = dm_launch_gate(ps, g->bits_flag, seq, g->cnt + CNT_OVERFLOW, kOvGate)) return rc;
+  }
+  if (end_stream) *end_stream = ps;
   // Tile kernel, chosen from the last collected pass (both are exact for any
   // map; they differ in speed): tiles whose frontiers are dense (more than
   // kDenseRuns runs per tile with frontier cells on average, e.g. C3's ray
   // fans, ~100) take the 256-thread kernel, one tile per workgroup; sparse
   // ones (an explored map's few frontier tiles among many listed tiles, a
   // 1 cm map's thin rays) the wave-per-tile kernel, which also screens the
-  // listed tiles without frontier cells at the rate of their loads and
-  // leaves tiles with more than kRunsFast runs to the 256-thread kernel.
+  // listed tiles without frontier cells at the rate of one 8-byte load per
+  // lane and leaves tiles with more than kRunsFast runs to the 256-thread
+  // kernel.
   const bool dense = g->frontier_kernel == 2 ||
                      (g->frontier_kernel == 0 && g->ftf_hint > 0 && g->runs_hint > kDenseRuns * g->ftf_hint);
   if (!dense) {
-    // one wave per listed tile: the grid follows the last collected pass's
-    // list length (+25 %; the kernel grid-strides, so any count is covered)
-    const int64_t want_waves = g->ftile_hint > 0 ? g->ftile_hint + g->ftile_hint / 4 + 64 : g->NT;
-    const int light_grid = grid_for(std::min<int64_t>(want_waves, g->NT), kFW, 8192);
-    dm_timer_begin(g, "frontier_tile", &t);
-    hipLaunchKernelGGL(k_frontier_tile, dim3(light_grid), dim3(kFW * 64), 0, g->stream, fg, g->state,
-                       g->halo, g->ftiles, list_n, g->border, g->rel, (unsigned long long)g->fr_pass,
+    dm_timer_begin(g, "frontier_tile", &t, ps);
+    hipLaunchKernelGGL(k_frontier_tile, dim3(wave_grid), dim3(kFW * 64), 0, ps, fg, g->fbits,
+                       g->ftiles, list_n, g->border, g->rel, (unsigned long long)g->fr_pass,
                        g->slot_label, g->slot_parent, g->slot_own, g->slot_acc, g->mask, g->cell_slot,
                        g->edge_slot, g->cnt, g->fsh, g->big_tiles);
     dm_timer_end(g, &t);
     DM_HIP(hipGetLastError());
   }
-  dm_timer_begin(g, dense ? "frontier_tile" : "frontier_big", &t);
+  dm_timer_begin(g, dense ? "frontier_tile" : "frontier_big", &t, ps);
   hipLaunchKernelGGL(k_frontier_tile_big, dim3(dense ? grid_for(g->NT, 1, 8192) : grid_for(g->NT, 1, 512)),
-                     dim3(kFT), 0, g->stream, fg, g->state, g->halo, dense ? g->ftiles : g->big_tiles,
+                     dim3(kFT), 0, ps, fg, g->fbits, dense ? nullptr : g->big_tiles, g->ftiles,
                      dense ? list_n : g->cnt + CNT_BIG, g->border, g->rel, (unsigned long long)g->fr_pass,
                      g->slot_label, g->slot_parent, g->slot_own,
                      g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh, dense ? 1 : 0);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   const int sgrid = grid_for(g->slot_cap, 256, 1024);
-  dm_timer_begin(g, "frontier_resolve", &t);
+  dm_timer_begin(g, "frontier_resolve", &t, ps);
   // min_size <= 1: every root is a cluster, compacted by the resolve itself
   // (no k_frontier_compact); the sort reads the sums by slot
   const int fuse = g->p.min_frontier_size <= 1 ? 1 : 0;
   // one workgroup per CU: fewer workgroups = fewer per-root flushes
-  hipLaunchKernelGGL(k_frontier_resolve, dim3(grid_for(g->slot_cap, 256, g->n_cu)), dim3(256), 0, g->stream, fg,
+  hipLaunchKernelGGL(k_frontier_resolve, dim3(grid_for(g->slot_cap, 256, g->n_cu)), dim3(256), 0, ps, fg,
                      g->slot_parent, g->slot_root, g->slot_own, g->slot_acc, g->fsh, fuse, g->slot_label,
                      g->clusters, g->slot_k, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (!fuse) {
-    dm_timer_begin(g, "frontier_compact", &t);
-    hipLaunchKernelGGL(k_frontier_compact, dim3(sgrid), dim3(256), 0, g->stream, fg,
+    dm_timer_begin(g, "frontier_compact", &t, ps);
+    hipLaunchKernelGGL(k_frontier_compact, dim3(sgrid), dim3(256), 0, ps, fg,
                        g->slot_root, g->slot_label, g->slot_acc, g->clusters, g->slot_k, g->cnt, g->fsh);
     dm_timer_end(g, &t);
     DM_HIP(hipGetLastError());
   }
   if (want_labels) {
-    hipLaunchKernelGGL(k_slot_labels, dim3(grid_for(cells, 256, 8192)), dim3(256), 0, g->stream,
+    hipLaunchKernelGGL(k_slot_labels, dim3(grid_for(cells, 256, 8192)), dim3(256), 0, ps,
                        cells, g->slot_cap, g->cell_slot, g->slot_root, g->slot_label, g->labels);
     DM_HIP(hipGetLastError());
   }
-  dm_timer_begin(g, "sort_clusters", &t);
+  dm_timer_begin(g, "sort_clusters", &t, ps);
   // the last collected pass predicts this one's cluster count (either sort
   // is exact for any count; only their speed differs)
   const int rc = g->sort_hint > kBucketSortMin
-      ? dm_launch_bucket_sort(g, g->clusters, fuse ? g->slot_acc : nullptr, fuse ? g->slot_label : nullptr,
+      ? dm_launch_bucket_sort(g, ps, g->clusters, fuse ? g->slot_acc : nullptr, fuse ? g->slot_label : nullptr,
                               g->cnt + CNT_CLUSTERS, g->slot_cap, g->row0, g->R, g->out_clu,
                               g->rank_of, g->cnt + CNT_SORTED, g->cnt, CNT_N, CNT_SORTED, g->fsh,
                               g->h_out_dev, g->h_out_cap)
-      : dm_launch_rank_sort(g->stream, g->clusters, fuse ? g->slot_acc : nullptr, fuse ? g->slot_label : nullptr,
+      : dm_launch_rank_sort(ps, g->clusters, fuse ? g->slot_acc : nullptr, fuse ? g->slot_label : nullptr,
                             g->cnt + CNT_CLUSTERS, g->slot_cap, g->p.origin_x,
                             g->p.origin_y, g->p.resolution, g->out_clu, g->rank_of, g->cnt + CNT_SORTED,
                             g->cnt, CNT_N, CNT_SORTED, g->fsh, g->h_out_dev, g->h_out_cap, g->sort_hint);
@@ -1637,10 +1582,13 @@ int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied) {
   if (g->h_cnt[CNT_OVERFLOW] & kOvUnionFind)
     return dm_set_error(DM_ERR_INCOMPLETE, "frontier union-find did not converge within its bound "
                                            "(dm_uf.h): this pass has no result");
+  if (g->h_cnt[CNT_OVERFLOW] & kOvGate)
+    return dm_set_error(DM_ERR_INCOMPLETE, "frontier pass: the bit-row hand-off to the pass stream "
+                                           "timed out: this pass has no result");
   *n_clusters = (int64_t)g->h_cnt[CNT_CLUSTERS];
   g->sort_hint = *n_clusters;
   // this pass's tile-list length (the other parity's counter is 0 or smaller)
-  g->ftile_hint = (int64_t)std::max(g->h_cnt[CNT_FL0], g->h_cnt[CNT_FL1]);
+  g->ftile_hint = (int64_t)g->h_cnt[CNT_FL0];
   g->runs_hint = (int64_t)hdr[CNT_N + 1];
   g->ftf_hint = (int64_t)hdr[CNT_N + 2];
   return DM_OK;

@@ -864,31 +864,32 @@ __global__ __launch_bounds__(256) void k_integrate_reset(unsigned long long* cnt
   if (i < kShards * kShardWords) ish[i] = 0ull;
 }
 
-// Front-end -> accumulation hand-off across the two streams (dm_set_overlap)
-// without a cross-queue event wait, which holds the map stream ~10 us even
-// when the front-end finished long before.  k_fe_signal runs on the
-// front-end stream after k_scatter (the kernel boundary has written its
-// outputs back) and stores the call's sequence number; k_fe_gate, one lane
-// on the map stream right before k_tile_accum, polls that word and exits;
-// k_tile_accum's own kernel-boundary acquire then sees the front-end's
-// outputs.  No deadlock: the gate holds one workgroup slot, and everything
-// the front-end waits for is ahead of the gate on the map stream.  Bounded:
-// after kFeGateTicks of the 100 MHz wall clock the gate sets flag 8 in the
-// call's CNT_IOVERFLOW (DM_ERR_CAPACITY at dm_last_counts) and exits.
-constexpr unsigned long long kFeGateTicks = 500000000ull;  // 5 s
+// Hand-off between two streams without a cross-queue event wait, which
+// holds the waiting stream ~10 us even when its producer finished long
+// before.  k_seq_signal runs on the producing stream after the producer
+// kernels (the kernel boundary has written their outputs back) and stores a
+// sequence number; k_seq_gate, one lane on the consuming stream, polls that
+// word and exits, and the consumer kernels' own kernel-boundary acquire then
+// sees the outputs.  Uses: the integrate front-end -> k_tile_accum (flag
+// fe_flag), a frontier pass's bit rows -> its labelling half on pass_stream
+// (bits_flag).  No deadlock: the gate holds one workgroup slot, and all the
+// producer waits for is ahead of the gate on the consuming stream.  Bounded:
+// after kGateTicks of the 100 MHz wall clock the gate sets err_bit in *err
+// (the consumer's result is then reported as an error) and exits.
+constexpr unsigned long long kGateTicks = 500000000ull;  // 5 s
 
-__global__ __launch_bounds__(64) void k_fe_signal(unsigned long long* flag, unsigned long long seq) {
+__global__ __launch_bounds__(64) void k_seq_signal(unsigned long long* flag, unsigned long long seq) {
   if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(64) void k_fe_gate(const unsigned long long* flag, unsigned long long seq,
-                                                unsigned long long* cnt) {
+__global__ __launch_bounds__(64) void k_seq_gate(const unsigned long long* flag, unsigned long long seq,
+                                                 unsigned long long* err, unsigned long long err_bit) {
   if (threadIdx.x != 0) return;
   const unsigned long long t0 = wall_clock64();
   while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < seq) {
     __builtin_amdgcn_s_sleep(2);
-    if (wall_clock64() - t0 > kFeGateTicks) {
-      atomicOr(&cnt[CNT_IOVERFLOW], 8ull);
+    if (wall_clock64() - t0 > kGateTicks) {
+      atomicOr(err, err_bit);
       return;
     }
   }
@@ -1044,10 +1045,8 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
     DM_HIP(hipStreamWaitEvent(g->stream, g->ev_fe, 0));
   } else if (g->overlap) {
     const unsigned long long seq = ++g->fe_seq;
-    hipLaunchKernelGGL(k_fe_signal, dim3(1), dim3(64), 0, fs, g->fe_flag, seq);
-    DM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_fe_gate, dim3(1), dim3(64), 0, g->stream, g->fe_flag, seq, w.cnt);
-    DM_HIP(hipGetLastError());
+    if (int rc = dm_launch_signal(fs, g->fe_flag, seq)) return rc;
+    if (int rc = dm_launch_gate(g->stream, g->fe_flag, seq, w.cnt + CNT_IOVERFLOW, 8ull)) return rc;
   }
   const int vec_ok = (g->W % 4 == 0) ? 1 : 0;
   // heavy chunks and medium tiles first (the long items), then the light
@@ -1072,6 +1071,19 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                      make_apply(g), w.heavy_list, w.tile_count, g->tile_free, w.slabs, g->L, g->state,
                      w.cnt, w.sh);
   dm_timer_end(g, &t);
+  DM_HIP(hipGetLastError());
+  return DM_OK;
+}
+
+int dm_launch_signal(hipStream_t s, unsigned long long* flag, unsigned long long seq) {
+  hipLaunchKernelGGL(k_seq_signal, dim3(1), dim3(64), 0, s, flag, seq);
+  DM_HIP(hipGetLastError());
+  return DM_OK;
+}
+
+int dm_launch_gate(hipStream_t s, const unsigned long long* flag, unsigned long long seq,
+                   unsigned long long* err, unsigned long long err_bit) {
+  hipLaunchKernelGGL(k_seq_gate, dim3(1), dim3(64), 0, s, flag, seq, err, err_bit);
   DM_HIP(hipGetLastError());
   return DM_OK;
 }

@@ -37,8 +37,8 @@ enum {
   CNT_HEAVY = 9,    // heavy tiles (> 256 pieces)
   CNT_TH = 10,      // touched cells of heavy tiles
   CNT_SORTED = 11,  // 1: out_clu holds the clusters sorted by label
-  CNT_FL0 = 12,     // frontier tile-list length, even calls (zeroed by the odd calls)
-  CNT_FL1 = 13,     // frontier tile-list length, odd calls (zeroed by the even calls)
+  CNT_FL0 = 12,     // frontier tile-list length of the pass (copied by k_frontier_bits)
+  CNT_FL1 = 13,     // (unused)
   CNT_LITEMS = 14,  // light work items (= light tiles)
   CNT_IOVERFLOW = 15,  // integrate capacity overflow flags (1 first-touch list, 2 pieces, 4 work lists)
   CNT_BIG = 16,     // frontier tiles with more runs than a tile-wave holds (big-tile list length)
@@ -47,6 +47,7 @@ enum {
 // CNT_OVERFLOW bits of a frontier pass
 constexpr unsigned long long kOvSlots = 4ull;      // a slot shard region overflowed
 constexpr unsigned long long kOvUnionFind = 8ull;  // a union-find loop hit its bound (dm_uf.h)
+constexpr unsigned long long kOvGate = 16ull;      // the pass stream's hand-off gate timed out
 // Integrate counters, zeroed by each integrate call; the others belong to the
 // frontier pass, which may still be running when the next call's front-end
 // starts (dm_set_overlap), so the integrate reset never touches them.
@@ -214,14 +215,49 @@ struct dm_grid {
   int32_t last_S = 0, last_N = 0;
 
   // frontier workspace
+  // What a pass's prep and bit kernels write on `stream` while the previous
+  // pass's labelling may still run on pass_stream is double-buffered by pass
+  // parity (fparity): counters, shards, list, frontier bit rows, edge slots,
+  // slot parents.  The current set's arrays are also reachable through the
+  // plain fields below (dm_select_fw).  A set is reused two passes later; its
+  // previous pass must be done by then (busy: the event that pass recorded,
+  // waited on by `stream` unless the host already saw it complete).
+  struct FrWs {
+    unsigned long long* cnt = nullptr;  // [CNT_N]
+    unsigned long long* fsh = nullptr;  // [kShards][kShardWords]
+    int32_t* ftiles = nullptr;          // [NT]
+    int32_t* big_tiles = nullptr;       // [NT]
+    uint64_t* fbits = nullptr;          // [NT][64]
+    int32_t* edge_slot = nullptr;       // [2][W]
+    int32_t* slot_parent = nullptr;     // [slot_cap]
+    hipEvent_t busy = nullptr;          // the last pass's end (an alias of its readback event)
+    bool busy_pending = false;
+    uint64_t busy_pass = 0;             // fr_pass of that pass
+  };
+  FrWs fw[2];
+  // tile-list lengths, a ring of three on separate lines: pass n counts into
+  // fl_n[16 * (n % 3)] and zeroes the next one (last used by pass n - 2)
+  unsigned long long* fl_n = nullptr;
+  // pass_stream (dm_set_overlap + dm_frontiers_begin): the labelling half of
+  // a pass (tile kernels, resolve, sort) runs there, after the prep and the
+  // bit-row kernel on `stream` (which alone read the map), so the next
+  // batch's map update overlaps it.  bits_flag / bits_seq: the bit rows'
+  // hand-off (k_seq_signal on `stream`, k_seq_gate on pass_stream).
+  hipStream_t pass_stream = nullptr;
+  unsigned long long* bits_flag = nullptr;
+  unsigned long long bits_seq = 0;
+  hipEvent_t p_tail = nullptr;        // the last pass_stream pass's end (alias)
+  bool p_pending = false;             // pass_stream work `stream` has not been ordered after
+  uint64_t p_tail_pass = 0;
   int32_t* ftiles = nullptr;   // tiles with free cells (built by k_frontier_prep)
-  int32_t* big_tiles = nullptr;  // [NT] tiles left to k_frontier_tile_big (too many runs for a tile-wave)
+  int32_t* big_tiles = nullptr;  // [NT] list positions left to k_frontier_tile_big (too many runs for a tile-wave)
+  uint64_t* fbits = nullptr;   // [NT][64] frontier bit rows of the listed tiles (k_frontier_bits)
   int32_t* border = nullptr;   // [tile][4][64] slot ids of a tile's edges (published sides only)
   // tile-edge hand-off words of k_frontier_tile, [4][NT]: horizontal (t, t+1),
   // vertical (t, t+TX), diagonal (t, t+TX+1), anti-diagonal (t, t+TX-1) pairs,
   // each (pass stamp << 2 | arrived sides); never reset (stamped)
   unsigned long long* rel = nullptr;
-  int32_t fparity = 0;         // which CNT_FL* counter the last frontier call used
+  int32_t fparity = 0;         // workspace set (fw) of the last frontier pass
   int64_t border_cap = 0;      // in tiles
   int64_t slot_cap = 0;
   long long* slot_label = nullptr;
@@ -301,6 +337,27 @@ inline hipError_t dm_mark_ws_free(dm_grid* g, hipEvent_t recorded = nullptr) {
   return hipSuccess;
 }
 
+// Point the current-set views (cnt, fsh, ftiles, big_tiles, fbits,
+// edge_slot, slot_parent) at frontier workspace set `s`.
+inline void dm_select_fw(dm_grid* g, int s) {
+  const dm_grid::FrWs& f = g->fw[s];
+  g->cnt = f.cnt;
+  g->fsh = f.fsh;
+  g->ftiles = f.ftiles;
+  g->big_tiles = f.big_tiles;
+  g->fbits = f.fbits;
+  g->edge_slot = f.edge_slot;
+  g->slot_parent = f.slot_parent;
+}
+
+// Order `stream` after the pass_stream work enqueued so far (the frontier
+// arrays other than the parity sets are shared by all passes).
+inline hipError_t dm_join_pass_stream(dm_grid* g) {
+  if (!g->p_pending) return hipSuccess;
+  g->p_pending = false;
+  return hipStreamWaitEvent(g->stream, g->p_tail, 0);
+}
+
 // A call with too few beams to fill the chip enumerates each beam's pieces
 // in `chunks` k-ranges on different threads (k_beam_prep / k_scatter): one
 // thread per beam would walk up to 2*nmax/64 pieces serially on a mostly
@@ -320,7 +377,16 @@ int dm_launch_recount(dm_grid* g);
 int dm_launch_state_from_logodds(dm_grid* g);
 int dm_launch_map_image(dm_grid* g, uint8_t* d_img);
 int dm_launch_set_state(dm_grid* g, const int8_t* d_state_in);
-int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels);
+// split: the labelling half on g->pass_stream (dm_frontiers_begin with
+// overlap); *end_stream receives the stream the pass ends on.
+int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool split = false,
+                         hipStream_t* end_stream = nullptr);
+// Sequence hand-off between streams (dm_integrate.hip): k_seq_signal stores
+// seq into *flag; k_seq_gate (one lane) waits until *flag >= seq, or sets
+// err_bit in *err after a bounded time.
+int dm_launch_signal(hipStream_t s, unsigned long long* flag, unsigned long long seq);
+int dm_launch_gate(hipStream_t s, const unsigned long long* flag, unsigned long long seq,
+                   unsigned long long* err, unsigned long long err_bit);
 int dm_launch_edge_labels(dm_grid* g);
 int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied);
 int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters,
@@ -340,7 +406,7 @@ constexpr int kBuckets = 4096;  // row buckets of the bucket sort (k_bs_scan: 4 
 int dm_grow_bucket_sort(dm_grid* g, int64_t n);
 // Row-bucket sort of the raw records (labels of rows [row_base, row_base +
 // rows)): same outputs, readback header and flags as dm_launch_rank_sort.
-int dm_launch_bucket_sort(dm_grid* g, long long* clusters, const long long* sums,
+int dm_launch_bucket_sort(dm_grid* g, hipStream_t stream, long long* clusters, const long long* sums,
                           const long long* labels, const unsigned long long* d_count,
                           int64_t max_records, int64_t row_base, int64_t rows, dm_cluster* out,
                           int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,

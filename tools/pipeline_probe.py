@@ -33,27 +33,27 @@ def main():
         p4, r = dpool[k % len(dpool)]
         m.integrate_device(p4.data_ptr(), S, r.data_ptr(), N, amin, inc)
 
-    for rep in range(2):
+    for depth in (1, 2, 1, 2):
         ti, te, tb = [], [], []
         t0 = time.perf_counter()
-        integrate(0)
-        m.frontiers_begin()
-        steps = 30
-        for k in range(1, steps):
+        steps = 60
+        for k in range(steps):
             a = time.perf_counter()
             integrate(k)
             b = time.perf_counter()
-            m.frontiers_end()
+            if k >= depth:
+                m.frontiers_end()
             c = time.perf_counter()
             m.frontiers_begin()
             d = time.perf_counter()
             ti.append(b - a)
             te.append(c - b)
             tb.append(d - c)
-        m.frontiers_end()
+        for _ in range(depth):
+            m.frontiers_end()
         el = time.perf_counter() - t0
-        f = lambda v: 1e6 * float(np.median(v))
-        print(f"rep {rep}: {1e6 * el / steps:.1f} us/step; integrate call {f(ti):.1f}, "
+        f = lambda v: 1e6 * float(np.median(v[depth:]))
+        print(f"depth {depth}: {1e6 * el / steps:.1f} us/step; integrate call {f(ti):.1f}, "
               f"frontiers_end {f(te):.1f}, frontiers_begin {f(tb):.1f} us (medians)", flush=True)
     m.close()
 
