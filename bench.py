@@ -189,7 +189,9 @@ def main():
     # unchanged, only independent kernels overlap.
     pipelined = not args.no_overlap
 
-    def run_steps(k0, n, integ=None):
+    def run_steps(k0, n, integ=None, marks=None):
+        """n steps from batch k0; marks (a list) receives the host clock at
+        every step's start and at the end (the step cadence record)."""
         integ = integ or integrate
         if n <= 0:
             return None
@@ -205,12 +207,16 @@ def main():
         depth = max(1, min(args.depth, n))
         fr = None
         for k in range(n):
+            if marks is not None:
+                marks.append(time.perf_counter())
             integ(k0 + k)
             if k >= depth:
                 mapper.frontiers_end()
             mapper.frontiers_begin()
         for _ in range(min(depth, n)):
             fr = mapper.frontiers_end()
+        if marks is not None:
+            marks.append(time.perf_counter())
         # None: the pass overflowed a capacity (grown now); rerun on this map
         return fr if fr is not None else mapper.frontiers()
 
@@ -225,7 +231,8 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    fr = run_steps(args.warmup, args.steps)
+    marks = []
+    fr = run_steps(args.warmup, args.steps, marks=marks)
     band.synchronize()
     torch.cuda.synchronize()
     barrier()
@@ -408,6 +415,9 @@ def main():
             if pipelined else None,
             "cpu_baseline": cpu,
             "gen_seconds": t_gen,
+            # host-side start-to-start time of each timed step (rank 0): a
+            # host stall shows here as a long tail, kernel time in `roofline`
+            "step_wall_us": _cadence(marks),
         }
         print(json.dumps(result), flush=True)
     mapper.close()
@@ -571,6 +581,17 @@ def _cpu_model():
 # the C5 beam-density sweep.  Same step definition as C3 (integrate + full
 # frontier extraction, pipelined), same roofline bookkeeping.
 # ---------------------------------------------------------------------------
+
+def _cadence(marks):
+    """p50 / p90 / max of the gaps between consecutive host clock marks (us)."""
+    import numpy as np
+
+    if len(marks) < 2:
+        return None
+    d = np.diff(np.asarray(marks)) * 1e6
+    return {"p50": float(np.percentile(d, 50)), "p90": float(np.percentile(d, 90)),
+            "max": float(d.max()), "n": int(d.size)}
+
 
 def _profiled_roofline(band, run, U_mean, T_mean, TH_mean):
     """Per-kernel average launch time (HIP events on the library's stream)

@@ -452,6 +452,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     DM_HIP(hipMemset(w.sh, 0, sizeof(unsigned long long) * kShards * kShardWords));
   }
   if ((rc = dev_alloc(&g->tile_free, g->NT, "tile free counts"))) return fail(rc);
+  if ((rc = dev_alloc(&g->fmask, g->NT * 2 * DM_TILE, "tile free / unknown bit rows"))) return fail(rc);
   {
     const char* sep = getenv("DM_HEAVY_SEPARATE");
     g->fuse_heavy = !(sep && sep[0] == '1');
@@ -558,7 +559,7 @@ int dm_destroy(dm_grid* g) {
     dev_free(w.pieces); dev_free(w.hitems); dev_free(w.litems); dev_free(w.heavy_list); dev_free(w.slabs);
     dev_free(w.heavy_done); dev_free(w.tile_count); dev_free(w.tile_cur); dev_free(w.cnt); dev_free(w.sh);
   }
-  dev_free(g->L); dev_free(g->state);
+  dev_free(g->L); dev_free(g->state); dev_free(g->fmask);
   dev_free(g->tile_free); dev_free(g->beams); dev_free(g->blk_hist); dev_free(g->blk_n);
   dev_free(g->trig);
   dev_free(g->pose4); dev_free(g->ranges); 
@@ -591,6 +592,7 @@ int dm_reset(dm_grid* g) {
   for (auto& w : g->iw)
     DM_HIP(hipMemsetAsync(w.tile_count, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
   DM_HIP(hipMemsetAsync(g->tile_free, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
+  if ((rc = dm_launch_recount(g))) return rc;  // fmask: every in-grid cell unknown
   for (auto& f : g->fw) DM_HIP(hipMemsetAsync(f.cnt, 0, sizeof(unsigned long long) * CNT_N, g->stream));
   DM_HIP(hipStreamSynchronize(g->stream));
   return DM_OK;

@@ -629,9 +629,16 @@ __device__ inline void edge_unions(int32_t sl, const int32_t* border, int32_t nb
 // cells are "not unknown").  The only kernel of a pass that reads the map:
 // with dm_set_overlap the next batch's map update may start right after it,
 // while the labelling kernels below (which read only these rows) run on the
-// pass stream.  Also copies the list length into the pass's counters.
+// pass stream.  The map is read as the per-tile free / unknown bit rows
+// (fmask, kept by the integrate apply): the tile's 2 x 512 B, the unknown
+// rows of its left / right neighbours (bit 63 / bit 0 of each) and one word
+// of each of the six tiles above and below — ~2 KB of coalesced loads
+// instead of the tile's 4 KB of state bytes plus ~130 scattered halo lines.
+// Tiles next to a band halo (sharded maps) read the state bytes and the
+// halo rows instead.  Also copies the list length into the pass's counters.
 __global__ __launch_bounds__(kFW * 64) void k_frontier_bits(FGeom g, const int8_t* __restrict__ state,
                                                             const int8_t* __restrict__ halo,
+                                                            const uint64_t* __restrict__ fmask,
                                                             const int32_t* __restrict__ ftiles,
                                                             const unsigned long long* __restrict__ list_n,
                                                             uint64_t* __restrict__ fbits,
@@ -643,10 +650,33 @@ __global__ __launch_bounds__(kFW * 64) void k_frontier_bits(FGeom g, const int8_
   // the 128-byte lines of their rows and halo columns
   for (int64_t jj = (int64_t)blockIdx.x * kFW + w; jj < nft; jj += (int64_t)gridDim.x * kFW) {
     const int32_t tile = __builtin_amdgcn_readfirstlane(ftiles[jj]);
-    const int32_t tx0 = (tile % g.TX) * DM_TS, ty0 = (tile / g.TX) * DM_TS;  // ty0 band-local
+    const int32_t tx = tile % g.TX, ty = tile / g.TX;
+    const int32_t tx0 = tx * DM_TS, ty0 = ty * DM_TS;  // ty0 band-local
     uint64_t U, Fr, Ue;
     uint32_t uL, uR, eL, eR;
-    tile_rows(g, state, halo, tx0, ty0, lane, U, Fr, uL, uR, Ue, eL, eR);
+    if ((ty == 0 && g.has_before) || (ty == g.TY - 1 && g.has_after)) {
+      tile_rows(g, state, halo, tx0, ty0, lane, U, Fr, uL, uR, Ue, eL, eR);
+    } else {
+      const uint64_t* rec = fmask + (int64_t)tile * (2 * DM_TS);
+      constexpr int kU = DM_TS;  // unknown rows follow the free rows
+      Fr = rec[lane];
+      U = rec[kU + lane];
+      uL = tx > 0 ? (uint32_t)(rec[kU + lane - 2 * DM_TS] >> 63) : 0u;
+      uR = tx + 1 < g.TX ? (uint32_t)(rec[kU + lane + 2 * DM_TS] & 1ull) : 0u;
+      // lane 0: row -1 (the tile above, its row 63); lane 63: row 64 (the
+      // tile below, its row 0); eL / eR the diagonal neighbours' corner cells
+      Ue = 0ull;
+      eL = 0u;
+      eR = 0u;
+      const int32_t dy = lane == 0 ? -1 : 1;
+      if ((lane == 0 && ty > 0) || (lane == 63 && ty + 1 < g.TY)) {
+        const int64_t nt = (int64_t)tile + (int64_t)dy * g.TX;
+        const int row = lane == 0 ? DM_TS - 1 : 0;
+        Ue = fmask[nt * (2 * DM_TS) + kU + row];
+        if (tx > 0) eL = (uint32_t)(fmask[(nt - 1) * (2 * DM_TS) + kU + row] >> 63);
+        if (tx + 1 < g.TX) eR = (uint32_t)(fmask[(nt + 1) * (2 * DM_TS) + kU + row] & 1ull);
+      }
+    }
     const uint64_t h = dilate_row(U, uL, uR);
     const uint64_t he = dilate_row(Ue, eL, eR);
     uint64_t hu = __shfl_up(h, 1);
@@ -1484,7 +1514,7 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   const int wave_grid = grid_for(std::min<int64_t>(want_waves, g->NT), kFW, 8192);
   dm_timer_begin(g, "frontier_bits", &t);
   hipLaunchKernelGGL(k_frontier_bits, dim3(wave_grid), dim3(kFW * 64), 0, g->stream, fg, g->state, g->halo,
-                     g->ftiles, list_n, g->fbits, g->cnt);
+                     g->fmask, g->ftiles, list_n, g->fbits, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   // the map has been read: with split, the rest runs on the pass stream,

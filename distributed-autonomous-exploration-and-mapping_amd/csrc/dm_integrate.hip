@@ -383,6 +383,15 @@ __device__ inline float apply_one(const ApplyArgs& p, float L, uint32_t h, uint3
   return __builtin_amdgcn_fmed3f(L, p.l_min, p.l_max);
 }
 
+// Bit j of x (16 bits) to bit 4j.
+__device__ inline uint64_t spread4(uint64_t x) {
+  x = (x | (x << 24)) & 0x000000FF000000FFull;
+  x = (x | (x << 12)) & 0x000F000F000F000Full;
+  x = (x | (x << 6)) & 0x0303030303030303ull;
+  x = (x | (x << 3)) & 0x1111111111111111ull;
+  return x;
+}
+
 // Number of zero bytes of x (exact, no false positives).
 __device__ inline int32_t zero_bytes(uint32_t x) {
   uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
@@ -426,9 +435,12 @@ struct CellRows {
   template <class Counts>
   __device__ void apply(const Geom& g, const ApplyArgs& p, int32_t tx0, int32_t ty0, int ly0, int dly,
                         int cx, float* __restrict__ L, int8_t* __restrict__ state, Counts&& counts,
-                        int32_t* sh_T, int32_t* sh_free, uint32_t* sh_U) {
+                        int32_t* sh_T, int32_t* sh_free, uint32_t* sh_U, uint64_t* __restrict__ tmask) {
     int32_t dT = 0, dFree = 0;
     uint32_t dU = 0;
+    uint32_t fin[ROWS];  // the 4 cells' final state bytes per row (vec tiles)
+#pragma unroll
+    for (int rr = 0; rr < ROWS; ++rr) fin[rr] = *reinterpret_cast<const uint32_t*>(&s[rr]);
 #pragma unroll
     for (int rr = 0; rr < ROWS; ++rr) {
       const int ly = ly0 + rr * dly;
@@ -456,6 +468,7 @@ struct CellRows {
           dT += hit ? 1 : 0;
         }
         const char4 ns4 = make_char4(sv[0], sv[1], sv[2], sv[3]);
+        fin[rr] = *reinterpret_cast<const uint32_t*>(&ns4);
         dFree += zero_bytes(*reinterpret_cast<const uint32_t*>(&ns4)) -
                  zero_bytes(*reinterpret_cast<const uint32_t*>(&s[rr]));
         *reinterpret_cast<float4*>(L + base) = make_float4(lv[0], lv[1], lv[2], lv[3]);
@@ -477,6 +490,38 @@ struct CellRows {
     if (dT) atomicAdd(sh_T, dT);
     if (dFree) atomicAdd(sh_free, dFree);
     if (dU) atomicAdd(sh_U, dU);
+    if (!tmask) return;
+    // the tile's free / unknown bit rows (fmask): this thread's 4 cells of
+    // each of its rows as nibbles; the 16 threads of a row are 16 consecutive
+    // lanes (cx = (tid & 15) * 4), so per nibble bit one ballot holds the bit
+    // for 4 rows, spread to every 4th bit of the row word
+    const int lane = __lane_id();
+#pragma unroll
+    for (int rr = 0; rr < ROWS; ++rr) {
+      const int ly = ly0 + rr * dly;
+      const int32_t y = ty0 + ly;
+      uint32_t fn = 0u, un = 0u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int32_t x = tx0 + cx + e;
+        if (y >= g.r.R || x >= g.r.W) continue;
+        // a non-vector row was applied cell by cell: read its bytes back
+        const int8_t b = vec ? (int8_t)((fin[rr] >> (8 * e)) & 0xFFu) : state[(int64_t)y * g.r.W + x];
+        fn |= (b == 0 ? 1u : 0u) << e;
+        un |= (b == -1 ? 1u : 0u) << e;
+      }
+      uint64_t fm = 0ull, um = 0ull;
+      const int sh = lane & 48;  // this lane's 16-lane row group
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        fm |= spread4((__ballot((fn >> e) & 1u) >> sh) & 0xFFFFull) << e;
+        um |= spread4((__ballot((un >> e) & 1u) >> sh) & 0xFFFFull) << e;
+      }
+      if ((lane & 15) == 0) {
+        tmask[ly] = fm;
+        tmask[DM_TS + ly] = um;
+      }
+    }
   }
 };
 
@@ -565,7 +610,7 @@ __device__ inline void finish_tile(const Geom& g, int32_t tile, int32_t T, int32
 __device__ inline void heavy_quarter(const Geom& g, const ApplyArgs& p, int64_t h, int q, int32_t tile,
                                      bool wide, uint32_t* __restrict__ slabs, float* __restrict__ L,
                                      int8_t* __restrict__ state, int32_t* s_T, int32_t* s_free,
-                                     uint32_t* s_U) {
+                                     uint32_t* s_U, uint64_t* __restrict__ fmask) {
   constexpr int kQ = DM_TS * DM_TS / 4;  // cells per quarter
   const int tid = threadIdx.x;
   const int32_t x = (tile % g.r.TX) * DM_TS + (tid & 63);
@@ -611,10 +656,26 @@ __device__ inline void heavy_quarter(const Geom& g, const ApplyArgs& p, int64_t 
     dU += hk + mk;
     dT += 1;
     dFree += (ns == 0) - (sv[k] == 0);
+    sv[k] = ns;
   }
   if (dT) atomicAdd(s_T, dT);
   if (dFree) atomicAdd(s_free, dFree);
   if (dU) atomicAdd(s_U, dU);
+  // the quarter's free / unknown bit rows (fmask): a wave is one row (lane =
+  // column), so one ballot per row and kind
+  uint64_t* tm = fmask + (int64_t)tile * (2 * DM_TS);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int32_t y = yq + 4 * k;
+    const bool in = y < g.r.R && x < g.r.W;
+    const uint64_t fm = __ballot(in && sv[k] == 0);
+    const uint64_t um = __ballot(in && sv[k] == -1);
+    if ((tid & 63) == 0) {
+      const int ly = q * (DM_TS / 4) + (tid >> 6) + 4 * k;
+      tm[ly] = fm;
+      tm[DM_TS + ly] = um;
+    }
+  }
 }
 
 // Per-cell hit/miss counts never touch HBM: a 256-thread workgroup takes one
@@ -645,7 +706,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     int cnt_b, const PackedPiece* __restrict__ pieces, int32_t* tile_count, int32_t* tile_free,
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
     const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok,
-    const int32_t* __restrict__ heavy_list, int32_t* heavy_done) {
+    const int32_t* __restrict__ heavy_list, int32_t* heavy_done, uint64_t* __restrict__ fmask) {
   __shared__ uint32_t tl[kTileWords + 64];  // + one spare word per lane (walk_piece_plain)
   __shared__ int32_t s_T, s_free, s_last;
   __shared__ uint32_t s_U;
@@ -752,7 +813,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
           const int64_t h = heavy >> 1;
           const bool wide = heavy_list[h] < 0;
           for (int q = 0; q < 4; ++q)
-            heavy_quarter(g, p, h, q, tile, wide, slabs, L, state, &s_T, &s_free, &s_U);
+            heavy_quarter(g, p, h, q, tile, wide, slabs, L, state, &s_T, &s_free, &s_U, fmask);
           __syncthreads();
           if (tid == 0) {
             finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
@@ -793,7 +854,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
                       m4[e] = v & 0xFFFFu;
                     }
                   },
-                  &s_T, &s_free, inside ? nullptr : &s_U);
+                  &s_T, &s_free, inside ? nullptr : &s_U, fmask + (int64_t)tile * (2 * DM_TS));
       DM_PH(dm_phase_acc_integrate, 4);
     }
     __syncthreads();
@@ -830,7 +891,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
 __global__ __launch_bounds__(kQuarter) void k_heavy_apply(
     Geom g, ApplyArgs p, const int32_t* __restrict__ heavy_list, int32_t* tile_count, int32_t* tile_free,
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
-    const unsigned long long* __restrict__ cnt, unsigned long long* ish) {
+    const unsigned long long* __restrict__ cnt, unsigned long long* ish, uint64_t* __restrict__ fmask) {
   __shared__ int32_t s_T, s_free;
   __shared__ uint32_t s_U;
   const int tid = threadIdx.x;
@@ -843,7 +904,7 @@ __global__ __launch_bounds__(kQuarter) void k_heavy_apply(
     const int32_t tile = hl & 0x7FFFFFFF;
     if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; }
     __syncthreads();
-    heavy_quarter(g, p, h, q, tile, hl < 0, slabs, L, state, &s_T, &s_free, &s_U);
+    heavy_quarter(g, p, h, q, tile, hl < 0, slabs, L, state, &s_T, &s_free, &s_U, fmask);
     __syncthreads();
     DM_PH(dm_phase_acc_integrate, 9);
     if (tid == 0) finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
@@ -895,17 +956,28 @@ __global__ __launch_bounds__(64) void k_seq_gate(const unsigned long long* flag,
   }
 }
 
+// Per-tile free counts and free / unknown bit rows (fmask) from the state
+// bytes, after a bulk state write (reset, dm_set_state, dm_set_logodds).
+// Element e of the loop is cell (e & 63, e >> 6): a wave is one row.
 __global__ __launch_bounds__(256) void k_recount(Geom g, const int8_t* __restrict__ state,
-                                                 int32_t* __restrict__ tile_free) {
+                                                 int32_t* __restrict__ tile_free, uint64_t* __restrict__ fmask) {
   const int64_t tile = blockIdx.x;
   const int32_t tx0 = (int32_t)(tile % g.r.TX) * DM_TS, ty0 = (int32_t)(tile / g.r.TX) * DM_TS;
   __shared__ int32_t acc;
   if (threadIdx.x == 0) acc = 0;
   __syncthreads();
   int32_t c = 0;
+  uint64_t* tm = fmask + tile * (2 * DM_TS);
   for (int e = threadIdx.x; e < DM_TS * DM_TS; e += 256) {
     const int32_t x = tx0 + (e & 63), y = ty0 + (e >> 6);
-    if (x < g.r.W && y < g.r.R) c += state[(int64_t)y * g.r.W + x] == 0;
+    const int8_t b = (x < g.r.W && y < g.r.R) ? state[(int64_t)y * g.r.W + x] : (int8_t)1;
+    c += b == 0;
+    const uint64_t fm = __ballot(b == 0);
+    const uint64_t um = __ballot(b == -1);
+    if ((e & 63) == 0) {
+      tm[e >> 6] = fm;
+      tm[DM_TS + (e >> 6)] = um;
+    }
   }
   if (c) atomicAdd(&acc, c);
   __syncthreads();
@@ -1056,7 +1128,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                      dim3(kQuarter), 0,
                      g->stream, ge, make_apply(g), w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS,
                      w.pieces, w.tile_count, g->tile_free, w.slabs, g->L, g->state, w.cnt, w.sh, vec_ok,
-                     w.heavy_list, g->fuse_heavy ? w.heavy_done : nullptr);
+                     w.heavy_list, g->fuse_heavy ? w.heavy_done : nullptr, g->fmask);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (g->overlap) w.free_owed = true;
@@ -1069,7 +1141,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   dm_timer_begin(g, "heavy_apply", &t);
   hipLaunchKernelGGL(k_heavy_apply, dim3(grid_for(4 * g->heavy_cap, 1, 1024)), dim3(kQuarter), 0, g->stream, ge,
                      make_apply(g), w.heavy_list, w.tile_count, g->tile_free, w.slabs, g->L, g->state,
-                     w.cnt, w.sh);
+                     w.cnt, w.sh, g->fmask);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   return DM_OK;
@@ -1091,7 +1163,7 @@ int dm_launch_gate(hipStream_t s, const unsigned long long* flag, unsigned long 
 int dm_launch_recount(dm_grid* g) {
   const Geom ge = make_geom(g);
   hipLaunchKernelGGL(k_recount, dim3((unsigned)g->NT), dim3(256), 0, g->stream, ge, g->state,
-                     g->tile_free);
+                     g->tile_free, g->fmask);
   DM_HIP(hipGetLastError());
   return DM_OK;
 }

@@ -159,6 +159,12 @@ struct dm_grid {
   float* L = nullptr;
   int8_t* state = nullptr;
   int32_t* tile_free = nullptr;
+  // [NT][2][64] per tile: free bit rows, then unknown bit rows (bit x of row
+  // y: the cell is free / unknown; out-of-grid cells are neither), kept in
+  // step with `state` by every kernel that writes it (k_tile_accum's apply,
+  // k_recount after bulk writes); the frontier pass reads these instead of
+  // the state bytes
+  uint64_t* fmask = nullptr;
   unsigned long long* cnt = nullptr;    // CNT_N device counters (frontier fields)
   unsigned long long* h_cnt = nullptr;  // pinned mirror: [CNT_N] frontier counters, [CNT_N] integrate counters
   unsigned long long* fsh = nullptr;    // [kShards][kShardWords] frontier shards
