@@ -285,6 +285,16 @@ int copy_clusters(dm_grid* g, bool sorted, int64_t n, int64_t nw, int64_t have,
   return DM_OK;
 }
 
+// The label-sorted device records of a collected result (slot's out_clu for
+// kind 1, m_out for kind 2), n records; n < 0: not sorted on the device.
+void note_goal_source(dm_grid* g, int slot, int kind, int64_t n) {
+  g->goal_slot = n >= 0 ? slot : -1;
+  g->goal_kind = kind;
+  g->goal_n = n;
+  g->goal_epoch = kind == 1 ? g->rb[slot].wepoch : g->rb[slot].mepoch;
+  g->goal_gen = g->rb_gen;
+}
+
 int grow_merge(dm_grid* g, int64_t n) {
   if (n <= g->m_cap) return DM_OK;
   int rc = dev_alloc(&g->m_parent, n, "merge parents");
@@ -452,11 +462,13 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     DM_HIP(hipMemset(w.sh, 0, sizeof(unsigned long long) * kShards * kShardWords));
   }
   if ((rc = dev_alloc(&g->tile_free, g->NT, "tile free counts"))) return fail(rc);
-  if ((rc = dev_alloc(&g->fmask, g->NT * 2 * DM_TILE, "tile free / unknown bit rows"))) return fail(rc);
+  if ((rc = dev_alloc(&g->fmask, g->NT * DM_TILE * 16, "tile free / unknown bit rows"))) return fail(rc);
   {
     const char* sep = getenv("DM_HEAVY_SEPARATE");
     g->fuse_heavy = !(sep && sep[0] == '1');
     g->fe_gate = !dm_env_off("DM_FE_GATE");
+    const char* fm = getenv("DM_FMASK");
+    g->fmask_mode = fm && !strcmp(fm, "on") ? 1 : (fm && !strcmp(fm, "off") ? 2 : 0);
     const char* fk = getenv("DM_FRONTIER_KERNEL");
     g->frontier_kernel = fk && !strcmp(fk, "wave") ? 1 : (fk && !strcmp(fk, "wg") ? 2 : 0);
   }
@@ -555,6 +567,8 @@ int dm_destroy(dm_grid* g) {
     dev_free(f.edge_slot); dev_free(f.slot_parent);
   }
   dev_free(g->fl_n); dev_free(g->bits_flag);
+  for (int b = 0; b < 2; ++b) { dev_free(g->goal_k[b]); dev_free(g->goal_i[b]); }
+  dev_free(g->goal_io); dev_free(g->goal_idx);
   for (auto& w : g->iw) {
     dev_free(w.pieces); dev_free(w.hitems); dev_free(w.litems); dev_free(w.heavy_list); dev_free(w.slabs);
     dev_free(w.heavy_done); dev_free(w.tile_count); dev_free(w.tile_cur); dev_free(w.cnt); dev_free(w.sh);
@@ -808,6 +822,7 @@ int dm_frontiers(dm_grid* g, uint8_t* mask, int64_t* labels, dm_cluster* out, in
   if (rc) return rc == DM_ERR_CAPACITY ? dm_set_error(rc, "frontier slot arrays kept overflowing") : rc;
   g->frontier_valid = true;
   const int64_t nw = std::min<int64_t>(n, cap);
+  note_goal_source(g, slot, 1, g->h_cnt[CNT_SORTED] != 0 ? n : -1);
   if ((rc = copy_clusters(g, g->h_cnt[CNT_SORTED] != 0, n, nw, copied, g->out_clu, g->clusters, out)))
     return rc;
   if ((rc = grow_host_out(g, slot, n + n / 4 + 64))) return rc;
@@ -904,6 +919,7 @@ int merge_readback(dm_grid* g, int slot, int64_t n, dm_cluster* out, int64_t cap
       (g->rb[slot].gen != g->rb_gen || (!g->h_mcnt[2] && g->rb[slot].pass != g->m_pass)))
     return dm_set_error(DM_ERR_INCOMPLETE, "merge result lost to a workspace reallocation or a later "
                                            "unsorted merge: rerun");
+  note_goal_source(g, slot, 2, g->h_mcnt[2] != 0 ? K : -1);
   int rc = copy_clusters(g, g->h_mcnt[2] != 0, K, K, hint, g->m_out, g->m_clu, out);
   if (rc) return rc;
   return grow_host_out(g, slot, K + K / 4 + 64);
@@ -1027,10 +1043,73 @@ int dm_frontiers_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out) {
   // the slot data (dm_get_edge_labels) describes the map only if this was
   // the last pass and no map change came in between
   g->frontier_valid = g->rb_count == 1 && r.seq == g->integrate_seq;
+  note_goal_source(g, slot, 1, sorted ? n : -1);
   rc = copy_clusters(g, sorted, n, n, copied, g->out_clu, g->clusters, out);
   retire_oldest(g);
   if (rc) return rc;
   return grow_host_out(g, slot, n + n / 4 + 64);
+}
+
+int dm_assign_goals(dm_grid* g, const double* robots_xy, int32_t n_robots, int64_t min_size,
+                    double distance_weight, double min_distance, int64_t* out_index, double* out_xy) {
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (n_robots < 0 || n_robots > 256)
+    return dm_set_error(DM_ERR_INVALID_ARG, "n_robots must be in [0, 256] (got %d)", n_robots);
+  if (n_robots > 0 && (!robots_xy || !out_index || !out_xy))
+    return dm_set_error(DM_ERR_INVALID_ARG, "robots_xy / out_index / out_xy is NULL");
+  if (!isfinite(distance_weight) || !isfinite(min_distance))
+    return dm_set_error(DM_ERR_INVALID_ARG, "distance_weight / min_distance must be finite");
+  const int s = g->goal_slot;
+  if (s < 0 || g->goal_gen != g->rb_gen ||
+      (g->goal_kind == 1 ? g->rb[s].wepoch : g->rb[s].mepoch) != g->goal_epoch)
+    return dm_set_error(DM_ERR_INVALID_ARG, "no collected frontier result on the device (call dm_frontiers, "
+                                            "dm_frontiers_end or dm_merge_bands first; a later pass may have "
+                                            "reused its readback slot)");
+  if (n_robots == 0) return DM_OK;
+  const dm_cluster* recs = g->goal_kind == 1 ? g->rb[s].out_clu : g->rb[s].m_out;
+  const int64_t K = g->goal_n;
+  if (!g->goal_io) {
+    DM_HIP(hipMalloc((void**)&g->goal_io, sizeof(double) * 4 * 256));
+    DM_HIP(hipMalloc((void**)&g->goal_idx, sizeof(int64_t) * 256));
+  }
+  DM_HIP(dm_join_pass_stream(g));
+  const int32_t R = n_robots, T = n_robots;
+  DM_HIP(hipMemcpyAsync(g->goal_io, robots_xy, sizeof(double) * 2 * (size_t)R, hipMemcpyHostToDevice,
+                        g->stream));
+  std::vector<int64_t> idx((size_t)R, -1);
+  if (K > 0) {
+    const unsigned long long* dk = nullptr;
+    const uint32_t* di = nullptr;
+    if ((rc = dm_launch_goal_topk(g, recs, K, g->goal_io, R, T, min_size, distance_weight, min_distance, &dk,
+                                  &di)))
+      return rc;
+    std::vector<unsigned long long> hk((size_t)R * T);
+    std::vector<uint32_t> hi((size_t)R * T);
+    DM_HIP(hipMemcpyAsync(hk.data(), dk, sizeof(unsigned long long) * hk.size(), hipMemcpyDeviceToHost,
+                          g->stream));
+    DM_HIP(hipMemcpyAsync(hi.data(), di, sizeof(uint32_t) * hi.size(), hipMemcpyDeviceToHost, g->stream));
+    DM_HIP(hipStreamSynchronize(g->stream));
+    // greedy in robot order over each robot's best-first list (its choice is
+    // within its first r + 1 entries: r clusters are taken before its turn)
+    for (int32_t r = 0; r < R; ++r) {
+      for (int32_t t = 0; t < T; ++t) {
+        if (hk[(size_t)r * T + t] == 0ull) break;  // no eligible cluster left in the list
+        const int64_t c = hi[(size_t)r * T + t];
+        if (std::find(idx.begin(), idx.begin() + r, c) != idx.begin() + r) continue;
+        idx[(size_t)r] = c;
+        break;
+      }
+    }
+  }
+  DM_HIP(hipMemcpyAsync(g->goal_idx, idx.data(), sizeof(int64_t) * (size_t)R, hipMemcpyHostToDevice,
+                        g->stream));
+  if ((rc = dm_launch_goal_gather(g, recs, g->goal_idx, R, g->goal_io + 2 * 256))) return rc;
+  DM_HIP(hipMemcpyAsync(out_xy, g->goal_io + 2 * 256, sizeof(double) * 2 * (size_t)R, hipMemcpyDeviceToHost,
+                        g->stream));
+  DM_HIP(hipStreamSynchronize(g->stream));
+  memcpy(out_index, idx.data(), sizeof(int64_t) * (size_t)R);
+  return DM_OK;
 }
 
 int dm_set_overlap(dm_grid* g, int32_t on) {

@@ -624,6 +624,21 @@ __device__ inline void edge_unions(int32_t sl, const int32_t* border, int32_t nb
   }
 }
 
+// The 64 bits of one fmask row (16 nibble bytes) of one kind: shift 0 the
+// free nibbles, 4 the unknown nibbles; each 4-byte word folds to 16 bits.
+__device__ inline uint64_t nib_row(uint4 v, int shift) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint64_t m = 0ull;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t x = (w[q] >> shift) & 0x0F0F0F0Fu;
+    x = (x | (x >> 4)) & 0x00FF00FFu;
+    x = (x | (x >> 8)) & 0x0000FFFFu;
+    m |= (uint64_t)x << (16 * q);
+  }
+  return m;
+}
+
 // Frontier bit rows of the listed tiles, one wave per tile (lane y = tile
 // row y): F = free & 3x3 dilation of unknown (out-of-grid / missing halo
 // cells are "not unknown").  The only kernel of a pass that reads the map:
@@ -638,11 +653,11 @@ __device__ inline void edge_unions(int32_t sl, const int32_t* border, int32_t nb
 // halo rows instead.  Also copies the list length into the pass's counters.
 __global__ __launch_bounds__(kFW * 64) void k_frontier_bits(FGeom g, const int8_t* __restrict__ state,
                                                             const int8_t* __restrict__ halo,
-                                                            const uint64_t* __restrict__ fmask,
+                                                            const uint8_t* __restrict__ fmask,
                                                             const int32_t* __restrict__ ftiles,
                                                             const unsigned long long* __restrict__ list_n,
                                                             uint64_t* __restrict__ fbits,
-                                                            unsigned long long* cnt) {
+                                                            unsigned long long* cnt, int use_fmask) {
   const int w = threadIdx.x >> 6, lane = __lane_id();
   const int64_t nft = (int64_t)*list_n;
   if (blockIdx.x == 0 && threadIdx.x == 0) cnt[CNT_FL0] = (unsigned long long)nft;
@@ -654,15 +669,18 @@ __global__ __launch_bounds__(kFW * 64) void k_frontier_bits(FGeom g, const int8_
     const int32_t tx0 = tx * DM_TS, ty0 = ty * DM_TS;  // ty0 band-local
     uint64_t U, Fr, Ue;
     uint32_t uL, uR, eL, eR;
-    if ((ty == 0 && g.has_before) || (ty == g.TY - 1 && g.has_after)) {
+    if (!use_fmask || (ty == 0 && g.has_before) || (ty == g.TY - 1 && g.has_after)) {
       tile_rows(g, state, halo, tx0, ty0, lane, U, Fr, uL, uR, Ue, eL, eR);
     } else {
-      const uint64_t* rec = fmask + (int64_t)tile * (2 * DM_TS);
-      constexpr int kU = DM_TS;  // unknown rows follow the free rows
-      Fr = rec[lane];
-      U = rec[kU + lane];
-      uL = tx > 0 ? (uint32_t)(rec[kU + lane - 2 * DM_TS] >> 63) : 0u;
-      uR = tx + 1 < g.TX ? (uint32_t)(rec[kU + lane + 2 * DM_TS] & 1ull) : 0u;
+      // fmask: [tile][row][16] nibble bytes (free | unknown << 4)
+      const uint8_t* rec = fmask + (int64_t)tile * (DM_TS * 16);
+      const uint4 v = *reinterpret_cast<const uint4*>(rec + lane * 16);
+      Fr = nib_row(v, 0);
+      U = nib_row(v, 4);
+      // column -1: the left tile's byte 15 bit 7; column 64: the right tile's
+      // byte 0 bit 4
+      uL = tx > 0 ? (uint32_t)(rec[lane * 16 + 15 - DM_TS * 16] >> 7) : 0u;
+      uR = tx + 1 < g.TX ? (uint32_t)((rec[lane * 16 + DM_TS * 16] >> 4) & 1u) : 0u;
       // lane 0: row -1 (the tile above, its row 63); lane 63: row 64 (the
       // tile below, its row 0); eL / eR the diagonal neighbours' corner cells
       Ue = 0ull;
@@ -672,9 +690,9 @@ __global__ __launch_bounds__(kFW * 64) void k_frontier_bits(FGeom g, const int8_
       if ((lane == 0 && ty > 0) || (lane == 63 && ty + 1 < g.TY)) {
         const int64_t nt = (int64_t)tile + (int64_t)dy * g.TX;
         const int row = lane == 0 ? DM_TS - 1 : 0;
-        Ue = fmask[nt * (2 * DM_TS) + kU + row];
-        if (tx > 0) eL = (uint32_t)(fmask[(nt - 1) * (2 * DM_TS) + kU + row] >> 63);
-        if (tx + 1 < g.TX) eR = (uint32_t)(fmask[(nt + 1) * (2 * DM_TS) + kU + row] & 1ull);
+        Ue = nib_row(*reinterpret_cast<const uint4*>(fmask + nt * (DM_TS * 16) + row * 16), 4);
+        if (tx > 0) eL = (uint32_t)(fmask[(nt - 1) * (DM_TS * 16) + row * 16 + 15] >> 7);
+        if (tx + 1 < g.TX) eR = (uint32_t)((fmask[(nt + 1) * (DM_TS * 16) + row * 16] >> 4) & 1u);
       }
     }
     const uint64_t h = dilate_row(U, uL, uR);
@@ -1489,6 +1507,7 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   // the pass stream (labelling of earlier passes) -- except for split passes,
   // which keep that order on the pass stream itself
   if (!split) DM_HIP(dm_join_pass_stream(g));
+  ++g->rb[g->cur_slot].wepoch;  // this pass rewrites the selected slot's records
   ++g->fr_pass;
   g->fparity ^= 1;
   dm_grid::FrWs& fw = g->fw[g->fparity];
@@ -1512,9 +1531,21 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   // list length (+25 %; the kernels grid-stride, so any count is covered)
   const int64_t want_waves = g->ftile_hint > 0 ? g->ftile_hint + g->ftile_hint / 4 + 64 : g->NT;
   const int wave_grid = grid_for(std::min<int64_t>(want_waves, g->NT), kFW, 8192);
+  // fmask while the passes list many tiles (dm_internal.h, fmask_on); a
+  // switch on rebuilds the records first unless they still match the state
+  const bool want_on = g->fmask_mode == 1 || (g->fmask_mode == 0 && g->ftile_hint >= kFmaskOnTiles);
+  const bool want_off = g->fmask_mode == 2 || (g->fmask_mode == 0 && g->ftile_hint < kFmaskOnTiles / 4);
+  if (!g->fmask_on && want_on) {
+    if (!g->fmask_valid) {
+      if (int rc = dm_launch_recount(g)) return rc;
+    }
+    g->fmask_on = true;
+  } else if (g->fmask_on && want_off) {
+    g->fmask_on = false;
+  }
   dm_timer_begin(g, "frontier_bits", &t);
   hipLaunchKernelGGL(k_frontier_bits, dim3(wave_grid), dim3(kFW * 64), 0, g->stream, fg, g->state, g->halo,
-                     g->fmask, g->ftiles, list_n, g->fbits, g->cnt);
+                     g->fmask, g->ftiles, list_n, g->fbits, g->cnt, g->fmask_on ? 1 : 0);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   // the map has been read: with split, the rest runs on the pass stream,

@@ -383,13 +383,29 @@ __device__ inline float apply_one(const ApplyArgs& p, float L, uint32_t h, uint3
   return __builtin_amdgcn_fmed3f(L, p.l_min, p.l_max);
 }
 
-// Bit j of x (16 bits) to bit 4j.
-__device__ inline uint64_t spread4(uint64_t x) {
-  x = (x | (x << 24)) & 0x000000FF000000FFull;
-  x = (x | (x << 12)) & 0x000F000F000F000Full;
-  x = (x | (x << 6)) & 0x0303030303030303ull;
-  x = (x | (x << 3)) & 0x1111111111111111ull;
-  return x;
+// Bits 0..3: which of the 4 bytes of w are 0 (free); bits 4..7: which are
+// 0xFF (unknown) — a state word's fmask byte.
+__device__ inline uint8_t state_nibbles(uint32_t w) {
+  auto zb = [](uint32_t v) {
+    uint32_t t = (v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+    t = ~(t | v | 0x7F7F7F7Fu);                 // 0x80 in each zero byte
+    return (((t >> 7) * 0x00204081u) >> 21) & 0xFu;
+  };
+  return (uint8_t)(zb(w) | (zb(~w) << 4));
+}
+
+// The same for the 4 cells from column x0 of row y read one by one (a ragged
+// tile column or an unaligned map: cells past the map's edge are neither).
+template <class G>
+__device__ inline uint8_t state_nibbles_at(const G& g, const int8_t* __restrict__ state, int32_t x0, int32_t y) {
+  uint32_t fn = 0u, un = 0u;
+  for (int e = 0; e < 4; ++e) {
+    if (x0 + e >= g.r.W) break;
+    const int8_t b = state[(int64_t)y * g.r.W + x0 + e];
+    fn |= (b == 0 ? 1u : 0u) << e;
+    un |= (b == -1 ? 1u : 0u) << e;
+  }
+  return (uint8_t)(fn | (un << 4));
 }
 
 // Number of zero bytes of x (exact, no false positives).
@@ -435,12 +451,9 @@ struct CellRows {
   template <class Counts>
   __device__ void apply(const Geom& g, const ApplyArgs& p, int32_t tx0, int32_t ty0, int ly0, int dly,
                         int cx, float* __restrict__ L, int8_t* __restrict__ state, Counts&& counts,
-                        int32_t* sh_T, int32_t* sh_free, uint32_t* sh_U, uint64_t* __restrict__ tmask) {
+                        int32_t* sh_T, int32_t* sh_free, uint32_t* sh_U) {
     int32_t dT = 0, dFree = 0;
     uint32_t dU = 0;
-    uint32_t fin[ROWS];  // the 4 cells' final state bytes per row (vec tiles)
-#pragma unroll
-    for (int rr = 0; rr < ROWS; ++rr) fin[rr] = *reinterpret_cast<const uint32_t*>(&s[rr]);
 #pragma unroll
     for (int rr = 0; rr < ROWS; ++rr) {
       const int ly = ly0 + rr * dly;
@@ -468,7 +481,6 @@ struct CellRows {
           dT += hit ? 1 : 0;
         }
         const char4 ns4 = make_char4(sv[0], sv[1], sv[2], sv[3]);
-        fin[rr] = *reinterpret_cast<const uint32_t*>(&ns4);
         dFree += zero_bytes(*reinterpret_cast<const uint32_t*>(&ns4)) -
                  zero_bytes(*reinterpret_cast<const uint32_t*>(&s[rr]));
         *reinterpret_cast<float4*>(L + base) = make_float4(lv[0], lv[1], lv[2], lv[3]);
@@ -490,38 +502,6 @@ struct CellRows {
     if (dT) atomicAdd(sh_T, dT);
     if (dFree) atomicAdd(sh_free, dFree);
     if (dU) atomicAdd(sh_U, dU);
-    if (!tmask) return;
-    // the tile's free / unknown bit rows (fmask): this thread's 4 cells of
-    // each of its rows as nibbles; the 16 threads of a row are 16 consecutive
-    // lanes (cx = (tid & 15) * 4), so per nibble bit one ballot holds the bit
-    // for 4 rows, spread to every 4th bit of the row word
-    const int lane = __lane_id();
-#pragma unroll
-    for (int rr = 0; rr < ROWS; ++rr) {
-      const int ly = ly0 + rr * dly;
-      const int32_t y = ty0 + ly;
-      uint32_t fn = 0u, un = 0u;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int32_t x = tx0 + cx + e;
-        if (y >= g.r.R || x >= g.r.W) continue;
-        // a non-vector row was applied cell by cell: read its bytes back
-        const int8_t b = vec ? (int8_t)((fin[rr] >> (8 * e)) & 0xFFu) : state[(int64_t)y * g.r.W + x];
-        fn |= (b == 0 ? 1u : 0u) << e;
-        un |= (b == -1 ? 1u : 0u) << e;
-      }
-      uint64_t fm = 0ull, um = 0ull;
-      const int sh = lane & 48;  // this lane's 16-lane row group
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        fm |= spread4((__ballot((fn >> e) & 1u) >> sh) & 0xFFFFull) << e;
-        um |= spread4((__ballot((un >> e) & 1u) >> sh) & 0xFFFFull) << e;
-      }
-      if ((lane & 15) == 0) {
-        tmask[ly] = fm;
-        tmask[DM_TS + ly] = um;
-      }
-    }
   }
 };
 
@@ -610,7 +590,7 @@ __device__ inline void finish_tile(const Geom& g, int32_t tile, int32_t T, int32
 __device__ inline void heavy_quarter(const Geom& g, const ApplyArgs& p, int64_t h, int q, int32_t tile,
                                      bool wide, uint32_t* __restrict__ slabs, float* __restrict__ L,
                                      int8_t* __restrict__ state, int32_t* s_T, int32_t* s_free,
-                                     uint32_t* s_U, uint64_t* __restrict__ fmask) {
+                                     uint32_t* s_U) {
   constexpr int kQ = DM_TS * DM_TS / 4;  // cells per quarter
   const int tid = threadIdx.x;
   const int32_t x = (tile % g.r.TX) * DM_TS + (tid & 63);
@@ -656,26 +636,10 @@ __device__ inline void heavy_quarter(const Geom& g, const ApplyArgs& p, int64_t 
     dU += hk + mk;
     dT += 1;
     dFree += (ns == 0) - (sv[k] == 0);
-    sv[k] = ns;
   }
   if (dT) atomicAdd(s_T, dT);
   if (dFree) atomicAdd(s_free, dFree);
   if (dU) atomicAdd(s_U, dU);
-  // the quarter's free / unknown bit rows (fmask): a wave is one row (lane =
-  // column), so one ballot per row and kind
-  uint64_t* tm = fmask + (int64_t)tile * (2 * DM_TS);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int32_t y = yq + 4 * k;
-    const bool in = y < g.r.R && x < g.r.W;
-    const uint64_t fm = __ballot(in && sv[k] == 0);
-    const uint64_t um = __ballot(in && sv[k] == -1);
-    if ((tid & 63) == 0) {
-      const int ly = q * (DM_TS / 4) + (tid >> 6) + 4 * k;
-      tm[ly] = fm;
-      tm[DM_TS + ly] = um;
-    }
-  }
 }
 
 // Per-cell hit/miss counts never touch HBM: a 256-thread workgroup takes one
@@ -706,7 +670,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     int cnt_b, const PackedPiece* __restrict__ pieces, int32_t* tile_count, int32_t* tile_free,
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
     const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok,
-    const int32_t* __restrict__ heavy_list, int32_t* heavy_done, uint64_t* __restrict__ fmask) {
+    const int32_t* __restrict__ heavy_list, int32_t* heavy_done) {
   __shared__ uint32_t tl[kTileWords + 64];  // + one spare word per lane (walk_piece_plain)
   __shared__ int32_t s_T, s_free, s_last;
   __shared__ uint32_t s_U;
@@ -813,7 +777,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
           const int64_t h = heavy >> 1;
           const bool wide = heavy_list[h] < 0;
           for (int q = 0; q < 4; ++q)
-            heavy_quarter(g, p, h, q, tile, wide, slabs, L, state, &s_T, &s_free, &s_U, fmask);
+            heavy_quarter(g, p, h, q, tile, wide, slabs, L, state, &s_T, &s_free, &s_U);
           __syncthreads();
           if (tid == 0) {
             finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
@@ -854,7 +818,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
                       m4[e] = v & 0xFFFFu;
                     }
                   },
-                  &s_T, &s_free, inside ? nullptr : &s_U, fmask + (int64_t)tile * (2 * DM_TS));
+                  &s_T, &s_free, inside ? nullptr : &s_U);
       DM_PH(dm_phase_acc_integrate, 4);
     }
     __syncthreads();
@@ -891,7 +855,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
 __global__ __launch_bounds__(kQuarter) void k_heavy_apply(
     Geom g, ApplyArgs p, const int32_t* __restrict__ heavy_list, int32_t* tile_count, int32_t* tile_free,
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
-    const unsigned long long* __restrict__ cnt, unsigned long long* ish, uint64_t* __restrict__ fmask) {
+    const unsigned long long* __restrict__ cnt, unsigned long long* ish) {
   __shared__ int32_t s_T, s_free;
   __shared__ uint32_t s_U;
   const int tid = threadIdx.x;
@@ -904,7 +868,7 @@ __global__ __launch_bounds__(kQuarter) void k_heavy_apply(
     const int32_t tile = hl & 0x7FFFFFFF;
     if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; }
     __syncthreads();
-    heavy_quarter(g, p, h, q, tile, hl < 0, slabs, L, state, &s_T, &s_free, &s_U, fmask);
+    heavy_quarter(g, p, h, q, tile, hl < 0, slabs, L, state, &s_T, &s_free, &s_U);
     __syncthreads();
     DM_PH(dm_phase_acc_integrate, 9);
     if (tid == 0) finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
@@ -956,32 +920,77 @@ __global__ __launch_bounds__(64) void k_seq_gate(const unsigned long long* flag,
   }
 }
 
-// Per-tile free counts and free / unknown bit rows (fmask) from the state
-// bytes, after a bulk state write (reset, dm_set_state, dm_set_logodds).
-// Element e of the loop is cell (e & 63, e >> 6): a wave is one row.
+// fmask bytes of a row of cells: byte j = free bits of cells 4j..4j+3 (low
+// nibble) | their unknown bits (high nibble), from the row's ballots.
+__device__ inline uint8_t fmask_byte(uint64_t fm, uint64_t um, int j) {
+  return (uint8_t)(((fm >> (4 * j)) & 0xFull) | (((um >> (4 * j)) & 0xFull) << 4));
+}
+
+// Per-tile free counts and fmask records from the state bytes, after a bulk
+// state write (reset, dm_set_state, dm_set_logodds).  Element e of the loop
+// is cell (e & 63, e >> 6): a wave is one row.
 __global__ __launch_bounds__(256) void k_recount(Geom g, const int8_t* __restrict__ state,
-                                                 int32_t* __restrict__ tile_free, uint64_t* __restrict__ fmask) {
+                                                 int32_t* __restrict__ tile_free, uint8_t* __restrict__ fmask) {
   const int64_t tile = blockIdx.x;
   const int32_t tx0 = (int32_t)(tile % g.r.TX) * DM_TS, ty0 = (int32_t)(tile / g.r.TX) * DM_TS;
   __shared__ int32_t acc;
   if (threadIdx.x == 0) acc = 0;
   __syncthreads();
   int32_t c = 0;
-  uint64_t* tm = fmask + tile * (2 * DM_TS);
+  uint8_t* tm = fmask + tile * (DM_TS * 16);
   for (int e = threadIdx.x; e < DM_TS * DM_TS; e += 256) {
     const int32_t x = tx0 + (e & 63), y = ty0 + (e >> 6);
     const int8_t b = (x < g.r.W && y < g.r.R) ? state[(int64_t)y * g.r.W + x] : (int8_t)1;
     c += b == 0;
     const uint64_t fm = __ballot(b == 0);
     const uint64_t um = __ballot(b == -1);
-    if ((e & 63) == 0) {
-      tm[e >> 6] = fm;
-      tm[DM_TS + (e >> 6)] = um;
-    }
+    const int l = e & 63;
+    if (l < 16) tm[(e >> 6) * 16 + l] = fmask_byte(fm, um, l);
   }
   if (c) atomicAdd(&acc, c);
   __syncthreads();
   if (threadIdx.x == 0) tile_free[tile] = acc;
+}
+
+// fmask records of the tiles this call's map update touched (its work items:
+// heavy chunks and medium tiles, then light tiles; a heavy tile appears once
+// per chunk and is rewritten with the same bytes), one wave per item, after
+// k_tile_accum on the grid stream.  Lane l reads the 16-byte chunk l % 4 of
+// tile rows l / 4, 16 + l / 4, ... (coalesced 64-byte row segments) and
+// stores its 4 nibble bytes per row.  Kept out of k_tile_accum, whose
+// registers are full at 7 workgroups per CU (inside it, every variant
+// measured 6-14 us slower per call).
+__global__ __launch_bounds__(256) void k_fmask_items(Geom g, const int4* __restrict__ list_a, int cnt_a,
+                                                     const int4* __restrict__ list_b, int cnt_b,
+                                                     const unsigned long long* __restrict__ cnt,
+                                                     const int8_t* __restrict__ state, uint8_t* __restrict__ fmask) {
+  const int64_t HI = min((int64_t)cnt[cnt_a], g.hitem_cap);
+  const int64_t LI = min((int64_t)cnt[cnt_b], (int64_t)g.act_cap);
+  const int lane = __lane_id();
+  for (int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); it < HI + LI; it += (int64_t)gridDim.x * 4) {
+    const int32_t tile = __builtin_amdgcn_readfirstlane(it < HI ? list_a[it].x : list_b[it - HI].x);
+    const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
+    const int32_t x0 = tx0 + (lane & 3) * 16;
+    uint8_t* tm = fmask + (int64_t)tile * (DM_TS * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ly = 16 * q + (lane >> 2);
+      const int32_t y = ty0 + ly;
+      uint32_t out = 0u;
+      if (y < g.r.R) {
+        const int64_t off = (int64_t)y * g.r.W + x0;
+        if (x0 + 16 <= g.r.W && (off & 15) == 0) {
+          const uint4 v = *reinterpret_cast<const uint4*>(state + off);
+          const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) out |= (uint32_t)state_nibbles(wd[k]) << (8 * k);
+        } else {
+          for (int k = 0; k < 4; ++k) out |= (uint32_t)state_nibbles_at(g, state, x0 + 4 * k, y) << (8 * k);
+        }
+      }
+      *reinterpret_cast<uint32_t*>(tm + ly * 16 + (lane & 3) * 4) = out;
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_state_from_l(ApplyArgs p, int64_t cells, const float* __restrict__ L,
@@ -1128,7 +1137,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                      dim3(kQuarter), 0,
                      g->stream, ge, make_apply(g), w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS,
                      w.pieces, w.tile_count, g->tile_free, w.slabs, g->L, g->state, w.cnt, w.sh, vec_ok,
-                     w.heavy_list, g->fuse_heavy ? w.heavy_done : nullptr, g->fmask);
+                     w.heavy_list, g->fuse_heavy ? w.heavy_done : nullptr);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (g->overlap) w.free_owed = true;
@@ -1137,11 +1146,23 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   // beams are chunked).  Calls that cannot reach kMedium pieces in any tile
   // (one 360-beam scan: C1 / C2) have no heavy tile: no k_heavy_apply.
   const int64_t max_tile_pieces = nb * (ge.chunks > 1 ? 2 : 1);
-  if (max_tile_pieces <= kMedium || g->fuse_heavy) return DM_OK;
-  dm_timer_begin(g, "heavy_apply", &t);
-  hipLaunchKernelGGL(k_heavy_apply, dim3(grid_for(4 * g->heavy_cap, 1, 1024)), dim3(kQuarter), 0, g->stream, ge,
-                     make_apply(g), w.heavy_list, w.tile_count, g->tile_free, w.slabs, g->L, g->state,
-                     w.cnt, w.sh, g->fmask);
+  if (max_tile_pieces > kMedium && !g->fuse_heavy) {
+    dm_timer_begin(g, "heavy_apply", &t);
+    hipLaunchKernelGGL(k_heavy_apply, dim3(grid_for(4 * g->heavy_cap, 1, 1024)), dim3(kQuarter), 0, g->stream,
+                       ge, make_apply(g), w.heavy_list, w.tile_count, g->tile_free, w.slabs, g->L, g->state,
+                       w.cnt, w.sh);
+    dm_timer_end(g, &t);
+    DM_HIP(hipGetLastError());
+  }
+  // the touched tiles' fmask records (one wave per work item), while the
+  // frontier passes read them
+  if (!g->fmask_on) {
+    g->fmask_valid = false;
+    return DM_OK;
+  }
+  dm_timer_begin(g, "fmask", &t);
+  hipLaunchKernelGGL(k_fmask_items, dim3(grid_for(g->hitem_cap + g->act_cap, 4, 8192)), dim3(256), 0, g->stream,
+                     ge, w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS, w.cnt, g->state, g->fmask);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   return DM_OK;
@@ -1165,6 +1186,7 @@ int dm_launch_recount(dm_grid* g) {
   hipLaunchKernelGGL(k_recount, dim3((unsigned)g->NT), dim3(256), 0, g->stream, ge, g->state,
                      g->tile_free, g->fmask);
   DM_HIP(hipGetLastError());
+  g->fmask_valid = true;
   return DM_OK;
 }
 

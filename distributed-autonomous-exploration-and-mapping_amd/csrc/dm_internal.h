@@ -142,11 +142,13 @@ struct dm_grid {
     uint64_t gen = 0;                 // rb_gen at the pass's start
     uint64_t pass = 0;                // fr_pass / m_pass of the pass
     int64_t merge_n = 0;              // nranks * rec_cap of a merge
+    uint64_t wepoch = 0, mepoch = 0;  // passes / merges that wrote out_clu / m_out so far
   };
   static constexpr int kRbSlots = 2;   // ring slots of asynchronous passes
   static constexpr int kRbSync = 2;    // the slot of synchronous calls (dm_frontiers, dm_merge_bands)
   RbSlot rb[kRbSlots + 1];
   int rb_head = 0, rb_count = 0;      // oldest pending slot, pending passes
+  int cur_slot = 0;                   // the slot dm_select_slot selected
   uint64_t rb_gen = 0;                // bumped when device record buffers are reallocated
   // frontier / merge passes enqueued so far: an unsorted result (more
   // clusters than the sort kernel takes) lives in the shared raw arrays
@@ -159,12 +161,20 @@ struct dm_grid {
   float* L = nullptr;
   int8_t* state = nullptr;
   int32_t* tile_free = nullptr;
-  // [NT][2][64] per tile: free bit rows, then unknown bit rows (bit x of row
-  // y: the cell is free / unknown; out-of-grid cells are neither), kept in
-  // step with `state` by every kernel that writes it (k_tile_accum's apply,
-  // k_recount after bulk writes); the frontier pass reads these instead of
-  // the state bytes
-  uint64_t* fmask = nullptr;
+  // [NT][64 rows][16] per tile: byte j of row y holds the free bits of cells
+  // 4j..4j+3 (low nibble) and their unknown bits (high nibble); out-of-grid
+  // cells are neither.  Kept in step with `state` by every kernel that writes
+  // it (k_tile_accum's apply: each thread stores its 4 cells' byte;
+  // k_recount after bulk writes); the frontier pass reads these 1 KB per tile
+  // instead of the state bytes.  Maintained only while passes list many tiles
+  // (fmask_on: a pass listing >= kFmaskOnTiles switches it on, one listing
+  // fewer than kFmaskOnTiles / 4 off): a few thousand listed tiles (C3) are
+  // latency-bound either way and the per-call update would only add a
+  // kernel.  fmask_valid: the records match the state (a full rebuild,
+  // k_recount, precedes switching on otherwise).
+  uint8_t* fmask = nullptr;
+  bool fmask_on = false, fmask_valid = false;
+  int fmask_mode = 0;  // DM_FMASK=auto|on|off (read at dm_create; tests / A/B): 0 auto, 1 on, 2 off
   unsigned long long* cnt = nullptr;    // CNT_N device counters (frontier fields)
   unsigned long long* h_cnt = nullptr;  // pinned mirror: [CNT_N] frontier counters, [CNT_N] integrate counters
   unsigned long long* fsh = nullptr;    // [kShards][kShardWords] frontier shards
@@ -311,6 +321,18 @@ struct dm_grid {
   unsigned long long* m_cnt = nullptr;    // [4] device: K, flags, sorted, max band K
   unsigned long long* h_mcnt = nullptr;   // pinned mirror
 
+  // goal selection (dm_goals.hip): the last collected sorted result on the
+  // device (a readback slot's out_clu / m_out while that slot's epoch is
+  // unchanged), top-T workspaces, robot / index / centroid staging
+  int goal_slot = -1, goal_kind = 0;  // kind 1: band frontiers (out_clu), 2: merge (m_out)
+  uint64_t goal_epoch = 0, goal_gen = 0;
+  int64_t goal_n = 0;
+  unsigned long long* goal_k[2] = {nullptr, nullptr};
+  uint32_t* goal_i[2] = {nullptr, nullptr};
+  int64_t goal_cap = 0;
+  double* goal_io = nullptr;          // [4 * 256] robots xy, then centroids xy
+  int64_t* goal_idx = nullptr;        // [256]
+
   // profiling
   bool profile = false;
   std::vector<KernelTimer> pending;
@@ -321,6 +343,7 @@ struct dm_grid {
 // at readback slot `slot`.
 inline void dm_select_slot(dm_grid* g, int slot) {
   const dm_grid::RbSlot& r = g->rb[slot];
+  g->cur_slot = slot;
   g->out_clu = r.out_clu;
   g->h_out = r.h_out;
   g->h_out_dev = r.h_out_dev;
@@ -406,6 +429,8 @@ int dm_launch_rank_sort(hipStream_t stream, long long* clusters, const long long
                         int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
                         int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
                         int64_t host_cap, int64_t expect);
+// Listed tiles from which a frontier pass reads fmask instead of state bytes.
+constexpr int64_t kFmaskOnTiles = 8192;
 // Clusters above which the row-bucket sort replaces the O(K^2) rank sort.
 constexpr int64_t kBucketSortMin = 4096;
 constexpr int kBuckets = 4096;  // row buckets of the bucket sort (k_bs_scan: 4 per thread)
@@ -423,6 +448,11 @@ int64_t dm_export_nbytes(int64_t W, int64_t rec_cap);
 int dm_launch_export(dm_grid* g, void* d_export, int64_t rec_cap);
 int dm_launch_merge(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap,
                     int64_t min_size);
+// goal selection (dm_goals.hip)
+int dm_launch_goal_topk(dm_grid* g, const dm_cluster* d_recs, int64_t K, const double* d_robots, int32_t R,
+                        int32_t T, int64_t min_size, double w, double min_dist,
+                        const unsigned long long** d_k, const uint32_t** d_i);
+int dm_launch_goal_gather(dm_grid* g, const dm_cluster* d_recs, const int64_t* d_idx, int32_t R, double* d_xy);
 int dm_launch_ld06(dm_grid* g, int32_t S, const dm_ld06_point* d_pts, const int64_t* d_offsets,
                    int32_t N, int dir, float* d_ranges, float* d_intensities);
 

@@ -262,6 +262,7 @@ int dm_launch_export(dm_grid* g, void* d_export, int64_t rec_cap) {
 int dm_launch_merge(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap,
                     int64_t min_size) {
   ++g->m_pass;
+  ++g->rb[g->cur_slot].mepoch;  // this merge rewrites the selected slot's records
   MGeom m;
   m.v.W = g->W;
   m.v.rec_cap = rec_cap;

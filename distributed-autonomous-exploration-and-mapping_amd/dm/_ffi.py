@@ -161,6 +161,7 @@ SIGNATURES = {
     "dm_frontiers_end": [_vp, _vp, _i64, ctypes.POINTER(_i64)],
     "dm_set_overlap": [_vp, _i32],
     "dm_atomic_peak": [ctypes.c_int, _vp, _i32, ctypes.POINTER(_i32)],
+    "dm_assign_goals": [_vp, _vp, _i32, ctypes.c_int64, ctypes.c_double, ctypes.c_double, _vp, _vp],
 }
 # functions returning const char*
 STRING_FUNCS = ("dm_last_error", "dm_version")

@@ -232,6 +232,21 @@ class OccupancyMapper:
             check(self._lib.dm_map_image(self._handle(), _vp(out)))
         return out
 
+    def assign_goals(self, robots_xy, min_size: int = 8, distance_weight: float = 1.0,
+                     min_distance: float = 0.0):
+        """Frontier goals on the device (dm_assign_goals) over the clusters of
+        the last collected frontier result: per robot, in order, (index into
+        that result's cluster list, (x, y)) or None.  Same policy as
+        dm.goals.assign_goals (the host restatement the tests compare with)."""
+        xy = np.ascontiguousarray(np.asarray(robots_xy, np.float64).reshape(-1, 2))
+        R = xy.shape[0]
+        idx = np.empty(R, np.int64)
+        out = np.empty((R, 2), np.float64)
+        with self._lock:
+            check(self._lib.dm_assign_goals(self._handle(), _vp(xy), R, int(min_size), float(distance_weight),
+                                            float(min_distance), _vp(idx), _vp(out)))
+        return [(int(i), (float(p[0]), float(p[1]))) if i >= 0 else None for i, p in zip(idx, out)]
+
     # -- frontiers --------------------------------------------------------
     def frontiers(self, want_mask=False, want_labels=False, cap=None) -> Frontiers:
         """Frontier mask / labels (optional dense copies) and the cluster

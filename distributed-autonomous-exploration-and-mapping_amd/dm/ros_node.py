@@ -44,7 +44,6 @@ from dataclasses import dataclass, field, fields
 
 import numpy as np
 
-from .goals import select_goal
 from .grid import OccupancyMapper, default_params
 
 try:  # pragma: no cover - ROS is absent in CI and on the GPU box
@@ -340,14 +339,17 @@ class MappingNode:
                 for c in fr.clusters]
 
     def choose_goal(self):
-        """The frontier goal for the robot at its latest pose (dm.goals):
-        PoseStamped in the map frame facing the goal, or None."""
+        """The frontier goal for the robot at its latest pose, chosen on the
+        device over the last published frontier clusters (dm_assign_goals;
+        policy: dm.goals): PoseStamped in the map frame facing the goal, or
+        None."""
         if self.last_frontiers is None or self.latest_pose is None:
             return None
         x, y, _ = self.latest_pose
         s = self.slam
-        g = select_goal(self.last_frontiers, (x, y), min_size=s.dm_goal_min_size,
-                        distance_weight=s.dm_goal_distance_weight, min_distance=s.dm_goal_min_distance)
+        g = self.mapper.assign_goals([(x, y)], min_size=s.dm_goal_min_size,
+                                     distance_weight=s.dm_goal_distance_weight,
+                                     min_distance=s.dm_goal_min_distance)[0]
         if g is None:
             return None
         gx, gy = g[1]

@@ -281,6 +281,22 @@ int dm_profile_reset(dm_grid* g);
  * out: uint8[band_rows*width]. */
 int dm_map_image(dm_grid* g, uint8_t* out);
 
+/* Frontier goals for n_robots robots (replaces the
+ * reactive IR / LiDAR policy, server/thymio_project/thymio_project/main.py:
+ * 123-188, with map-based exploration).  Over the clusters of the last
+ * collected result (dm_frontiers, dm_frontiers_end or dm_merge_bands; on the
+ * device), robot r at robots_xy[2r], [2r+1] (metres) scores cluster c:
+ *   dist = sqrt(dx*dx + dy*dy), dx = cx_m - x, dy = cy_m - y
+ *   util = size / (1 + distance_weight * dist)   (double, no FMA)
+ * over clusters with size >= min_size and dist >= min_distance, best util
+ * first, ties to the smaller label; robots choose in order, each skipping the
+ * clusters earlier robots took.  out_index[r] = index into that result's
+ * label-sorted list (-1: none), out_xy[2r], [2r+1] = its centroid (NaN if
+ * none).  n_robots <= 256.  DM_ERR_INVALID_ARG if no result is on the device
+ * (none collected yet, or a later pass reused its readback slot). */
+int dm_assign_goals(dm_grid* g, const double* robots_xy, int32_t n_robots, int64_t min_size,
+                    double distance_weight, double min_distance, int64_t* out_index, double* out_xy);
+
 /* Measured uncontended atomic throughput of HIP device `device` (the
  * north star's "atomic throughput against MI355X peak": no vendor figure
  * exists for integer atomics, so the peak is measured in-harness,
