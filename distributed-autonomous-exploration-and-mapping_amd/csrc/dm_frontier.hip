@@ -481,6 +481,7 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
 // hand-off: it arrives later than every tile here, so it unites with them).
 constexpr int kFW = 4;            // tile-waves per workgroup
 constexpr int64_t kDenseRuns = 48;  // runs per frontier tile above which a pass is "dense"
+constexpr int64_t kDenseMaxTiles = 4096;  // ... if it has at most this many tiles with frontier cells
 #ifndef DM_FL_RUNS
 #define DM_FL_RUNS 512
 #endif
@@ -1567,8 +1568,12 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   // listed tiles without frontier cells at the rate of one 8-byte load per
   // lane and leaves tiles with more than kRunsFast runs to the 256-thread
   // kernel.
+  // Dense only while the tiles fit about two rounds of the 256-thread
+  // kernel's slots: with tens of thousands of tiles (a 1 cm map's rays) the
+  // wave kernel's 4x more tiles in flight win even where runs are many.
   const bool dense = g->frontier_kernel == 2 ||
-                     (g->frontier_kernel == 0 && g->ftf_hint > 0 && g->runs_hint > kDenseRuns * g->ftf_hint);
+                     (g->frontier_kernel == 0 && g->ftf_hint > 0 && g->runs_hint > kDenseRuns * g->ftf_hint &&
+                      g->ftf_hint <= kDenseMaxTiles);
   if (!dense) {
     dm_timer_begin(g, "frontier_tile", &t, ps);
     hipLaunchKernelGGL(k_frontier_tile, dim3(wave_grid), dim3(kFW * 64), 0, ps, fg, g->fbits,
@@ -1579,7 +1584,10 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
     DM_HIP(hipGetLastError());
   }
   dm_timer_begin(g, dense ? "frontier_tile" : "frontier_big", &t, ps);
-  hipLaunchKernelGGL(k_frontier_tile_big, dim3(dense ? grid_for(g->NT, 1, 8192) : grid_for(g->NT, 1, 512)),
+  // the leftover tiles of the wave kernel: the grid follows the last pass's
+  // count (the kernel grid-strides)
+  const int big_grid = grid_for(std::min<int64_t>(g->NT, g->big_hint + g->big_hint / 4 + 64), 1, 8192);
+  hipLaunchKernelGGL(k_frontier_tile_big, dim3(dense ? grid_for(g->NT, 1, 8192) : big_grid),
                      dim3(kFT), 0, ps, fg, g->fbits, dense ? nullptr : g->big_tiles, g->ftiles,
                      dense ? list_n : g->cnt + CNT_BIG, g->border, g->rel, (unsigned long long)g->fr_pass,
                      g->slot_label, g->slot_parent, g->slot_own,
@@ -1652,6 +1660,7 @@ int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied) {
   g->ftile_hint = (int64_t)g->h_cnt[CNT_FL0];
   g->runs_hint = (int64_t)hdr[CNT_N + 1];
   g->ftf_hint = (int64_t)hdr[CNT_N + 2];
+  g->big_hint = (int64_t)hdr[CNT_BIG];
   return DM_OK;
 }
 

@@ -306,6 +306,7 @@ struct dm_grid {
   int64_t sort_hint = 0, msort_hint = 0;  // clusters of the last band / merge readback
   int64_t ftile_hint = 0;                 // listed tiles of the last collected frontier pass
   int64_t runs_hint = 0, ftf_hint = 0;    // its runs and tiles with frontier cells
+  int64_t big_hint = 0;                   // its tiles left to k_frontier_tile_big by k_frontier_tile
   // tile kernel choice: 0 from those statistics, 1 always the wave-per-tile
   // kernel, 2 always the 256-thread kernel (DM_FRONTIER_KERNEL=auto|wave|wg,
   // read at dm_create, for A/B measurements; all three are exact)

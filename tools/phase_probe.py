@@ -21,10 +21,10 @@ import dm  # noqa: E402
 from dm import synth  # noqa: E402
 
 NAMES = {
-    "frontier": {0: "load+bitrows", 1: "F+run scan", 2: "enum runs", 3: "unions", 4: "compress",
+    "frontier": {0: "tile index + bit rows", 1: "F+run scan", 2: "enum runs", 3: "unions", 4: "compress",
                  5: "roots", 6: "sums+slot atomic", 7: "slot writes + edge unions + band rows", 8: "empty tile exit",
                  16: "#tiles", 17: "#runs", 18: "#tiles with F"},
-    "ftile": {9: "tile index load", 0: "loads + frontier bits", 1: "run scan + LDS init", 2: "row unions",
+    "ftile": {9: "tile index load", 0: "bit rows", 1: "run scan + LDS init", 2: "row unions",
               3: "compress + root ranks", 4: "sums", 5: "slot atomic + slot writes", 6: "border publish + drain",
               7: "pair arrivals", 8: "edge unions", 10: "dense / band-edge writes",
               16: "#tiles", 17: "#tiles with F", 18: "#runs"},
@@ -36,7 +36,10 @@ NAMES = {
 
 
 def main():
+    # default: C3; "c5 N": 65536^2 @ 1 cm, 64 robots x N beams
     G, res, S, N, steps = 16384, 0.05, 64, 4096, 10
+    if len(sys.argv) > 1 and sys.argv[1] == "c5":
+        G, res, N = 65536, 0.01, int(sys.argv[2]) if len(sys.argv) > 2 else 192
     half = G * res / 2
     world = synth.make_world(0, -half, -half, half, half)
     st = synth.ScanStream(world, S, N, 500, region=(-half + 1, -half + 1, half - 1, half - 1))
