@@ -1587,7 +1587,12 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   // the leftover tiles of the wave kernel: the grid follows the last pass's
   // count (the kernel grid-strides)
   const int big_grid = grid_for(std::min<int64_t>(g->NT, g->big_hint + g->big_hint / 4 + 64), 1, 8192);
-  hipLaunchKernelGGL(k_frontier_tile_big, dim3(dense ? grid_for(g->NT, 1, 8192) : big_grid),
+  // dense: one workgroup per listed tile of the last collected pass (+25 %;
+  // the kernel grid-strides): thousands of empty workgroups would only keep
+  // the dispatcher from the other streams' kernels
+  const int dense_grid = grid_for(std::min<int64_t>(g->NT, g->ftile_hint > 0 ? g->ftile_hint + g->ftile_hint / 4 + 64
+                                                                            : g->NT), 1, 8192);
+  hipLaunchKernelGGL(k_frontier_tile_big, dim3(dense ? dense_grid : big_grid),
                      dim3(kFT), 0, ps, fg, g->fbits, dense ? nullptr : g->big_tiles, g->ftiles,
                      dense ? list_n : g->cnt + CNT_BIG, g->border, g->rel, (unsigned long long)g->fr_pass,
                      g->slot_label, g->slot_parent, g->slot_own,

@@ -19,6 +19,11 @@ LINES = {
     "r01_c2_replay_bench.json": "C2",
     "r01_c4_1gpu_bench.json": "C4",
     "r01_c5_sweep_bench.json": "C5",
+    "r02_bench.json": "C3",
+    "r02_c1_bench.json": "C1",
+    "r02_c2_bench.json": "C2",
+    "r02_c4_bench.json": "C4",
+    "r02_c5_bench.json": "C5",
 }
 
 
@@ -54,6 +59,23 @@ def test_headline_line_has_traffic_and_cpu_baseline():
     assert d["cpu_baseline"] and d["cpu_baseline"]["value"] > 0
     # the north-star targets (BASELINE.json): >= 1e10 updates/s, < 2 ms frontiers
     assert d["value"] >= 1e10 and d["frontier_ms"] < 2.0
+
+
+def test_r02_headline_fields():
+    """Round 2's C3 line: the frontier and atomic rooflines, the explored-map
+    frontier pass, the host-input rate and the step cadence record."""
+    d = _load("r02_bench.json")
+    r = d["roofline"]
+    assert r["traffic"] and r["traffic"] > 0
+    fr = r["frontier"]
+    assert fr["bound"] == "hbm" and abs(fr["frac"] - fr["achieved"] / fr["peak"]) < 1e-9
+    at = r["atomics"]
+    assert at["peak"] > 0 and 0 < at["frac"] <= 1.5
+    assert d["frontier_ms_explored"] and d["frontier_ms_explored"] < 2.0
+    assert d["value_host_inputs"] and d["value_host_inputs"] >= 1e10
+    c = d["step_wall_us"]
+    assert c["n"] == d["steps"] and c["p50"] <= c["p90"] <= c["max"]
+    assert d["value"] >= 1e10 and d["frontier_ms"] < 2.0 and d["cpu_baseline"]["value"] > 0
 
 
 def test_bench_parser_knows_every_config():
