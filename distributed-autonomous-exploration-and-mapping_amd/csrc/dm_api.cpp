@@ -337,8 +337,13 @@ int read_counters(dm_grid* g) {
                         hipMemcpyDeviceToHost, g->stream));
   DM_HIP(hipMemcpyAsync(g->h_cnt + CNT_N, g->iw[g->iw_cur].cnt, sizeof(unsigned long long) * CNT_N,
                         hipMemcpyDeviceToHost, g->stream));
+  DM_HIP(hipMemcpyAsync(g->h_cnt + 2 * CNT_N, g->fe_flag + kHaltWord, sizeof(unsigned long long),
+                        hipMemcpyDeviceToHost, g->stream));
   DM_HIP(dm_copy_shards(g));
   DM_HIP(hipStreamSynchronize(g->stream));
+  if (g->h_cnt[2 * CNT_N])
+    return dm_set_error(DM_ERR_PIPELINE, "the overlapped pipeline's front-end hand-off timed out: a map "
+                        "update was skipped; dm_reset the handle");
   return DM_OK;
 }
 
@@ -350,7 +355,7 @@ int finish_counts(dm_grid* g, uint64_t* U, uint64_t* T) {
     // cannot happen with the bounds in grow_integrate; keep the map consistent anyway
     (void)hipMemset(g->iw[g->iw_cur].tile_count, 0, sizeof(int32_t) * (size_t)g->NT);
     return dm_set_error(DM_ERR_CAPACITY, "integrate workspace overflow (flags %llu: 1 first-touch "
-                        "list, 2 pieces, 4 work lists, 8 front-end hand-off timed out)",
+                        "list, 2 pieces, 4 work lists)",
                         (unsigned long long)ic[CNT_IOVERFLOW]);
   }
   if (U) *U = dm_shard_sum(g->h_sh, SH_U);
@@ -467,6 +472,9 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     const char* sep = getenv("DM_HEAVY_SEPARATE");
     g->fuse_heavy = !(sep && sep[0] == '1');
     g->fe_gate = !dm_env_off("DM_FE_GATE");
+    g->pass_gate = !dm_env_off("DM_PASS_GATE");
+    const char* fg = getenv("DM_FAULT_GATE");
+    g->fault_gate = fg && fg[0] == '1';
     const char* fm = getenv("DM_FMASK");
     g->fmask_mode = fm && !strcmp(fm, "on") ? 1 : (fm && !strcmp(fm, "off") ? 2 : 0);
     const char* fk = getenv("DM_FRONTIER_KERNEL");
@@ -500,7 +508,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   for (int sl = 0; sl <= dm_grid::kRbSlots; ++sl)
     if ((rc = grow_host_out(g, sl, 1 << 14))) return fail(rc);
   dm_select_slot(g, 0);
-  e = hipHostMalloc((void**)&g->h_cnt, sizeof(unsigned long long) * 2 * CNT_N, hipHostMallocDefault);
+  e = hipHostMalloc((void**)&g->h_cnt, sizeof(unsigned long long) * (2 * CNT_N + 1), hipHostMallocDefault);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipHostMalloc(counters)"));
   e = hipHostMalloc((void**)&g->h_sh, sizeof(unsigned long long) * 2 * kShards * kShardWords,
                     hipHostMallocDefault);
@@ -530,7 +538,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   // scope fence (no host-visible cache writeback at every step).  The host
   // waits on a readback slot's event and then reads mapped host memory:
   // default fences.
-  for (hipEvent_t* ev : {&g->ev_fe, &g->iw[0].ev_free, &g->iw[1].ev_free}) {
+  for (hipEvent_t* ev : {&g->ev_fe, &g->ev_bits, &g->iw[0].ev_free, &g->iw[1].ev_free}) {
     e = hipEventCreateWithFlags(ev, hipEventDisableTiming | hipEventDisableSystemFence);
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
   }
@@ -552,7 +560,7 @@ int dm_destroy(dm_grid* g) {
   (void)hipSetDevice(g->device);
   (void)dm_sync_all(g);
   for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
-  for (hipEvent_t ev : {g->ev_fe, g->iw[0].ev_free, g->iw[1].ev_free})
+  for (hipEvent_t ev : {g->ev_fe, g->ev_bits, g->iw[0].ev_free, g->iw[1].ev_free})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& r : g->rb) {
     if (r.ev) (void)hipEventDestroy(r.ev);
@@ -608,6 +616,7 @@ int dm_reset(dm_grid* g) {
   DM_HIP(hipMemsetAsync(g->tile_free, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
   if ((rc = dm_launch_recount(g))) return rc;  // fmask: every in-grid cell unknown
   for (auto& f : g->fw) DM_HIP(hipMemsetAsync(f.cnt, 0, sizeof(unsigned long long) * CNT_N, g->stream));
+  DM_HIP(hipMemsetAsync(g->fe_flag + kHaltWord, 0, sizeof(unsigned long long), g->stream));  // sticky error
   DM_HIP(hipStreamSynchronize(g->stream));
   return DM_OK;
 }

@@ -68,11 +68,14 @@ __global__ __launch_bounds__(256) void k_frontier_prep(int64_t NT, const int32_t
                                                        unsigned long long* other_n, int64_t n_edge,
                                                        unsigned long long* cnt, unsigned long long* fsh,
                                                        int32_t* __restrict__ edge_slot,
-                                                       int32_t* __restrict__ slot_parent, int64_t slot_cap) {
+                                                       int32_t* __restrict__ slot_parent, int64_t slot_cap,
+                                                       const unsigned long long* __restrict__ halt) {
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int lane = __lane_id();
-  if (i0 < 3) cnt[CNT_SLOTS + i0] = 0ull;  // slots, clusters, overflow
+  // slots, clusters, overflow (kOvPipeline while the handle's sticky
+  // hand-off error is set: the map misses a batch, DM_ERR_PIPELINE)
+  if (i0 < 3) cnt[CNT_SLOTS + i0] = (i0 == 2 && *halt) ? kOvPipeline : 0ull;
   if (i0 == 3) cnt[CNT_BIG] = 0ull;
   if (i0 == 0) *other_n = 0ull;
   if (i0 < kShards * kShardWords) fsh[i0] = 0ull;
@@ -1523,7 +1526,7 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   dm_timer_begin(g, "frontier_prep", &t);
   hipLaunchKernelGGL(k_frontier_prep, dim3(grid_for(std::max<int64_t>(std::max<int64_t>(g->NT, 2 * g->W), kShards * kShardWords), 256, 1024)), dim3(256), 0,
                      g->stream, g->NT, g->tile_free, g->ftiles, list_n, zero_n, 2 * g->W, g->cnt, g->fsh,
-                     g->edge_slot, g->slot_parent, g->slot_cap);
+                     g->edge_slot, g->slot_parent, g->slot_cap, g->fe_flag + kHaltWord);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));
@@ -1554,9 +1557,14 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   hipStream_t ps = g->stream;
   if (split) {
     ps = g->pass_stream;
-    const unsigned long long seq = ++g->bits_seq;
-    if (int rc = dm_launch_signal(g->stream, g->bits_flag, seq)) return rc;
-    if (int rc = dm_launch_gate(ps, g->bits_flag, seq, g->cnt + CNT_OVERFLOW, kOvGate)) return rc;
+    if (g->pass_gate) {
+      const unsigned long long seq = ++g->bits_seq;
+      if (int rc = dm_launch_signal(g->stream, g->bits_flag, seq)) return rc;
+      if (int rc = dm_launch_gate(ps, g->bits_flag, seq, g->cnt + CNT_OVERFLOW, kOvGate)) return rc;
+    } else {
+      DM_HIP(hipEventRecord(g->ev_bits, g->stream));
+      DM_HIP(hipStreamWaitEvent(ps, g->ev_bits, 0));
+    }
   }
   if (end_stream) *end_stream = ps;
   // Tile kernel, chosen from the last collected pass (both are exact for any
@@ -1649,6 +1657,9 @@ int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied) {
   memcpy(g->h_cnt, hdr, sizeof(unsigned long long) * CNT_N);
   *copied = std::min<int64_t>(g->h_out_cap, g->slot_cap);
   const unsigned long long most = hdr[CNT_N];
+  if (g->h_cnt[CNT_OVERFLOW] & kOvPipeline)
+    return dm_set_error(DM_ERR_PIPELINE, "the overlapped pipeline's front-end hand-off timed out: a map "
+                                         "update was skipped; dm_reset the handle");
   if ((int64_t)most > g->slot_cap / kShards || (g->h_cnt[CNT_OVERFLOW] & kOvSlots)) {
     *n_clusters = (int64_t)most * kShards;  // slot capacity that fits the fullest shard
     return DM_ERR_CAPACITY;

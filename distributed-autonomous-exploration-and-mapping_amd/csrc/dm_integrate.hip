@@ -670,7 +670,10 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     int cnt_b, const PackedPiece* __restrict__ pieces, int32_t* tile_count, int32_t* tile_free,
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
     const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok,
-    const int32_t* __restrict__ heavy_list, int32_t* heavy_done) {
+    const int32_t* __restrict__ heavy_list, int32_t* heavy_done, const unsigned long long* __restrict__ halt) {
+  // a timed-out front-end hand-off (kHaltWord): this call's workspace was
+  // never written, so nothing is applied (the host reports DM_ERR_PIPELINE)
+  if (*halt) return;
   __shared__ uint32_t tl[kTileWords + 64];  // + one spare word per lane (walk_piece_plain)
   __shared__ int32_t s_T, s_free, s_last;
   __shared__ uint32_t s_U;
@@ -855,7 +858,9 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
 __global__ __launch_bounds__(kQuarter) void k_heavy_apply(
     Geom g, ApplyArgs p, const int32_t* __restrict__ heavy_list, int32_t* tile_count, int32_t* tile_free,
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
-    const unsigned long long* __restrict__ cnt, unsigned long long* ish) {
+    const unsigned long long* __restrict__ cnt, unsigned long long* ish,
+    const unsigned long long* __restrict__ halt) {
+  if (*halt) return;  // as k_tile_accum
   __shared__ int32_t s_T, s_free;
   __shared__ uint32_t s_U;
   const int tid = threadIdx.x;
@@ -900,7 +905,10 @@ __global__ __launch_bounds__(256) void k_integrate_reset(unsigned long long* cnt
 // (bits_flag).  No deadlock: the gate holds one workgroup slot, and all the
 // producer waits for is ahead of the gate on the consuming stream.  Bounded:
 // after kGateTicks of the 100 MHz wall clock the gate sets err_bit in *err
-// (the consumer's result is then reported as an error) and exits.
+// (the consumer's result is then reported as an error) and exits.  Under a
+// tool that runs one dispatch at a time across all queues (rocprofv3 --pmc)
+// a gate can be dispatched before the kernels it waits for and then times
+// out: PMC passes run the steps without overlap (tools/pmc_passes.sh).
 constexpr unsigned long long kGateTicks = 500000000ull;  // 5 s
 
 __global__ __launch_bounds__(64) void k_seq_signal(unsigned long long* flag, unsigned long long seq) {
@@ -908,12 +916,13 @@ __global__ __launch_bounds__(64) void k_seq_signal(unsigned long long* flag, uns
 }
 
 __global__ __launch_bounds__(64) void k_seq_gate(const unsigned long long* flag, unsigned long long seq,
-                                                 unsigned long long* err, unsigned long long err_bit) {
+                                                 unsigned long long* err, unsigned long long err_bit,
+                                                 unsigned long long ticks) {
   if (threadIdx.x != 0) return;
   const unsigned long long t0 = wall_clock64();
   while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < seq) {
     __builtin_amdgcn_s_sleep(2);
-    if (wall_clock64() - t0 > kGateTicks) {
+    if (wall_clock64() - t0 > ticks) {
       atomicOr(err, err_bit);
       return;
     }
@@ -963,7 +972,9 @@ __global__ __launch_bounds__(256) void k_recount(Geom g, const int8_t* __restric
 __global__ __launch_bounds__(256) void k_fmask_items(Geom g, const int4* __restrict__ list_a, int cnt_a,
                                                      const int4* __restrict__ list_b, int cnt_b,
                                                      const unsigned long long* __restrict__ cnt,
-                                                     const int8_t* __restrict__ state, uint8_t* __restrict__ fmask) {
+                                                     const int8_t* __restrict__ state, uint8_t* __restrict__ fmask,
+                                                     const unsigned long long* __restrict__ halt) {
+  if (*halt) return;  // as k_tile_accum
   const int64_t HI = min((int64_t)cnt[cnt_a], g.hitem_cap);
   const int64_t LI = min((int64_t)cnt[cnt_b], (int64_t)g.act_cap);
   const int lane = __lane_id();
@@ -1127,7 +1138,11 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   } else if (g->overlap) {
     const unsigned long long seq = ++g->fe_seq;
     if (int rc = dm_launch_signal(fs, g->fe_flag, seq)) return rc;
-    if (int rc = dm_launch_gate(g->stream, g->fe_flag, seq, w.cnt + CNT_IOVERFLOW, 8ull)) return rc;
+    // a timeout sets the sticky halt word (not this call's counters: the
+    // front-end's own reset, still queued, would clear them)
+    if (int rc = dm_launch_gate(g->stream, g->fe_flag, g->fault_gate ? seq + (1ull << 40) : seq,
+                                g->fe_flag + kHaltWord, 1ull, g->fault_gate ? 1000ull : 0ull))
+      return rc;
   }
   const int vec_ok = (g->W % 4 == 0) ? 1 : 0;
   // heavy chunks and medium tiles first (the long items), then the light
@@ -1137,7 +1152,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                      dim3(kQuarter), 0,
                      g->stream, ge, make_apply(g), w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS,
                      w.pieces, w.tile_count, g->tile_free, w.slabs, g->L, g->state, w.cnt, w.sh, vec_ok,
-                     w.heavy_list, g->fuse_heavy ? w.heavy_done : nullptr);
+                     w.heavy_list, g->fuse_heavy ? w.heavy_done : nullptr, g->fe_flag + kHaltWord);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (g->overlap) w.free_owed = true;
@@ -1150,7 +1165,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
     dm_timer_begin(g, "heavy_apply", &t);
     hipLaunchKernelGGL(k_heavy_apply, dim3(grid_for(4 * g->heavy_cap, 1, 1024)), dim3(kQuarter), 0, g->stream,
                        ge, make_apply(g), w.heavy_list, w.tile_count, g->tile_free, w.slabs, g->L, g->state,
-                       w.cnt, w.sh);
+                       w.cnt, w.sh, g->fe_flag + kHaltWord);
     dm_timer_end(g, &t);
     DM_HIP(hipGetLastError());
   }
@@ -1162,7 +1177,8 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   }
   dm_timer_begin(g, "fmask", &t);
   hipLaunchKernelGGL(k_fmask_items, dim3(grid_for(g->hitem_cap + g->act_cap, 4, 8192)), dim3(256), 0, g->stream,
-                     ge, w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS, w.cnt, g->state, g->fmask);
+                     ge, w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS, w.cnt, g->state, g->fmask,
+                     g->fe_flag + kHaltWord);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   return DM_OK;
@@ -1175,8 +1191,8 @@ int dm_launch_signal(hipStream_t s, unsigned long long* flag, unsigned long long
 }
 
 int dm_launch_gate(hipStream_t s, const unsigned long long* flag, unsigned long long seq,
-                   unsigned long long* err, unsigned long long err_bit) {
-  hipLaunchKernelGGL(k_seq_gate, dim3(1), dim3(64), 0, s, flag, seq, err, err_bit);
+                   unsigned long long* err, unsigned long long err_bit, unsigned long long ticks) {
+  hipLaunchKernelGGL(k_seq_gate, dim3(1), dim3(64), 0, s, flag, seq, err, err_bit, ticks ? ticks : kGateTicks);
   DM_HIP(hipGetLastError());
   return DM_OK;
 }

@@ -48,6 +48,13 @@ enum {
 constexpr unsigned long long kOvSlots = 4ull;      // a slot shard region overflowed
 constexpr unsigned long long kOvUnionFind = 8ull;  // a union-find loop hit its bound (dm_uf.h)
 constexpr unsigned long long kOvGate = 16ull;      // the pass stream's hand-off gate timed out
+constexpr unsigned long long kOvPipeline = 32ull;  // the handle's sticky hand-off error was set (kHaltWord)
+// fe_flag[kHaltWord]: sticky error word of the overlapped pipeline.  The
+// integrate front-end -> map update gate sets bit 1 when it times out; from
+// then on k_tile_accum and k_fmask_items return at once (the workspace they
+// would read was not written), k_frontier_prep flags every pass kOvPipeline,
+// and the host reports DM_ERR_PIPELINE until dm_reset clears it.
+constexpr int kHaltWord = 8;
 // Integrate counters, zeroed by each integrate call; the others belong to the
 // frontier pass, which may still be running when the next call's front-end
 // starts (dm_set_overlap), so the integrate reset never touches them.
@@ -120,9 +127,14 @@ struct dm_grid {
   hipEvent_t ev_fe = nullptr;
   // front-end completion word (k_fe_signal / k_fe_gate, dm_integrate.hip):
   // the sequence number of the last call whose front-end finished
-  unsigned long long* fe_flag = nullptr;
+  unsigned long long* fe_flag = nullptr;  // [0] sequence, [kHaltWord] sticky hand-off error
   unsigned long long fe_seq = 0;
+  // DM_FAULT_GATE=1 (read at dm_create; fault-injection tests only): the
+  // front-end gate waits for a sequence number that never comes, ~10 us
+  bool fault_gate = false;
   bool fe_gate = true;  // DM_FE_GATE=0: cross-stream event wait instead (A/B)
+  bool pass_gate = true;  // DM_PASS_GATE=0: the bit rows' hand-off by an event wait (ev_bits) instead
+  hipEvent_t ev_bits = nullptr;
   uint64_t integrate_seq = 0;  // map changes so far
   // Asynchronous passes (dm_frontiers_begin / dm_merge_bands_begin) use a
   // ring of kRbSlots readback slots, so a pass can be started before the
@@ -413,10 +425,10 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
                          hipStream_t* end_stream = nullptr);
 // Sequence hand-off between streams (dm_integrate.hip): k_seq_signal stores
 // seq into *flag; k_seq_gate (one lane) waits until *flag >= seq, or sets
-// err_bit in *err after a bounded time.
+// err_bit in *err after a bounded time (ticks of the 100 MHz clock, 0: 5 s).
 int dm_launch_signal(hipStream_t s, unsigned long long* flag, unsigned long long seq);
 int dm_launch_gate(hipStream_t s, const unsigned long long* flag, unsigned long long seq,
-                   unsigned long long* err, unsigned long long err_bit);
+                   unsigned long long* err, unsigned long long err_bit, unsigned long long ticks = 0);
 int dm_launch_edge_labels(dm_grid* g);
 int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied);
 int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters,

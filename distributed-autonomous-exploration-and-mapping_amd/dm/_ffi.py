@@ -23,6 +23,7 @@ DM_ERR_CAPACITY = -5
 DM_ERR_IO = -6
 DM_ERR_STATE = -7
 DM_ERR_INCOMPLETE = -8
+DM_ERR_PIPELINE = -9
 DM_TILE = 64
 
 _ERR_NAMES = {
@@ -34,6 +35,7 @@ _ERR_NAMES = {
     DM_ERR_IO: "DM_ERR_IO",
     DM_ERR_STATE: "DM_ERR_STATE",
     DM_ERR_INCOMPLETE: "DM_ERR_INCOMPLETE",
+    DM_ERR_PIPELINE: "DM_ERR_PIPELINE",
 }
 
 

@@ -48,6 +48,9 @@ extern "C" {
 #define DM_ERR_STATE (-7)
 #define DM_ERR_INCOMPLETE (-8) /* a pass has no result: an export record was incomplete, or a
                                   union-find loop hit its iteration bound */
+#define DM_ERR_PIPELINE (-9)   /* a cross-stream hand-off of the overlapped pipeline (dm_set_overlap)
+                                  timed out: the map update it guarded was skipped, so the map
+                                  misses batches; sticky until dm_reset */
 
 /* Tile edge (cells) used by the kernels; band_row0 must be a multiple of it. */
 #define DM_TILE 64
@@ -191,7 +194,11 @@ int dm_frontiers_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out);
  * stream; the map update itself stays in the handle's stream order, after
  * every earlier call.  Results are identical with overlap on or off.  With
  * overlap on, the device inputs of dm_integrate_device must be complete when
- * the call is made (e.g. produced by work the host already synchronised). */
+ * the call is made (e.g. produced by work the host already synchronised).
+ * The streams hand off through bounded device-side waits (5 s); one that
+ * times out (a tool that runs one dispatch at a time, e.g. rocprofv3 --pmc,
+ * can cause it) skips the map update it guarded and every later call that
+ * reads results returns DM_ERR_PIPELINE until dm_reset. */
 int dm_set_overlap(dm_grid* g, int32_t on);
 
 /* Sharding support (row bands).  Halo rows are the global

@@ -209,3 +209,44 @@ def test_async_host_inputs_pipelined(oracle_lib, overlap):
         assert_map_equal(m, om)
         om2 = oracle_lib.OracleMap(p)
         assert m.last_counts() == om2.integrate(*batches[-1], amin, inc)  # U, T of the last call
+
+
+def test_front_end_gate_timeout_is_a_sticky_error(oracle_lib, monkeypatch):
+    """A timed-out front-end hand-off (fault injection: DM_FAULT_GATE=1 makes
+    the gate wait for a sequence number that never comes, ~10 us) must not
+    apply the previous workspace's items: the map stays unchanged, every
+    result-reading call reports DM_ERR_PIPELINE, and dm_reset clears it."""
+    from dm import _ffi
+
+    p, batches, amin, inc = cases.world_case(49, 600, 500, 0.05, 4, 720, 2, region_frac=0.7)
+    dev = _device_batches(batches)
+    monkeypatch.setenv("DM_FAULT_GATE", "1")
+    with dm.OccupancyMapper(p) as m:
+        monkeypatch.delenv("DM_FAULT_GATE")
+        # a first call without overlap fills workspace set 0; the faulted
+        # calls then find stale items in both sets
+        pose4, rng = dev[0]
+        m.integrate_device(pose4.data_ptr(), pose4.shape[0], rng.data_ptr(), 720, amin, inc)
+        m.synchronize()
+        before = m.state().copy()
+        m.set_overlap(True)
+        for pose4, rng in dev:
+            m.integrate_device(pose4.data_ptr(), pose4.shape[0], rng.data_ptr(), 720, amin, inc)
+        m.frontiers_begin()
+        with pytest.raises(_ffi.DmError) as e:
+            m.frontiers_end()
+        assert e.value.code == _ffi.DM_ERR_PIPELINE
+        with pytest.raises(_ffi.DmError) as e:
+            m.frontiers()
+        assert e.value.code == _ffi.DM_ERR_PIPELINE
+        with pytest.raises(_ffi.DmError) as e:
+            m.last_stats()
+        assert e.value.code == _ffi.DM_ERR_PIPELINE
+        np.testing.assert_array_equal(m.state(), before)  # no stale re-application
+        m.set_overlap(False)
+        m.reset()
+        om, expect = _oracle_steps(oracle_lib, p, batches, amin, inc)
+        for pose4, rng in dev:  # no gate without overlap: the handle works again
+            m.integrate_device(pose4.data_ptr(), pose4.shape[0], rng.data_ptr(), 720, amin, inc)
+        np.testing.assert_array_equal(m.frontiers().clusters, expect[-1])
+        assert_map_equal(m, om)

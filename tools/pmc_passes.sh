@@ -3,7 +3,10 @@
 # rocprofv3 does not split counters over passes, MI355X_MICROARCH.md §PMC).
 # Usage (on the GPU box, from the repo root):
 #   bash tools/pmc_passes.sh OUTDIR [command...]
-# default command: a short C3 bench run.  Summarise with
+# default command: a short C3 bench run, steps back to back (--no-overlap):
+# rocprofv3 --pmc runs one dispatch at a time, and the overlapped pipeline's
+# cross-stream gates would wait for kernels queued behind them (DM_ERR_PIPELINE).
+# Summarise with
 #   python tools/pmc_summary.py OUTDIR profiles/pmc_latest.json WORKLOAD
 set -o pipefail
 R=$PWD
@@ -11,7 +14,7 @@ OUT=${1:-gpurun_out/pmc}
 shift
 CMD=("$@")
 [ ${#CMD[@]} -eq 0 ] && CMD=(python3 $R/bench.py --steps 5 --warmup 2 --cpu-seconds 0 --profile-steps 0 --pool 3 \
-                             --no-explored --no-host-inputs)
+                             --no-explored --no-host-inputs --no-overlap)
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 i=0
