@@ -237,6 +237,8 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    batching = {k: band.last_stats()[k] for k in ("graph_launches", "direct_launches", "graph_hits",
+                                                  "graph_misses")}
     cdev = dev if args.backend == "nccl" else torch.device("cpu")
     if world_size > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
@@ -418,6 +420,8 @@ def main():
             # host-side start-to-start time of each timed step (rank 0): a
             # host stall shows here as a long tail, kernel time in `roofline`
             "step_wall_us": _cadence(marks),
+            # libdm's launch batching (dm_batch.h) over the whole run so far
+            "launch_batching": batching,
         }
         print(json.dumps(result), flush=True)
     mapper.close()

@@ -473,6 +473,10 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     g->fuse_heavy = !(sep && sep[0] == '1');
     g->fe_gate = !dm_env_off("DM_FE_GATE");
     g->pass_gate = !dm_env_off("DM_PASS_GATE");
+    // launch batching into graphs (dm_batch.h) only with DM_GRAPHS=1: measured
+    // neutral to slightly slower at C3
+    const char* gr = getenv("DM_GRAPHS");
+    g->batch.enabled = gr && gr[0] == '1';
     const char* fg = getenv("DM_FAULT_GATE");
     g->fault_gate = fg && fg[0] == '1';
     const char* fm = getenv("DM_FMASK");
@@ -522,17 +526,24 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   // chain (accumulation, frontier pass) high, the integrate front-end low,
   // so a front-end enqueued early fills what the map chain leaves idle
   // instead of competing with the accumulation for its CUs.
+  // DM_STREAM_PRIO=XYZ (A/B): priorities of the map stream, the front-end
+  // stream and the pass stream, 'h' or 'l' each (default "hlh").
   int prio_lo = 0, prio_hi = 0;
+  int p_grid = 0, p_fe = 0, p_pass = 0;
   {
     const char* sp = getenv("DM_STREAM_PRIO");
     if (!(sp && sp[0] == '0')) (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    const char* pr = sp && strlen(sp) == 3 ? sp : "hlh";
+    p_grid = pr[0] == 'h' ? prio_hi : prio_lo;
+    p_fe = pr[1] == 'h' ? prio_hi : prio_lo;
+    p_pass = pr[2] == 'h' ? prio_hi : prio_lo;
   }
-  e = hipStreamCreateWithPriority(&g->stream, hipStreamNonBlocking, prio_hi);
+  e = hipStreamCreateWithPriority(&g->stream, hipStreamNonBlocking, p_grid);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate"));
   g->own_stream = true;
-  e = hipStreamCreateWithPriority(&g->fe_stream, hipStreamNonBlocking, prio_lo);
+  e = hipStreamCreateWithPriority(&g->fe_stream, hipStreamNonBlocking, p_fe);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(front-end)"));
-  e = hipStreamCreateWithPriority(&g->pass_stream, hipStreamNonBlocking, prio_hi);
+  e = hipStreamCreateWithPriority(&g->pass_stream, hipStreamNonBlocking, p_pass);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(pass)"));
   // ev_fe / ev_free only order the two streams on the device: no system-
   // scope fence (no host-visible cache writeback at every step).  The host
@@ -559,6 +570,7 @@ int dm_destroy(dm_grid* g) {
   if (!g) return DM_OK;
   (void)hipSetDevice(g->device);
   (void)dm_sync_all(g);
+  dm_batch_release(&g->batch);
   for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
   for (hipEvent_t ev : {g->ev_fe, g->ev_bits, g->iw[0].ev_free, g->iw[1].ev_free})
     if (ev) (void)hipEventDestroy(ev);
@@ -744,13 +756,15 @@ int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out) {
   const unsigned long long* fs = g->h_sh + kShards * kShardWords;
   const unsigned long long* ic = g->h_cnt + CNT_N;  // the last integrate call's counters
   const uint64_t items = ic[CNT_ITEMS] + ic[CNT_LITEMS];  // heavy + light work items
-  const uint64_t v[10] = {dm_shard_sum(g->h_sh, SH_U),  dm_shard_sum(g->h_sh, SH_T),
+  const uint64_t v[14] = {dm_shard_sum(g->h_sh, SH_U),  dm_shard_sum(g->h_sh, SH_T),
                           dm_shard_sum(g->h_sh, SH_TH), ic[CNT_SEGS],
                           ic[CNT_ACTIVE],               items,
                           ic[CNT_HEAVY],                g->h_cnt[CNT_FL0],
-                          dm_shard_sum(fs, SH_SLOT),    g->h_cnt[CNT_CLUSTERS]};
-  for (int32_t i = 0; i < cap && i < 10; ++i) out[i] = v[i];
-  if (n_out) *n_out = 10;
+                          dm_shard_sum(fs, SH_SLOT),    g->h_cnt[CNT_CLUSTERS],
+                          g->batch.graph_launches,      g->batch.direct_launches,
+                          g->batch.hits,                g->batch.misses};
+  for (int32_t i = 0; i < cap && i < 14; ++i) out[i] = v[i];
+  if (n_out) *n_out = 14;
   return DM_OK;
 }
 

@@ -47,6 +47,7 @@ constexpr int kMaxRoots = 1024;       // 8-connected components in a 64x64 tile
 struct FGeom {
   int32_t W, R, row0, TX, TY;
   int32_t has_before, has_after;
+  int32_t pad_ = 0;  // no implicit padding: equal geometries are equal bytes (dm_batch.h cache keys)
   int64_t NT;
   int32_t want_mask, want_labels;
   int64_t H;
@@ -69,7 +70,8 @@ __global__ __launch_bounds__(256) void k_frontier_prep(int64_t NT, const int32_t
                                                        unsigned long long* cnt, unsigned long long* fsh,
                                                        int32_t* __restrict__ edge_slot,
                                                        int32_t* __restrict__ slot_parent, int64_t slot_cap,
-                                                       const unsigned long long* __restrict__ halt) {
+                                                       const unsigned long long* __restrict__ halt,
+                                                       unsigned long long* stamp_word) {
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int lane = __lane_id();
@@ -77,6 +79,11 @@ __global__ __launch_bounds__(256) void k_frontier_prep(int64_t NT, const int32_t
   // hand-off error is set: the map misses a batch, DM_ERR_PIPELINE)
   if (i0 < 3) cnt[CNT_SLOTS + i0] = (i0 == 2 && *halt) ? kOvPipeline : 0ull;
   if (i0 == 3) cnt[CNT_BIG] = 0ull;
+  if (i0 == 4) {  // this pass's stamp: every prep runs on the handle's stream, one after the other
+    const unsigned long long st = *stamp_word + 1;
+    *stamp_word = st;
+    cnt[CNT_STAMP] = st;
+  }
   if (i0 == 0) *other_n = 0ull;
   if (i0 < kShards * kShardWords) fsh[i0] = 0ull;
   for (int64_t i = i0; i < n_edge; i += stride) edge_slot[i] = -1;
@@ -182,11 +189,12 @@ __device__ inline int root_rank(const uint64_t* s_root, const int32_t* pre, int 
 __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
     FGeom g, const uint64_t* __restrict__ fbits, const int32_t* __restrict__ jlist,
     const int32_t* __restrict__ ftiles, const unsigned long long* __restrict__ list_n,
-    int32_t* border, unsigned long long* rel, unsigned long long stamp,
+    int32_t* border, unsigned long long* rel,
     long long* __restrict__ slot_label, int32_t* slot_parent,
     long long* __restrict__ slot_own, long long* __restrict__ slot_acc,
     uint8_t* __restrict__ mask, int32_t* __restrict__ cell_slot, int32_t* __restrict__ edge_slot,
     unsigned long long* cnt, unsigned long long* fsh, int count_stats) {
+  const unsigned long long stamp = cnt[CNT_STAMP];  // this pass's (k_frontier_prep)
   __shared__ uint64_t s_F[DM_TS];          // frontier bit rows
   __shared__ int32_t s_rbase[DM_TS + 1];
   __shared__ int32_t r_par[kMaxRuns];
@@ -712,11 +720,12 @@ __global__ __launch_bounds__(kFW * 64) void k_frontier_bits(FGeom g, const int8_
 __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
     FGeom g, const uint64_t* __restrict__ fbits,
     const int32_t* __restrict__ ftiles, const unsigned long long* __restrict__ list_n,
-    int32_t* border, unsigned long long* rel, unsigned long long stamp,
+    int32_t* border, unsigned long long* rel,
     long long* __restrict__ slot_label, int32_t* slot_parent,
     long long* __restrict__ slot_own, long long* __restrict__ slot_acc,
     uint8_t* __restrict__ mask, int32_t* __restrict__ cell_slot, int32_t* __restrict__ edge_slot,
     unsigned long long* cnt, unsigned long long* fsh, int32_t* __restrict__ big_list) {
+  const unsigned long long stamp = cnt[CNT_STAMP];  // this pass's (k_frontier_prep)
   __shared__ int32_t s_par[kFW][kRunsFast];
   __shared__ unsigned long long s_acc[kFW][kRunsFast];  // size << 40 | sum_x << 20 | sum_y (tile-local)
   __shared__ uint64_t s_rootw[kFW][kRunsFast / 64];     // root-run bits
@@ -1417,6 +1426,8 @@ int grid_for(int64_t n, int threads, int64_t cap) {
 
 }  // namespace
 
+static_assert(sizeof(FGeom) == 88, "FGeom has no implicit padding");
+
 static FGeom make_fgeom(const dm_grid* g, bool want_mask, bool want_labels) {
   FGeom fg;
   fg.W = (int32_t)g->W;
@@ -1443,7 +1454,7 @@ DM_PH_READER(ftile)
 // Band edge-row labels (dm_get_edge_labels; only the host-side band merge
 // reads them), from the last frontier call's slots.
 int dm_launch_edge_labels(dm_grid* g) {
-  hipLaunchKernelGGL(k_slot_labels, dim3(grid_for(2 * g->W, 256, 1024)), dim3(256), 0, g->stream,
+  DM_LAUNCH(k_slot_labels, dim3(grid_for(2 * g->W, 256, 1024)), dim3(256), 0, g->stream,
                      2 * g->W, g->slot_cap, g->edge_slot, g->slot_root, g->slot_label, g->edge_label);
   DM_HIP(hipGetLastError());
   return DM_OK;
@@ -1458,8 +1469,8 @@ int dm_launch_rank_sort(hipStream_t stream, long long* clusters, const long long
   const int64_t cap = std::min<int64_t>(max_records, kRankSortCap);
   // one workgroup per 64 expected records (twice the last pass's count, at
   // least 2048): a thousand idle 1024-thread workgroups cost microseconds
-  const int64_t want = std::max<int64_t>(2 * expect, 2048);
-  hipLaunchKernelGGL(k_rank_sort, dim3(grid_for(std::min(cap, want), 64, 1 << 20)), dim3(kSortThreads), 0, stream,
+  const int64_t want = dm_quantize_up(std::max<int64_t>(2 * expect, 2048));
+  DM_LAUNCH(k_rank_sort, dim3(grid_for(std::min(cap, want), 64, 1 << 20)), dim3(kSortThreads), 0, stream,
                      ox, oy, res, clusters, sums, labels, d_count, cap, out, rank_of, d_sorted, cnt, ncnt, sorted_idx,
                      fsh, host_out, host_cap);
   DM_HIP(hipGetLastError());
@@ -1485,16 +1496,16 @@ int dm_launch_bucket_sort(dm_grid* g, hipStream_t stream, long long* clusters, c
   int32_t* roff = rcnt + (kBuckets + 1);
   int32_t* rcur = roff + (kBuckets + 1);
   const int eg = grid_for(max_records, 256, 2048);
-  hipLaunchKernelGGL(k_bs_count, dim3(eg), dim3(256), 0, stream, clusters, labels, d_count, max_records, base,
+  DM_LAUNCH(k_bs_count, dim3(eg), dim3(256), 0, stream, clusters, labels, d_count, max_records, base,
                      shift, rcnt);
   DM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_bs_scan, dim3(1), dim3(kScanThreads), 0, stream, d_count, max_records, nbk, rcnt,
+  DM_LAUNCH(k_bs_scan, dim3(1), dim3(kScanThreads), 0, stream, d_count, max_records, nbk, rcnt,
                      roff, rcur);
   DM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_bs_place, dim3(eg), dim3(256), 0, stream, clusters, labels, d_count, max_records,
+  DM_LAUNCH(k_bs_place, dim3(eg), dim3(256), 0, stream, clusters, labels, d_count, max_records,
                      base, shift, rcur, g->bs_key, g->bs_idx);
   DM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_bs_rank, dim3(eg), dim3(256), 0, stream, g->p.origin_x, g->p.origin_y,
+  DM_LAUNCH(k_bs_rank, dim3(eg), dim3(256), 0, stream, g->p.origin_x, g->p.origin_y,
                      g->p.resolution, clusters, sums, labels, d_count, max_records, base, shift, roff, g->bs_key,
                      g->bs_idx, out, rank_of, d_sorted, cnt, ncnt, sorted_idx, fsh, host_out, host_cap);
   DM_HIP(hipGetLastError());
@@ -1507,6 +1518,8 @@ int dm_launch_bucket_sort(dm_grid* g, hipStream_t stream, long long* clusters, c
 int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool split, hipStream_t* end_stream) {
   const FGeom fg = make_fgeom(g, want_mask, want_labels);
   const int64_t cells = g->R * g->W;
+  // the kernels below go out as one graph per stream (dm_batch.h)
+  DmBatchScope batch(&g->batch, !g->profile);
   // the prep and the bit rows run on g->stream after everything shared with
   // the pass stream (labelling of earlier passes) -- except for split passes,
   // which keep that order on the pass stream itself
@@ -1524,16 +1537,19 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   unsigned long long* zero_n = g->fl_n + 16 * ((g->fr_pass + 1) % 3);  // last used by pass fr_pass - 2
   KernelTimer t;
   dm_timer_begin(g, "frontier_prep", &t);
-  hipLaunchKernelGGL(k_frontier_prep, dim3(grid_for(std::max<int64_t>(std::max<int64_t>(g->NT, 2 * g->W), kShards * kShardWords), 256, 1024)), dim3(256), 0,
+  DM_LAUNCH(k_frontier_prep, dim3(grid_for(std::max<int64_t>(std::max<int64_t>(g->NT, 2 * g->W), kShards * kShardWords), 256, 1024)), dim3(256), 0,
                      g->stream, g->NT, g->tile_free, g->ftiles, list_n, zero_n, 2 * g->W, g->cnt, g->fsh,
-                     g->edge_slot, g->slot_parent, g->slot_cap, g->fe_flag + kHaltWord);
+                     g->edge_slot, g->slot_parent, g->slot_cap, g->fe_flag + kHaltWord,
+                     g->bits_flag + kStampWord);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
+  if (want_mask || want_labels) DM_HIP(dm_batch_flush_all());
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));
   // one wave per listed tile; the grid follows the last collected pass's
   // list length (+25 %; the kernels grid-stride, so any count is covered)
-  const int64_t want_waves = g->ftile_hint > 0 ? g->ftile_hint + g->ftile_hint / 4 + 64 : g->NT;
+  // (quantised: the grid is part of the cached graph's key, dm_batch.h)
+  const int64_t want_waves = g->ftile_hint > 0 ? dm_quantize_up(g->ftile_hint + g->ftile_hint / 4 + 64) : g->NT;
   const int wave_grid = grid_for(std::min<int64_t>(want_waves, g->NT), kFW, 8192);
   // fmask while the passes list many tiles (dm_internal.h, fmask_on); a
   // switch on rebuilds the records first unless they still match the state
@@ -1548,7 +1564,7 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
     g->fmask_on = false;
   }
   dm_timer_begin(g, "frontier_bits", &t);
-  hipLaunchKernelGGL(k_frontier_bits, dim3(wave_grid), dim3(kFW * 64), 0, g->stream, fg, g->state, g->halo,
+  DM_LAUNCH(k_frontier_bits, dim3(wave_grid), dim3(kFW * 64), 0, g->stream, fg, g->state, g->halo,
                      g->fmask, g->ftiles, list_n, g->fbits, g->cnt, g->fmask_on ? 1 : 0);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
@@ -1558,10 +1574,10 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   if (split) {
     ps = g->pass_stream;
     if (g->pass_gate) {
-      const unsigned long long seq = ++g->bits_seq;
-      if (int rc = dm_launch_signal(g->stream, g->bits_flag, seq)) return rc;
-      if (int rc = dm_launch_gate(ps, g->bits_flag, seq, g->cnt + CNT_OVERFLOW, kOvGate)) return rc;
+      if (int rc = dm_launch_signal(g->stream, g->bits_flag)) return rc;
+      if (int rc = dm_launch_gate(ps, g->bits_flag, g->cnt + CNT_OVERFLOW, kOvGate)) return rc;
     } else {
+      DM_HIP(dm_batch_flush_all());
       DM_HIP(hipEventRecord(g->ev_bits, g->stream));
       DM_HIP(hipStreamWaitEvent(ps, g->ev_bits, 0));
     }
@@ -1584,8 +1600,8 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
                       g->ftf_hint <= kDenseMaxTiles);
   if (!dense) {
     dm_timer_begin(g, "frontier_tile", &t, ps);
-    hipLaunchKernelGGL(k_frontier_tile, dim3(wave_grid), dim3(kFW * 64), 0, ps, fg, g->fbits,
-                       g->ftiles, list_n, g->border, g->rel, (unsigned long long)g->fr_pass,
+    DM_LAUNCH(k_frontier_tile, dim3(wave_grid), dim3(kFW * 64), 0, ps, fg, g->fbits,
+                       g->ftiles, list_n, g->border, g->rel,
                        g->slot_label, g->slot_parent, g->slot_own, g->slot_acc, g->mask, g->cell_slot,
                        g->edge_slot, g->cnt, g->fsh, g->big_tiles);
     dm_timer_end(g, &t);
@@ -1594,15 +1610,14 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   dm_timer_begin(g, dense ? "frontier_tile" : "frontier_big", &t, ps);
   // the leftover tiles of the wave kernel: the grid follows the last pass's
   // count (the kernel grid-strides)
-  const int big_grid = grid_for(std::min<int64_t>(g->NT, g->big_hint + g->big_hint / 4 + 64), 1, 8192);
+  const int big_grid = grid_for(std::min<int64_t>(g->NT, dm_quantize_up(g->big_hint + g->big_hint / 4 + 64)), 1, 8192);
   // dense: one workgroup per listed tile of the last collected pass (+25 %;
   // the kernel grid-strides): thousands of empty workgroups would only keep
   // the dispatcher from the other streams' kernels
-  const int dense_grid = grid_for(std::min<int64_t>(g->NT, g->ftile_hint > 0 ? g->ftile_hint + g->ftile_hint / 4 + 64
-                                                                            : g->NT), 1, 8192);
-  hipLaunchKernelGGL(k_frontier_tile_big, dim3(dense ? dense_grid : big_grid),
+  const int dense_grid = grid_for(std::min<int64_t>(g->NT, g->ftile_hint > 0 ? want_waves : g->NT), 1, 8192);
+  DM_LAUNCH(k_frontier_tile_big, dim3(dense ? dense_grid : big_grid),
                      dim3(kFT), 0, ps, fg, g->fbits, dense ? nullptr : g->big_tiles, g->ftiles,
-                     dense ? list_n : g->cnt + CNT_BIG, g->border, g->rel, (unsigned long long)g->fr_pass,
+                     dense ? list_n : g->cnt + CNT_BIG, g->border, g->rel,
                      g->slot_label, g->slot_parent, g->slot_own,
                      g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh, dense ? 1 : 0);
   dm_timer_end(g, &t);
@@ -1613,20 +1628,20 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   // (no k_frontier_compact); the sort reads the sums by slot
   const int fuse = g->p.min_frontier_size <= 1 ? 1 : 0;
   // one workgroup per CU: fewer workgroups = fewer per-root flushes
-  hipLaunchKernelGGL(k_frontier_resolve, dim3(grid_for(g->slot_cap, 256, g->n_cu)), dim3(256), 0, ps, fg,
+  DM_LAUNCH(k_frontier_resolve, dim3(grid_for(g->slot_cap, 256, g->n_cu)), dim3(256), 0, ps, fg,
                      g->slot_parent, g->slot_root, g->slot_own, g->slot_acc, g->fsh, fuse, g->slot_label,
                      g->clusters, g->slot_k, g->cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (!fuse) {
     dm_timer_begin(g, "frontier_compact", &t, ps);
-    hipLaunchKernelGGL(k_frontier_compact, dim3(sgrid), dim3(256), 0, ps, fg,
+    DM_LAUNCH(k_frontier_compact, dim3(sgrid), dim3(256), 0, ps, fg,
                        g->slot_root, g->slot_label, g->slot_acc, g->clusters, g->slot_k, g->cnt, g->fsh);
     dm_timer_end(g, &t);
     DM_HIP(hipGetLastError());
   }
   if (want_labels) {
-    hipLaunchKernelGGL(k_slot_labels, dim3(grid_for(cells, 256, 8192)), dim3(256), 0, ps,
+    DM_LAUNCH(k_slot_labels, dim3(grid_for(cells, 256, 8192)), dim3(256), 0, ps,
                        cells, g->slot_cap, g->cell_slot, g->slot_root, g->slot_label, g->labels);
     DM_HIP(hipGetLastError());
   }
@@ -1644,6 +1659,7 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
                             g->cnt, CNT_N, CNT_SORTED, g->fsh, g->h_out_dev, g->h_out_cap, g->sort_hint);
   dm_timer_end(g, &t);
   if (rc) return rc;
+  DM_HIP(batch.finish());
   return DM_OK;
 }
 

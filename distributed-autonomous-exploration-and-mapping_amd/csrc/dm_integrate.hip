@@ -911,16 +911,21 @@ __global__ __launch_bounds__(256) void k_integrate_reset(unsigned long long* cnt
 // out: PMC passes run the steps without overlap (tools/pmc_passes.sh).
 constexpr unsigned long long kGateTicks = 500000000ull;  // 5 s
 
-__global__ __launch_bounds__(64) void k_seq_signal(unsigned long long* flag, unsigned long long seq) {
-  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__global__ __launch_bounds__(64) void k_seq_signal(unsigned long long* flag) {
+  if (threadIdx.x != 0) return;
+  // only this stream's signals write the word, one after the other
+  const unsigned long long v = __hip_atomic_load(flag + kSigWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(flag + kSigWord, v + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(64) void k_seq_gate(const unsigned long long* flag, unsigned long long seq,
-                                                 unsigned long long* err, unsigned long long err_bit,
-                                                 unsigned long long ticks) {
+__global__ __launch_bounds__(64) void k_seq_gate(unsigned long long* flag, unsigned long long* err,
+                                                 unsigned long long err_bit, unsigned long long ticks,
+                                                 unsigned long long fault) {
   if (threadIdx.x != 0) return;
+  const unsigned long long seq = flag[kGateWord] + 1;  // this gate's turn (only gates write the word)
+  flag[kGateWord] = seq;
   const unsigned long long t0 = wall_clock64();
-  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < seq) {
+  while (__hip_atomic_load(flag + kSigWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < seq + fault) {
     __builtin_amdgcn_s_sleep(2);
     if (wall_clock64() - t0 > ticks) {
       atomicOr(err, err_bit);
@@ -1035,6 +1040,9 @@ __global__ __launch_bounds__(256) void k_map_image(int64_t R, int64_t W, const i
   }
 }
 
+static_assert(sizeof(Geom) == 64 && sizeof(RayArgs) == 40 && sizeof(ApplyArgs) == 24,
+              "kernel argument structs have no implicit padding (dm_batch.h cache keys)");
+
 Geom make_geom(const dm_grid* g) {
   Geom ge;
   ge.r.W = (int32_t)g->W;
@@ -1083,6 +1091,8 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   // two calls ago
   g->iw_cur ^= 1;
   dm_grid::IntWs& w = g->iw[g->iw_cur];
+  // the kernels below go out as one graph per stream (dm_batch.h)
+  DmBatchScope batch(&g->batch, !g->profile);
   // front-end stream: with overlap, its own stream, after the accumulation
   // that last used this set (ev_free), so it runs beside the previous call's
   // accumulation and a frontier pass still in flight on g->stream
@@ -1092,9 +1102,10 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
     DM_HIP(dm_mark_ws_free(g));  // still owed when no frontier pass came in between
     DM_HIP(hipStreamWaitEvent(fs, w.free_wait ? w.free_wait : w.ev_free, 0));
   }
-  hipLaunchKernelGGL(k_integrate_reset, dim3(2), dim3(256), 0, fs, w.cnt, w.sh);
+  DM_LAUNCH(k_integrate_reset, dim3(2), dim3(256), 0, fs, w.cnt, w.sh);
   DM_HIP(hipGetLastError());
   if (nb == 0) {
+    DM_HIP(batch.finish());
     if (g->overlap) {  // keep the stream order of the calls
       DM_HIP(hipEventRecord(g->ev_fe, fs));
       DM_HIP(hipStreamWaitEvent(g->stream, g->ev_fe, 0));
@@ -1117,38 +1128,38 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   const int nblk = (int)((nb * ge.chunks + 255) / 256);
   KernelTimer t;
   dm_timer_begin(g, "beam_prep", &t, fs);
-  hipLaunchKernelGGL(k_beam_prep, dim3(nblk), dim3(256), 0, fs, a, ge, d_pose4, d_ranges,
+  DM_LAUNCH(k_beam_prep, dim3(nblk), dim3(256), 0, fs, a, ge, d_pose4, d_ranges,
                      d_trig, g->beams, w.tile_count, g->act_raw, w.sh, g->blk_hist, g->blk_n, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "plan", &t, fs);
-  hipLaunchKernelGGL(k_plan, dim3(grid_for(g->act_cap, kPlanThreads, 256)), dim3(kPlanThreads), 0, fs,
+  DM_LAUNCH(k_plan, dim3(grid_for(g->act_cap, kPlanThreads, 256)), dim3(kPlanThreads), 0, fs,
                      ge, g->act_raw, w.sh, w.tile_cur, w.tile_count, w.hitems, w.litems,
                      w.heavy_list, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "scatter", &t, fs);
-  hipLaunchKernelGGL(k_scatter, dim3(nblk), dim3(256), 0, fs, a, ge, g->beams,
+  DM_LAUNCH(k_scatter, dim3(nblk), dim3(256), 0, fs, a, ge, g->beams,
                      w.tile_cur, g->blk_hist, g->blk_n, w.pieces, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (g->overlap && !g->fe_gate) {
+    DM_HIP(dm_batch_flush_all());
     DM_HIP(hipEventRecord(g->ev_fe, fs));
     DM_HIP(hipStreamWaitEvent(g->stream, g->ev_fe, 0));
   } else if (g->overlap) {
-    const unsigned long long seq = ++g->fe_seq;
-    if (int rc = dm_launch_signal(fs, g->fe_flag, seq)) return rc;
+    if (int rc = dm_launch_signal(fs, g->fe_flag)) return rc;
     // a timeout sets the sticky halt word (not this call's counters: the
     // front-end's own reset, still queued, would clear them)
-    if (int rc = dm_launch_gate(g->stream, g->fe_flag, g->fault_gate ? seq + (1ull << 40) : seq,
-                                g->fe_flag + kHaltWord, 1ull, g->fault_gate ? 1000ull : 0ull))
+    if (int rc = dm_launch_gate(g->stream, g->fe_flag, g->fe_flag + kHaltWord, 1ull, g->fault_gate ? 1000ull : 0ull,
+                                g->fault_gate ? (1ull << 40) : 0ull))
       return rc;
   }
   const int vec_ok = (g->W % 4 == 0) ? 1 : 0;
   // heavy chunks and medium tiles first (the long items), then the light
   // tiles; k_heavy_apply then applies the heavy tiles' merged slabs
   dm_timer_begin(g, "tile_accum", &t);
-  hipLaunchKernelGGL(k_tile_accum, dim3(grid_for(g->hitem_cap + g->act_cap, 1, 16384)),
+  DM_LAUNCH(k_tile_accum, dim3(grid_for(g->hitem_cap + g->act_cap, 1, 16384)),
                      dim3(kQuarter), 0,
                      g->stream, ge, make_apply(g), w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS,
                      w.pieces, w.tile_count, g->tile_free, w.slabs, g->L, g->state, w.cnt, w.sh, vec_ok,
@@ -1163,7 +1174,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   const int64_t max_tile_pieces = nb * (ge.chunks > 1 ? 2 : 1);
   if (max_tile_pieces > kMedium && !g->fuse_heavy) {
     dm_timer_begin(g, "heavy_apply", &t);
-    hipLaunchKernelGGL(k_heavy_apply, dim3(grid_for(4 * g->heavy_cap, 1, 1024)), dim3(kQuarter), 0, g->stream,
+    DM_LAUNCH(k_heavy_apply, dim3(grid_for(4 * g->heavy_cap, 1, 1024)), dim3(kQuarter), 0, g->stream,
                        ge, make_apply(g), w.heavy_list, w.tile_count, g->tile_free, w.slabs, g->L, g->state,
                        w.cnt, w.sh, g->fe_flag + kHaltWord);
     dm_timer_end(g, &t);
@@ -1173,33 +1184,37 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   // frontier passes read them
   if (!g->fmask_on) {
     g->fmask_valid = false;
+    DM_HIP(batch.finish());
     return DM_OK;
   }
   dm_timer_begin(g, "fmask", &t);
-  hipLaunchKernelGGL(k_fmask_items, dim3(grid_for(g->hitem_cap + g->act_cap, 4, 8192)), dim3(256), 0, g->stream,
+  DM_LAUNCH(k_fmask_items, dim3(grid_for(g->hitem_cap + g->act_cap, 4, 8192)), dim3(256), 0, g->stream,
                      ge, w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS, w.cnt, g->state, g->fmask,
                      g->fe_flag + kHaltWord);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
+  DM_HIP(batch.finish());
   return DM_OK;
 }
 
-int dm_launch_signal(hipStream_t s, unsigned long long* flag, unsigned long long seq) {
-  hipLaunchKernelGGL(k_seq_signal, dim3(1), dim3(64), 0, s, flag, seq);
+int dm_launch_signal(hipStream_t s, unsigned long long* flag) {
+  DM_LAUNCH(k_seq_signal, dim3(1), dim3(64), 0, s, flag);
   DM_HIP(hipGetLastError());
   return DM_OK;
 }
 
-int dm_launch_gate(hipStream_t s, const unsigned long long* flag, unsigned long long seq,
-                   unsigned long long* err, unsigned long long err_bit, unsigned long long ticks) {
-  hipLaunchKernelGGL(k_seq_gate, dim3(1), dim3(64), 0, s, flag, seq, err, err_bit, ticks ? ticks : kGateTicks);
+int dm_launch_gate(hipStream_t s, unsigned long long* flag, unsigned long long* err, unsigned long long err_bit,
+                   unsigned long long ticks, unsigned long long fault) {
+  // the signals it may wait for are submitted first (dm_batch.h)
+  DM_HIP(dm_batch_flush_others(s));
+  DM_LAUNCH(k_seq_gate, dim3(1), dim3(64), 0, s, flag, err, err_bit, ticks ? ticks : kGateTicks, fault);
   DM_HIP(hipGetLastError());
   return DM_OK;
 }
 
 int dm_launch_recount(dm_grid* g) {
   const Geom ge = make_geom(g);
-  hipLaunchKernelGGL(k_recount, dim3((unsigned)g->NT), dim3(256), 0, g->stream, ge, g->state,
+  DM_LAUNCH(k_recount, dim3((unsigned)g->NT), dim3(256), 0, g->stream, ge, g->state,
                      g->tile_free, g->fmask);
   DM_HIP(hipGetLastError());
   g->fmask_valid = true;
@@ -1208,7 +1223,7 @@ int dm_launch_recount(dm_grid* g) {
 
 int dm_launch_state_from_logodds(dm_grid* g) {
   const int64_t cells = g->R * g->W;
-  hipLaunchKernelGGL(k_state_from_l, dim3(grid_for(cells, 256)), dim3(256), 0, g->stream,
+  DM_LAUNCH(k_state_from_l, dim3(grid_for(cells, 256)), dim3(256), 0, g->stream,
                      make_apply(g), cells, g->L, g->state);
   DM_HIP(hipGetLastError());
   return dm_launch_recount(g);
@@ -1216,7 +1231,7 @@ int dm_launch_state_from_logodds(dm_grid* g) {
 
 int dm_launch_set_state(dm_grid* g, const int8_t* d_in) {
   const int64_t cells = g->R * g->W;
-  hipLaunchKernelGGL(k_set_state, dim3(grid_for(cells, 256)), dim3(256), 0, g->stream,
+  DM_LAUNCH(k_set_state, dim3(grid_for(cells, 256)), dim3(256), 0, g->stream,
                      make_apply(g), cells, d_in, g->L, g->state);
   DM_HIP(hipGetLastError());
   return dm_launch_recount(g);
@@ -1224,7 +1239,7 @@ int dm_launch_set_state(dm_grid* g, const int8_t* d_in) {
 
 int dm_launch_map_image(dm_grid* g, uint8_t* d_img) {
   const int64_t cells = g->R * g->W;
-  hipLaunchKernelGGL(k_map_image, dim3(grid_for(cells, 256)), dim3(256), 0, g->stream, g->R,
+  DM_LAUNCH(k_map_image, dim3(grid_for(cells, 256)), dim3(256), 0, g->stream, g->R,
                      g->W, g->state, d_img);
   DM_HIP(hipGetLastError());
   return DM_OK;

@@ -20,6 +20,7 @@
 
 #include "../../include/dm.h"
 
+#include "dm_batch.h"
 #include "dm_ray.h"
 
 
@@ -38,7 +39,7 @@ enum {
   CNT_TH = 10,      // touched cells of heavy tiles
   CNT_SORTED = 11,  // 1: out_clu holds the clusters sorted by label
   CNT_FL0 = 12,     // frontier tile-list length of the pass (copied by k_frontier_bits)
-  CNT_FL1 = 13,     // (unused)
+  CNT_STAMP = 13,   // the pass's stamp (k_frontier_prep: ++ the handle's stamp word), tile-edge hand-offs
   CNT_LITEMS = 14,  // light work items (= light tiles)
   CNT_IOVERFLOW = 15,  // integrate capacity overflow flags (1 first-touch list, 2 pieces, 4 work lists)
   CNT_BIG = 16,     // frontier tiles with more runs than a tile-wave holds (big-tile list length)
@@ -55,6 +56,13 @@ constexpr unsigned long long kOvPipeline = 32ull;  // the handle's sticky hand-o
 // would read was not written), k_frontier_prep flags every pass kOvPipeline,
 // and the host reports DM_ERR_PIPELINE until dm_reset clears it.
 constexpr int kHaltWord = 8;
+// Hand-off words (fe_flag, bits_flag): k_seq_signal increments [kSigWord],
+// k_seq_gate increments [kGateWord] and waits until [kSigWord] reaches it:
+// the n-th gate waits for the n-th signal, with no host-side sequence number
+// in the kernel arguments (dm_batch.h: the graphs are reused).
+constexpr int kSigWord = 0;
+constexpr int kGateWord = 4;
+constexpr int kStampWord = 8;  // bits_flag: the last frontier pass's stamp (k_frontier_prep)
 // Integrate counters, zeroed by each integrate call; the others belong to the
 // frontier pass, which may still be running when the next call's front-end
 // starts (dm_set_overlap), so the integrate reset never touches them.
@@ -127,8 +135,7 @@ struct dm_grid {
   hipEvent_t ev_fe = nullptr;
   // front-end completion word (k_fe_signal / k_fe_gate, dm_integrate.hip):
   // the sequence number of the last call whose front-end finished
-  unsigned long long* fe_flag = nullptr;  // [0] sequence, [kHaltWord] sticky hand-off error
-  unsigned long long fe_seq = 0;
+  unsigned long long* fe_flag = nullptr;  // [kSigWord] / [kGateWord] hand-off counts, [kHaltWord] sticky error
   // DM_FAULT_GATE=1 (read at dm_create; fault-injection tests only): the
   // front-end gate waits for a sequence number that never comes, ~10 us
   bool fault_gate = false;
@@ -272,8 +279,7 @@ struct dm_grid {
   // batch's map update overlaps it.  bits_flag / bits_seq: the bit rows'
   // hand-off (k_seq_signal on `stream`, k_seq_gate on pass_stream).
   hipStream_t pass_stream = nullptr;
-  unsigned long long* bits_flag = nullptr;
-  unsigned long long bits_seq = 0;
+  unsigned long long* bits_flag = nullptr;  // [kSigWord] / [kGateWord] counts, [kStampWord] pass stamp
   hipEvent_t p_tail = nullptr;        // the last pass_stream pass's end (alias)
   bool p_pending = false;             // pass_stream work `stream` has not been ordered after
   uint64_t p_tail_pass = 0;
@@ -345,6 +351,9 @@ struct dm_grid {
   int64_t goal_cap = 0;
   double* goal_io = nullptr;          // [4 * 256] robots xy, then centroids xy
   int64_t* goal_idx = nullptr;        // [256]
+
+  // launch batching (dm_batch.h): chains and the graph cache
+  DmBatch batch;
 
   // profiling
   bool profile = false;
@@ -423,12 +432,13 @@ int dm_launch_set_state(dm_grid* g, const int8_t* d_state_in);
 // overlap); *end_stream receives the stream the pass ends on.
 int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool split = false,
                          hipStream_t* end_stream = nullptr);
-// Sequence hand-off between streams (dm_integrate.hip): k_seq_signal stores
-// seq into *flag; k_seq_gate (one lane) waits until *flag >= seq, or sets
+// Hand-off between streams (dm_integrate.hip): k_seq_signal counts
+// flag[kSigWord] up; k_seq_gate (one lane) counts flag[kGateWord] up and waits
+// until flag[kSigWord] reaches it (+ fault: fault-injection tests), or sets
 // err_bit in *err after a bounded time (ticks of the 100 MHz clock, 0: 5 s).
-int dm_launch_signal(hipStream_t s, unsigned long long* flag, unsigned long long seq);
-int dm_launch_gate(hipStream_t s, const unsigned long long* flag, unsigned long long seq,
-                   unsigned long long* err, unsigned long long err_bit, unsigned long long ticks = 0);
+int dm_launch_signal(hipStream_t s, unsigned long long* flag);
+int dm_launch_gate(hipStream_t s, unsigned long long* flag, unsigned long long* err, unsigned long long err_bit,
+                   unsigned long long ticks = 0, unsigned long long fault = 0);
 int dm_launch_edge_labels(dm_grid* g);
 int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied);
 int dm_launch_frontiers(dm_grid* g, bool want_mask, bool want_labels, int64_t* n_clusters,
@@ -480,3 +490,7 @@ void dm_timer_end(dm_grid* g, KernelTimer* t);
     hipError_t _e = (call);                                  \
     if (_e != hipSuccess) return dm_hip_check(_e, #call);    \
   } while (0)
+
+// Kernel launch (dm_batch.h: recorded into a graph chain inside a
+// DmBatchScope, launched directly otherwise).
+#define DM_LAUNCH(...) DM_HIP(dm_launch(__VA_ARGS__))
