@@ -42,9 +42,9 @@ hipError_t dm_copy_shards(dm_grid* g) {
 namespace {
 thread_local std::string t_err;
 
-bool dm_env_off(const char* name) {
+bool dm_env_on(const char* name) {  // opt-in A/B switches: NAME=1
   const char* v = getenv(name);
-  return v && v[0] == '0';
+  return v && v[0] == '1';
 }
 
 struct HostCluster {
@@ -471,14 +471,15 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   {
     const char* sep = getenv("DM_HEAVY_SEPARATE");
     g->fuse_heavy = !(sep && sep[0] == '1');
-    g->fe_gate = !dm_env_off("DM_FE_GATE");
-    g->pass_gate = !dm_env_off("DM_PASS_GATE");
+    // cross-stream hand-offs by event waits unless DM_FE_GATE=1 / DM_PASS_GATE=1
+    // (device-side seq gates): events measured 185-188 vs 179-183 x 10^9 at
+    // C3 (profiles/r02_gate_ab.log, r02_graphs_ab.log)
+    g->fe_gate = dm_env_on("DM_FE_GATE");
+    g->pass_gate = dm_env_on("DM_PASS_GATE");
     // launch batching into graphs (dm_batch.h) only with DM_GRAPHS=1: measured
     // neutral to slightly slower at C3
-    const char* gr = getenv("DM_GRAPHS");
-    g->batch.enabled = gr && gr[0] == '1';
-    const char* fg = getenv("DM_FAULT_GATE");
-    g->fault_gate = fg && fg[0] == '1';
+    g->batch.enabled = dm_env_on("DM_GRAPHS");
+    g->fault_gate = dm_env_on("DM_FAULT_GATE");
     const char* fm = getenv("DM_FMASK");
     g->fmask_mode = fm && !strcmp(fm, "on") ? 1 : (fm && !strcmp(fm, "off") ? 2 : 0);
     const char* fk = getenv("DM_FRONTIER_KERNEL");
@@ -549,7 +550,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   // scope fence (no host-visible cache writeback at every step).  The host
   // waits on a readback slot's event and then reads mapped host memory:
   // default fences.
-  for (hipEvent_t* ev : {&g->ev_fe, &g->ev_bits, &g->iw[0].ev_free, &g->iw[1].ev_free}) {
+  for (hipEvent_t* ev : {&g->ev_fe, &g->ev_bits[0], &g->ev_bits[1], &g->iw[0].ev_free, &g->iw[1].ev_free}) {
     e = hipEventCreateWithFlags(ev, hipEventDisableTiming | hipEventDisableSystemFence);
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
   }
@@ -572,7 +573,7 @@ int dm_destroy(dm_grid* g) {
   (void)dm_sync_all(g);
   dm_batch_release(&g->batch);
   for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
-  for (hipEvent_t ev : {g->ev_fe, g->ev_bits, g->iw[0].ev_free, g->iw[1].ev_free})
+  for (hipEvent_t ev : {g->ev_fe, g->ev_bits[0], g->ev_bits[1], g->iw[0].ev_free, g->iw[1].ev_free})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& r : g->rb) {
     if (r.ev) (void)hipEventDestroy(r.ev);

@@ -56,6 +56,8 @@ hipError_t dm_batch_flush(DmBatch* b, DmChain& c) {
     reset(c);
     return e;
   }
+  const unsigned inst = (unsigned)(c.flushes++ % DmBatch::kInstances);
+  c.key.append(reinterpret_cast<const char*>(&inst), sizeof inst);
   auto it = b->cache.find(c.key);
   if (it != b->cache.end()) {
     ++b->hits;

@@ -55,10 +55,17 @@ struct DmChain {
   std::vector<unsigned char> args;  // packed arguments of every launch
   std::vector<size_t> offs;         // offset of each argument in args
   std::string key;
+  uint64_t flushes = 0;  // graph flushes of this chain: the instance index (DmBatch::kInstances)
 };
 
 struct DmBatch {
   static constexpr int kChains = 4;
+  // Consecutive flushes of a chain use different instances of the same
+  // graph (kInstances in rotation), so an instantiated graph is never
+  // relaunched while its previous launch may still be queued.  (With the
+  // rotation, some graph launches still blocked the host for 60-115 us per
+  // step in the C3 pipeline: DESIGN.md §3.3.)
+  static constexpr unsigned kInstances = 4;
   DmChain chains[kChains];
   int n_chains = 0;
   struct Entry {
@@ -67,7 +74,7 @@ struct DmBatch {
   };
   std::unordered_map<std::string, Entry> cache;
   std::list<std::string> order;  // most recently used first
-  size_t cap = 128;
+  size_t cap = 512;
   uint64_t hits = 0, misses = 0, graph_launches = 0, direct_launches = 0;
   bool enabled = true;  // DM_GRAPHS=0: never batch (A/B)
 };

@@ -1578,8 +1578,13 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
       if (int rc = dm_launch_gate(ps, g->bits_flag, g->cnt + CNT_OVERFLOW, kOvGate)) return rc;
     } else {
       DM_HIP(dm_batch_flush_all());
-      DM_HIP(hipEventRecord(g->ev_bits, g->stream));
-      DM_HIP(hipStreamWaitEvent(ps, g->ev_bits, 0));
+      hipEvent_t eb = g->ev_bits[g->fparity];
+      DM_HIP(hipEventRecord(eb, g->stream));
+      // (re-recorded two passes later: a front-end waiting on it then waits
+      // longer than needed, never too little -- every record follows the
+      // accumulations it frees in stream order)
+      DM_HIP(dm_mark_ws_free(g, eb));
+      DM_HIP(hipStreamWaitEvent(ps, eb, 0));
     }
   }
   if (end_stream) *end_stream = ps;

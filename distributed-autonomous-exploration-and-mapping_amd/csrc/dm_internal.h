@@ -139,9 +139,13 @@ struct dm_grid {
   // DM_FAULT_GATE=1 (read at dm_create; fault-injection tests only): the
   // front-end gate waits for a sequence number that never comes, ~10 us
   bool fault_gate = false;
-  bool fe_gate = true;  // DM_FE_GATE=0: cross-stream event wait instead (A/B)
-  bool pass_gate = true;  // DM_PASS_GATE=0: the bit rows' hand-off by an event wait (ev_bits) instead
-  hipEvent_t ev_bits = nullptr;
+  bool fe_gate = false;    // DM_FE_GATE=1: the front-end hand-off by a seq gate instead of ev_fe
+  bool pass_gate = false;  // DM_PASS_GATE=1: the bit rows' hand-off by a seq gate instead of ev_bits
+  // ev_bits[parity]: the end of a split pass's bit rows on `stream` (the pass
+  // stream waits for it); it also frees the integrate workspaces whose
+  // accumulations are ahead of it (dm_mark_ws_free), so the next front-end
+  // using them can start right away instead of after the whole pass
+  hipEvent_t ev_bits[2] = {nullptr, nullptr};
   uint64_t integrate_seq = 0;  // map changes so far
   // Asynchronous passes (dm_frontiers_begin / dm_merge_bands_begin) use a
   // ring of kRbSlots readback slots, so a pass can be started before the

@@ -15,6 +15,18 @@ __global__ void k_spin(unsigned long long ticks) {
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(1);
 }
 
+struct G64 { int a[16]; };
+struct R40 { int s, n; double x, y, z; float lo, hi; };
+__global__ void k_many(G64 g, R40 r, const double* p0, const float* p1, const double* p2, void* p3, int* p4,
+                       int* p5, unsigned long long* p6, int* p7, unsigned long long* p8, void* p9, int* p10,
+                       unsigned long long* p11, int i0, int i1) {
+  if (threadIdx.x == 0 && g.a[0] == 12345) *p4 = r.s + i0 + i1;
+}
+struct AllArgs { G64 g; R40 r; void* p[12]; int i0, i1; };
+__global__ void k_one(AllArgs a) {
+  if (threadIdx.x == 0 && a.g.a[0] == 12345) *(int*)a.p[4] = a.r.s + a.i0;
+}
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
 static double now_us() {
@@ -99,6 +111,43 @@ int main() {
     CK(hipDeviceSynchronize());
     printf("spin %llu us: 7 launches one stream: host %.1f us/step, wall %.1f us/step\n", us, host / steps,
            (now_us() - t0) / steps);
+  }
+  // argument count: 16 arguments (two structs + 12 pointers + 2 ints) vs the
+  // same bytes in one struct argument
+  {
+    G64 g{}; R40 r{}; AllArgs aa{};
+    int* d = nullptr;
+    CK(hipMalloc(&d, 64));
+    for (int rep = 0; rep < 2; ++rep) {
+      CK(hipDeviceSynchronize());
+      double host = 0;
+      for (int i = 0; i < steps; ++i) {
+        double a = now_us();
+        for (int k = 0; k < 14; ++k)
+          hipLaunchKernelGGL(k_many, dim3(64), dim3(256), 0, s[k % 3], g, r, (const double*)d, (const float*)d,
+                             (const double*)d, (void*)d, d, d, (unsigned long long*)d, d, (unsigned long long*)d,
+                             (void*)d, d, (unsigned long long*)d, 1, 2);
+        host += now_us() - a;
+      }
+      CK(hipDeviceSynchronize());
+      printf("16 args: host %.2f us/launch\n", host / steps / 14);
+      host = 0;
+      for (int i = 0; i < steps; ++i) {
+        double a = now_us();
+        for (int k = 0; k < 14; ++k) hipLaunchKernelGGL(k_one, dim3(64), dim3(256), 0, s[k % 3], aa);
+        host += now_us() - a;
+      }
+      CK(hipDeviceSynchronize());
+      printf("1 struct arg (same bytes): host %.2f us/launch\n", host / steps / 14);
+      host = 0;
+      for (int i = 0; i < steps; ++i) {
+        double a = now_us();
+        for (int k = 0; k < 14; ++k) hipLaunchKernelGGL(k_spin, dim3(64), dim3(256), 0, s[k % 3], 0ull);
+        host += now_us() - a;
+      }
+      CK(hipDeviceSynchronize());
+      printf("1 scalar arg: host %.2f us/launch\n", host / steps / 14);
+    }
   }
   return 0;
 }

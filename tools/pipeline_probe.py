@@ -33,6 +33,38 @@ def main():
         p4, r = dpool[k % len(dpool)]
         m.integrate_device(p4.data_ptr(), S, r.data_ptr(), N, amin, inc)
 
+    # raw ctypes calls (no Python wrapper): the C-ABI's own host cost
+    import ctypes
+    lib, h = m._lib, m._handle()
+    buf = np.empty(1 << 16, dtype=np.dtype(dm.CLUSTER_DTYPE))
+    bp, bc = buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(buf.shape[0])
+    nout = ctypes.c_int64(0)
+    raw_args = [(ctypes.c_void_p(p4.data_ptr()), ctypes.c_int32(S), ctypes.c_void_p(r.data_ptr()),
+                 ctypes.c_int32(N), ctypes.c_float(amin), ctypes.c_float(inc)) for p4, r in dpool]
+    for rep in range(2):
+        ti, te, tb = [], [], []
+        t0 = time.perf_counter()
+        steps, depth = 200, 2
+        for k in range(steps):
+            a = time.perf_counter()
+            pp, ss, rr, nn, am, ic = raw_args[k % len(raw_args)]
+            lib.dm_integrate_device(h, ss, pp, nn, rr, am, ic)
+            b = time.perf_counter()
+            if k >= depth:
+                lib.dm_frontiers_end(h, bp, bc, ctypes.byref(nout))
+            c = time.perf_counter()
+            lib.dm_frontiers_begin(h)
+            d = time.perf_counter()
+            ti.append(b - a)
+            te.append(c - b)
+            tb.append(d - c)
+        for _ in range(depth):
+            lib.dm_frontiers_end(h, bp, bc, ctypes.byref(nout))
+        el = time.perf_counter() - t0
+        f = lambda v: 1e6 * float(np.median(v[depth:]))
+        print(f"raw C-ABI depth 2: {1e6 * el / steps:.1f} us/step; integrate call {f(ti):.1f}, "
+              f"frontiers_end {f(te):.1f}, frontiers_begin {f(tb):.1f} us (medians)", flush=True)
+
     for depth in (1, 2, 1, 2):
         ti, te, tb = [], [], []
         t0 = time.perf_counter()
