@@ -413,7 +413,7 @@ def main():
                          if world_size > 1 else None),
             "exchange_fallbacks": getattr(mapper, "fallbacks", 0),
             "pipelined": (f"step k+1's integrate front-end overlaps step k's frontier pass "
-                          f"(dm_set_overlap + dm_frontiers_begin/_end), {min(args.depth, 2)} passes in flight")
+                          f"(dm_set_overlap + dm_frontiers_begin/_end), {args.depth} passes in flight")
             if pipelined else None,
             "cpu_baseline": cpu,
             "gen_seconds": t_gen,

@@ -47,6 +47,11 @@ bool dm_env_on(const char* name) {  // opt-in A/B switches: NAME=1
   return v && v[0] == '1';
 }
 
+bool dm_env_off(const char* name) {  // opt-out A/B switches: NAME=0
+  const char* v = getenv(name);
+  return v && v[0] == '0';
+}
+
 struct HostCluster {
   long long label, size, sum_x, sum_y;
 };
@@ -403,6 +408,7 @@ extern "C" {
 
 const char* dm_last_error(void) { return t_err.c_str(); }
 const char* dm_version(void) { return "dm 0.1.0 (gfx950, HIP)"; }
+int dm_max_passes_in_flight(void) { return dm_grid::kRbSlots; }
 
 int dm_default_params(dm_params* p, int64_t width, int64_t height) {
   if (!p) return dm_set_error(DM_ERR_INVALID_ARG, "params is NULL");
@@ -471,10 +477,13 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   {
     const char* sep = getenv("DM_HEAVY_SEPARATE");
     g->fuse_heavy = !(sep && sep[0] == '1');
-    // cross-stream hand-offs by event waits unless DM_FE_GATE=1 / DM_PASS_GATE=1
-    // (device-side seq gates): events measured 185-188 vs 179-183 x 10^9 at
-    // C3 (profiles/r02_gate_ab.log, r02_graphs_ab.log)
-    g->fe_gate = dm_env_on("DM_FE_GATE");
+    // cross-stream hand-offs (C3 A/B): the front-end ->
+    // map update by a device-side seq gate (DM_FE_GATE=0: an event wait;
+    // gate 215-218 vs event 211-213 x 10^9, profiles/r02_fe_gate_ab.log), the
+    // bit rows -> pass stream by an event wait, which also frees the
+    // integrate workspaces early (DM_PASS_GATE=1: a seq gate, and the
+    // workspaces wait for the pass's readback event: 179-183 x 10^9)
+    g->fe_gate = !dm_env_off("DM_FE_GATE");
     g->pass_gate = dm_env_on("DM_PASS_GATE");
     // launch batching into graphs (dm_batch.h) only with DM_GRAPHS=1: measured
     // neutral to slightly slower at C3

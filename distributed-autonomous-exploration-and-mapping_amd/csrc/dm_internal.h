@@ -139,7 +139,7 @@ struct dm_grid {
   // DM_FAULT_GATE=1 (read at dm_create; fault-injection tests only): the
   // front-end gate waits for a sequence number that never comes, ~10 us
   bool fault_gate = false;
-  bool fe_gate = false;    // DM_FE_GATE=1: the front-end hand-off by a seq gate instead of ev_fe
+  bool fe_gate = true;     // DM_FE_GATE=0: the front-end hand-off by an event wait (ev_fe) instead of a seq gate
   bool pass_gate = false;  // DM_PASS_GATE=1: the bit rows' hand-off by a seq gate instead of ev_bits
   // ev_bits[parity]: the end of a split pass's bit rows on `stream` (the pass
   // stream waits for it); it also frees the integrate workspaces whose
@@ -167,8 +167,11 @@ struct dm_grid {
     int64_t merge_n = 0;              // nranks * rec_cap of a merge
     uint64_t wepoch = 0, mepoch = 0;  // passes / merges that wrote out_clu / m_out so far
   };
-  static constexpr int kRbSlots = 2;   // ring slots of asynchronous passes
-  static constexpr int kRbSync = 2;    // the slot of synchronous calls (dm_frontiers, dm_merge_bands)
+#ifndef DM_RB_SLOTS
+#define DM_RB_SLOTS 2
+#endif
+  static constexpr int kRbSlots = DM_RB_SLOTS;  // ring slots of asynchronous passes
+  static constexpr int kRbSync = kRbSlots;      // the slot of synchronous calls (dm_frontiers, dm_merge_bands)
   RbSlot rb[kRbSlots + 1];
   int rb_head = 0, rb_count = 0;      // oldest pending slot, pending passes
   int cur_slot = 0;                   // the slot dm_select_slot selected

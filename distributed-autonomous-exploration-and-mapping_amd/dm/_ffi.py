@@ -160,6 +160,7 @@ SIGNATURES = {
     "dm_merge_bands_begin": [_vp, _vp, _i32, _i64, _i64],
     "dm_merge_bands_end": [_vp, _vp, _i64, ctypes.POINTER(_i64)],
     "dm_frontiers_begin": [_vp],
+    "dm_max_passes_in_flight": [],
     "dm_frontiers_end": [_vp, _vp, _i64, ctypes.POINTER(_i64)],
     "dm_set_overlap": [_vp, _i32],
     "dm_atomic_peak": [ctypes.c_int, _vp, _i32, ctypes.POINTER(_i32)],

@@ -36,7 +36,7 @@ import collections
 
 import numpy as np
 
-from ._ffi import CLUSTER_DTYPE, DM_TILE, DmParams
+from ._ffi import CLUSTER_DTYPE, DM_TILE, DmParams, load_library
 from .grid import Frontiers, OccupancyMapper
 
 
@@ -161,6 +161,10 @@ class ShardedMapper:
         self._device = None
         self._dev_path = False
         self._pending = collections.deque()  # frontiers_begin() passes in flight, oldest first
+        try:
+            self.max_in_flight = int(load_library().dm_max_passes_in_flight())
+        except Exception:  # a non-libdm band (CPU tests): libdm's default ring
+            self.max_in_flight = 2
         if world_size > 1:
             import torch.distributed as dist
 
@@ -306,10 +310,12 @@ class ShardedMapper:
     def frontiers_begin(self):
         """Start a clusters-only frontier pass over the map as it is now and
         return; frontiers_end() returns its clusters (the same as frontiers()
-        would have), and integrate calls may be made in between.  Up to two
-        passes may be in flight; frontiers_end() collects the oldest."""
-        if len(self._pending) == 2:
-            raise RuntimeError("two frontiers_begin() passes are in flight: call frontiers_end() first")
+        would have), and integrate calls may be made in between.  Up to
+        dm_max_passes_in_flight() passes may be in flight (libdm's readback
+        ring); frontiers_end() collects the oldest."""
+        if len(self._pending) >= self.max_in_flight:
+            raise RuntimeError(f"{len(self._pending)} frontiers_begin() passes are in flight: "
+                               "call frontiers_end() first")
         if self.world_size == 1 and hasattr(self.band, "frontiers_begin"):
             self.band.frontiers_begin()
             self._pending.append(("band", None))

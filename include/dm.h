@@ -187,6 +187,9 @@ int dm_frontiers(dm_grid* g, uint8_t* mask, int64_t* labels, dm_cluster* out,
  * integrating scans while the last frontier request completes. */
 int dm_frontiers_begin(dm_grid* g);
 int dm_frontiers_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out);
+/* The number of asynchronous passes (dm_frontiers_begin /
+ * dm_merge_bands_begin) a handle holds in flight: the readback ring's size. */
+int dm_max_passes_in_flight(void);
 
 /* Overlap mode (default off).  When on, the integrate front-end of
  * dm_integrate / dm_integrate_device (beam preparation, tile planning, piece

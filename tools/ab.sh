@@ -3,6 +3,9 @@
 #   bash tools/ab.sh ROUNDS "tag:VAR=V,VAR2=V2" "tag2:VAR=W" ...
 # Prints value, us/step and the host step cadence per run -> gpurun_out/ab.log
 set -o pipefail
+# per-tag extra bench.py arguments: BENCH_ARGS_<tag>="--depth 3" in the environment
+declare -A BENCH_ARGS
+for v in $(env | grep '^BENCH_ARGS_' | cut -d= -f1); do BENCH_ARGS[${v#BENCH_ARGS_}]="${!v}"; done
 OUT=gpurun_out/ab.log
 : > $OUT
 R=$1; shift
@@ -10,7 +13,7 @@ for r in $(seq $R); do
   for v in "$@"; do
     tag=${v%%:*}; envs=${v#*:}
     env ${envs//,/ } timeout -k 10 120 python -u bench.py --steps 400 --warmup 40 --cpu-seconds 0 --profile-steps 0 \
-      --no-explored --no-host-inputs > gpurun_out/ab_tmp.log 2>&1 || { echo "$tag failed"; tail -5 gpurun_out/ab_tmp.log; exit 1; }
+      --no-explored --no-host-inputs ${BENCH_ARGS[$tag]} > gpurun_out/ab_tmp.log 2>&1 || { echo "$tag failed"; tail -5 gpurun_out/ab_tmp.log; exit 1; }
     python -c "import json; d=json.loads(open('gpurun_out/ab_tmp.log').read().strip().splitlines()[-1]); s=d.get('launch_batching') or {}; print('$tag', round(d['value']/1e9,1), 'e9', round(d['ms_per_step']*1e3,1), 'us/step', 'p50', round(d['step_wall_us']['p50'],1), 'graphs', s.get('graph_launches'), 'hits', s.get('graph_hits'), 'misses', s.get('graph_misses'))" | tee -a $OUT
   done
 done
