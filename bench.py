@@ -822,6 +822,7 @@ def _run_c5(args, np, torch, synth, m, params, amin, dev, world):
             a = time.perf_counter()
             m.frontiers()
             tf.append(time.perf_counter() - a)
+        fst = m.last_stats()  # the last pass's listed tiles, tile-local components, clusters
         mean = lambda key: float(np.mean([st[key] for st in stats]))  # noqa: E731
         avg, roof = _profiled_roofline(m, lambda: [(integrate(k), m.frontiers()) for k in range(5)],
                                        mean("updates"), mean("touched"), mean("touched_heavy"))
@@ -832,6 +833,8 @@ def _run_c5(args, np, torch, synth, m, params, amin, dev, world):
                      "integrate_updates_per_s": mean("updates") / float(np.median(ti)),
                      "updates_per_batch": mean("updates"), "touched_cells_per_batch": mean("touched"),
                      "clusters": len(fr) if fr is not None else None,
+                     "stage_stats": {k: mean(k) for k in ("pieces", "active_tiles", "work_items", "heavy_tiles")},
+                     "frontier_tiles": fst["frontier_tiles"], "frontier_slots": fst["frontier_slots"],
                      "kernel_avg_ms": avg, "roofline": roof})
         if N == sweep[-1] and args.cpu_seconds > 0:
             # CPU restatement, integrate only: its frontier pass over 2^32

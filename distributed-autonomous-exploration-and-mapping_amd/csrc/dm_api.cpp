@@ -485,6 +485,8 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     // workspaces wait for the pass's readback event: 179-183 x 10^9)
     g->fe_gate = !dm_env_off("DM_FE_GATE");
     g->pass_gate = dm_env_on("DM_PASS_GATE");
+    if (const char* ag = getenv("DM_ACCUM_GRID")) g->accum_grid = std::max(1, atoi(ag));
+    if (const char* ct = getenv("DM_CHUNK_THREADS")) g->chunk_threads_per_cu = std::max(1, atoi(ct));
     // launch batching into graphs (dm_batch.h) only with DM_GRAPHS=1: measured
     // neutral to slightly slower at C3
     g->batch.enabled = dm_env_on("DM_GRAPHS");

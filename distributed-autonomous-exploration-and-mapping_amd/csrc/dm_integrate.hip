@@ -1159,7 +1159,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   // heavy chunks and medium tiles first (the long items), then the light
   // tiles; k_heavy_apply then applies the heavy tiles' merged slabs
   dm_timer_begin(g, "tile_accum", &t);
-  DM_LAUNCH(k_tile_accum, dim3(grid_for(g->hitem_cap + g->act_cap, 1, 16384)),
+  DM_LAUNCH(k_tile_accum, dim3(grid_for(g->hitem_cap + g->act_cap, 1, g->accum_grid)),
                      dim3(kQuarter), 0,
                      g->stream, ge, make_apply(g), w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS,
                      w.pieces, w.tile_count, g->tile_free, w.slabs, g->L, g->state, w.cnt, w.sh, vec_ok,

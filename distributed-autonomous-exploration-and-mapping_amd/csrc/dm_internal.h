@@ -336,6 +336,11 @@ struct dm_grid {
   // kernel, 2 always the 256-thread kernel (DM_FRONTIER_KERNEL=auto|wave|wg,
   // read at dm_create, for A/B measurements; all three are exact)
   int frontier_kernel = 0;
+  // k_tile_accum's largest grid (DM_ACCUM_GRID, A/B; the kernel grid-strides)
+  int accum_grid = 16384;
+  // beams are split into k-ranges below this many threads per CU
+  // (dm_integrate_chunks; DM_CHUNK_THREADS, A/B)
+  int chunk_threads_per_cu = 512;
 
   // cross-band merge workspace (dm_merge.hip), sized nranks * rec_cap
   int64_t m_cap = 0;
@@ -421,7 +426,7 @@ inline hipError_t dm_join_pass_stream(dm_grid* g) {
 // thread per beam would walk up to 2*nmax/64 pieces serially on a mostly
 // idle GPU (sparse scans, 1 cm maps).  Chunks stay >= 64 steps long.
 inline int32_t dm_integrate_chunks(const dm_grid* g, int64_t nb) {
-  const int64_t want = 512 * (int64_t)(g->n_cu > 0 ? g->n_cu : 256);
+  const int64_t want = (int64_t)g->chunk_threads_per_cu * (int64_t)(g->n_cu > 0 ? g->n_cu : 256);
   if (nb <= 0 || nb >= want) return 1;
   const int64_t by_len = (g->nmax + 1) / 64 > 1 ? (g->nmax + 1) / 64 : 1;
   const int64_t by_fill = (want + nb - 1) / nb;
