@@ -487,6 +487,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     g->pass_gate = dm_env_on("DM_PASS_GATE");
     if (const char* ag = getenv("DM_ACCUM_GRID")) g->accum_grid = std::max(1, atoi(ag));
     if (const char* ct = getenv("DM_CHUNK_THREADS")) g->chunk_threads_per_cu = std::max(1, atoi(ct));
+    if (const char* sp = getenv("DM_SPARSE_PIECES")) g->sparse_pieces = std::max(0, atoi(sp));
     // launch batching into graphs (dm_batch.h) only with DM_GRAPHS=1: measured
     // neutral to slightly slower at C3
     g->batch.enabled = dm_env_on("DM_GRAPHS");
@@ -767,7 +768,7 @@ int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out) {
   if ((rc = read_counters(g))) return rc;
   const unsigned long long* fs = g->h_sh + kShards * kShardWords;
   const unsigned long long* ic = g->h_cnt + CNT_N;  // the last integrate call's counters
-  const uint64_t items = ic[CNT_ITEMS] + ic[CNT_LITEMS];  // heavy + light work items
+  const uint64_t items = ic[CNT_ITEMS] + ic[CNT_LITEMS] + ic[CNT_SITEMS];  // heavy + light + sparse items
   const uint64_t v[14] = {dm_shard_sum(g->h_sh, SH_U),  dm_shard_sum(g->h_sh, SH_T),
                           dm_shard_sum(g->h_sh, SH_TH), ic[CNT_SEGS],
                           ic[CNT_ACTIVE],               items,

@@ -14,13 +14,15 @@
 // log-odds update to the tile's cells in one coalesced read-modify-write of L
 // and state.  Integer counts make the result independent of atomic order.
 //
-//   k_beam_prep   one thread per beam: endpoint cells (double, no FMA),
-//                 Bresenham params, per-tile piece counts (wave-aggregated
-//                 atomics), first-touch list of active tiles
-//   k_scan_active one workgroup: exclusive scan of piece counts
-//   k_scatter     one thread per beam: pieces -> per-tile bins
-//   k_tile_apply  one workgroup per active tile (grid-stride): LDS counts +
-//                 fused apply, tile summaries, counter reset
+//   k_beam_prep   one thread per beam (or beam chunk): endpoint cells (double,
+//                 no FMA), Bresenham params, per-block LDS histogram of pieces
+//                 per tile -> tile_count, first-touch lists of active tiles
+//   k_plan        one thread per active tile: its bin and work items by
+//                 wave-aggregated bumps
+//   k_scatter     one thread per beam: pieces -> per-tile bins (packed)
+//   k_tile_accum  one workgroup per work item: LDS counts + fused apply;
+//                 heavy tiles merged in slabs, sparse tiles load only the
+//                 cells they touch
 #include "dm_internal.h"
 #include "dm_phase.h"
 
@@ -39,6 +41,8 @@ struct Geom {
   int64_t hitem_cap, heavy_cap;  // capacities of hitems / heavy_list (k_plan clamps its writes)
   int64_t nb;  // beams in this call
   int32_t chunks, chunk_len;  // each beam enumerated as `chunks` k-ranges (dm_integrate_chunks)
+  int32_t sparse_pieces;  // light tiles with at most this many pieces are sparse items
+  int32_t pad;
 };
 
 // Thread v of k_beam_prep / k_scatter: beam v % nb, k-range v / nb (chunk-
@@ -230,7 +234,7 @@ __device__ inline unsigned long long wave_alloc(unsigned long long* counter, uns
 // scan: bin order does not matter, so each tile's bin (its pieces' range in
 // `pieces`) and its work items are bump-allocated with wave-aggregated
 // atomics (wave_alloc).  Writes k_scatter's bin cursor per tile and the
-// items; counters: pieces, heavy + medium items, light items, heavy tiles.
+// items; counters: pieces, heavy + medium items, light items, sparse items, heavy tiles.
 __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __restrict__ act_raw,
                                                        const unsigned long long* __restrict__ ish,
                                                        int32_t* __restrict__ tile_cur,
@@ -268,23 +272,30 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __
     }
     const bool heavy = c > kMedium;
     const bool medium = c > kChunk && !heavy;
-    const bool light = t >= 0 && c <= kChunk;
+    const bool sparse = t >= 0 && c <= g.sparse_pieces;
+    const bool light = t >= 0 && c <= kChunk && !sparse;
     const int32_t nh_items = heavy ? (c + kChunk - 1) / kChunk : (medium ? 1 : 0);
     const unsigned long long p0 = wave_alloc(&cnt[CNT_SEGS], (unsigned long long)c);
     const unsigned long long hi = wave_alloc(&cnt[CNT_ITEMS], (unsigned long long)nh_items);
     const unsigned long long li = wave_alloc(&cnt[CNT_LITEMS], light ? 1ull : 0ull);
+    const unsigned long long si = wave_alloc(&cnt[CNT_SITEMS], sparse ? 1ull : 0ull);
     const unsigned long long ho = wave_alloc(&cnt[CNT_HEAVY], heavy ? 1ull : 0ull);
     if (t < 0) continue;
     tile_cur[t] = (int32_t)p0;  // k_scatter's cursor: the tile's bin start
     // the host sizes every list for the worst case (grow_integrate); a write
     // past a capacity anyway is flagged (DM_ERR_CAPACITY) and dropped
+    // light items fill litems from the bottom, sparse ones from the top: a
+    // tile is one or the other, so the two never meet below act_cap tiles
     const bool fits = (int64_t)(p0 + c) <= g.seg_cap && (int64_t)(hi + nh_items) <= g.hitem_cap &&
-                      (int64_t)li < (int64_t)g.act_cap && (int64_t)ho < g.heavy_cap;
+                      (int64_t)li < (int64_t)g.act_cap && (int64_t)si < (int64_t)g.act_cap &&
+                      (int64_t)ho < g.heavy_cap;
     if (!fits) {
       atomicOr(&cnt[CNT_IOVERFLOW], 4ull);
       continue;
     }
-    if (light) {
+    if (sparse) {
+      litems[(int64_t)g.act_cap - 1 - (int64_t)si] = make_int4(t, (int32_t)p0, c, -1);
+    } else if (light) {
       litems[li] = make_int4(t, (int32_t)p0, c, -1);
     } else if (medium) {  // one item, walked in rounds of kChunk, applied directly
       hitems[hi] = make_int4(t, (int32_t)p0, c, -1);
@@ -439,6 +450,28 @@ struct CellRows {
       const int64_t base = (vec && y < g.r.R) ? (int64_t)y * g.r.W + tx0 + cx : 0;
       l[rr] = *reinterpret_cast<const float4*>(L + base);
       s[rr] = *reinterpret_cast<const char4*>(state + base);
+    }
+  }
+
+  // Sparse items: after the walk, load only the 4-cell groups that have a
+  // count (touched(ly) for this thread's group of row ly); the apply skips
+  // the others, so a tile crossed by a ray or two does not read its 20 KB of
+  // L and state.
+  template <class Touched>
+  __device__ void load_touched(const Geom& g, int32_t tx0, int32_t ty0, int ly0, int dly, int cx,
+                               const float* __restrict__ L, const int8_t* __restrict__ state, int vec_ok,
+                               Touched&& touched) {
+    vec = vec_ok && tx0 + cx + 4 <= g.r.W;
+#pragma unroll
+    for (int rr = 0; rr < ROWS; ++rr) {
+      const int32_t y = ty0 + ly0 + rr * dly;
+      l[rr] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      s[rr] = make_char4(0, 0, 0, 0);
+      if (vec && y < g.r.R && touched(ly0 + rr * dly)) {
+        const int64_t base = (int64_t)y * g.r.W + tx0 + cx;
+        l[rr] = *reinterpret_cast<const float4*>(L + base);
+        s[rr] = *reinterpret_cast<const char4*>(state + base);
+      }
     }
   }
 
@@ -667,7 +700,7 @@ __device__ inline void heavy_quarter(const Geom& g, const ApplyArgs& p, int64_t 
 constexpr int kAccumPerCu = DM_ACCUM_OCC;  // resident k_tile_accum workgroups per CU (4 waves each)
 __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     Geom g, ApplyArgs p, const int4* __restrict__ list_a, int cnt_a, const int4* __restrict__ list_b,
-    int cnt_b, const PackedPiece* __restrict__ pieces, int32_t* tile_count, int32_t* tile_free,
+    int cnt_b, int cnt_c, const PackedPiece* __restrict__ pieces, int32_t* tile_count, int32_t* tile_free,
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
     const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok,
     const int32_t* __restrict__ heavy_list, int32_t* heavy_done, const unsigned long long* __restrict__ halt) {
@@ -682,8 +715,10 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
   const int64_t HI = min((int64_t)cnt[cnt_a], g.hitem_cap);
   const int64_t LI = cnt_b >= 0 ? min((int64_t)cnt[cnt_b], (int64_t)g.act_cap) : 0;
   const int64_t n_items = HI + LI;
+  // sparse items (litems from the top, cnt_c of them): a second loop
+  const int64_t SI = cnt_c >= 0 ? min((int64_t)cnt[cnt_c], (int64_t)g.act_cap) : 0;
   const int64_t G = gridDim.x;
-  if ((int64_t)blockIdx.x >= n_items) return;
+  if ((int64_t)blockIdx.x >= n_items && (int64_t)blockIdx.x >= SI) return;
   auto item_of = [&](int64_t it) {
     int4 d = it < n_items ? (it < HI ? list_a[it] : list_b[it - HI]) : make_int4(0, 0, 0, -1);
     // an item never reads past the piece array (k_plan keeps p0 + c <= seg_cap)
@@ -839,6 +874,55 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; }
     __syncthreads();
   }
+  // Sparse items (a few pieces: C5's sparse scans on a 1 cm map): walk first,
+  // then load and apply only the touched 4-cell groups.  A loop of its own
+  // (after the dense items), so none of its registers are live across the
+  // dense walk.  The LDS tile is zero here: every dense item clears it.
+  for (int64_t it = blockIdx.x; it < SI; it += G) {
+    int4 d = list_b[(int64_t)g.act_cap - 1 - it];
+    d.z = (int64_t)d.y + d.z <= g.seg_cap ? d.z : 0;  // never past the piece array
+    const int32_t tile = __builtin_amdgcn_readfirstlane(d.x);
+    const int32_t c0 = __builtin_amdgcn_readfirstlane(d.y);
+    const int32_t c = __builtin_amdgcn_readfirstlane(d.z);
+    const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
+    const PackedPiece sp = tid < c ? pieces[c0 + tid] : no_piece();
+    const int32_t sfree = tile_free[tile];
+    int32_t u = walk_piece_plain(tl, sp, tid < c, lane);
+    const bool inside = tx0 + DM_TS <= g.r.W && ty0 + DM_TS <= g.r.R;  // workgroup-uniform
+    if (inside) {
+      for (int o = 32; o > 0; o >>= 1) u += __shfl_xor(u, o);
+      if (lane == 0) atomicAdd(&s_U, (uint32_t)u);
+    }
+    __syncthreads();
+    DM_PH(dm_phase_acc_integrate, 6);
+    CellRows<4> sc;
+    sc.load_touched(g, tx0, ty0, tid >> 4, 16, cx, L, state, vec_ok, [&](int ly) {
+      const uint32_t* w = tl + ly * kLdsPitch + cx;
+      return (w[0] | w[1] | w[2] | w[3]) != 0u;
+    });
+    sc.apply(g, p, tx0, ty0, tid >> 4, 16, cx, L, state,
+             [&](int ly, uint32_t* h4, uint32_t* m4) {
+               for (int e = 0; e < 4; ++e) {
+                 const uint32_t v = tl[ly * kLdsPitch + cx + e];
+                 h4[e] = v >> 16;
+                 m4[e] = v & 0xFFFFu;
+               }
+             },
+             &s_T, &s_free, inside ? nullptr : &s_U);
+    DM_PH(dm_phase_acc_integrate, 7);
+    DM_PH_COUNT(dm_phase_acc_integrate, 21, 1);
+    DM_PH_COUNT(dm_phase_acc_integrate, 22, c);
+    __syncthreads();
+    if (tid == 0) {
+      s_accT += (unsigned long long)s_T;
+      s_accU += (unsigned long long)s_U;
+      if (s_free) tile_free[tile] = sfree + s_free;
+      tile_count[tile] = 0;  // ready for the next call
+      s_T = 0; s_free = 0; s_U = 0u;
+    }
+    for (int e = tid; e < kTileWords; e += kQuarter) tl[e] = 0u;
+    __syncthreads();
+  }
   if (tid == 0) {
     unsigned long long* sh = ish + (blockIdx.x % kShards) * kShardWords;
     if (s_accT) atomicAdd(&sh[SH_T], s_accT);
@@ -975,16 +1059,20 @@ __global__ __launch_bounds__(256) void k_recount(Geom g, const int8_t* __restric
 // registers are full at 7 workgroups per CU (inside it, every variant
 // measured 6-14 us slower per call).
 __global__ __launch_bounds__(256) void k_fmask_items(Geom g, const int4* __restrict__ list_a, int cnt_a,
-                                                     const int4* __restrict__ list_b, int cnt_b,
+                                                     const int4* __restrict__ list_b, int cnt_b, int cnt_c,
                                                      const unsigned long long* __restrict__ cnt,
                                                      const int8_t* __restrict__ state, uint8_t* __restrict__ fmask,
                                                      const unsigned long long* __restrict__ halt) {
   if (*halt) return;  // as k_tile_accum
   const int64_t HI = min((int64_t)cnt[cnt_a], g.hitem_cap);
   const int64_t LI = min((int64_t)cnt[cnt_b], (int64_t)g.act_cap);
+  const int64_t SI = min((int64_t)cnt[cnt_c], (int64_t)g.act_cap);  // sparse: list_b from the top
   const int lane = __lane_id();
-  for (int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); it < HI + LI; it += (int64_t)gridDim.x * 4) {
-    const int32_t tile = __builtin_amdgcn_readfirstlane(it < HI ? list_a[it].x : list_b[it - HI].x);
+  for (int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); it < HI + LI + SI;
+       it += (int64_t)gridDim.x * 4) {
+    const int32_t tile = __builtin_amdgcn_readfirstlane(
+        it < HI ? list_a[it].x
+                : (it < HI + LI ? list_b[it - HI].x : list_b[(int64_t)g.act_cap - 1 - (it - HI - LI)].x));
     const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
     const int32_t x0 = tx0 + (lane & 3) * 16;
     uint8_t* tm = fmask + (int64_t)tile * (DM_TS * 16);
@@ -1040,7 +1128,7 @@ __global__ __launch_bounds__(256) void k_map_image(int64_t R, int64_t W, const i
   }
 }
 
-static_assert(sizeof(Geom) == 64 && sizeof(RayArgs) == 40 && sizeof(ApplyArgs) == 24,
+static_assert(sizeof(Geom) == 72 && sizeof(RayArgs) == 40 && sizeof(ApplyArgs) == 24,
               "kernel argument structs have no implicit padding (dm_batch.h cache keys)");
 
 Geom make_geom(const dm_grid* g) {
@@ -1057,6 +1145,8 @@ Geom make_geom(const dm_grid* g) {
   ge.nb = 0;
   ge.chunks = 1;
   ge.chunk_len = 0;
+  ge.sparse_pieces = g->sparse_pieces;
+  ge.pad = 0;
   return ge;
 }
 
@@ -1162,7 +1252,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   DM_LAUNCH(k_tile_accum, dim3(grid_for(g->hitem_cap + g->act_cap, 1, g->accum_grid)),
                      dim3(kQuarter), 0,
                      g->stream, ge, make_apply(g), w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS,
-                     w.pieces, w.tile_count, g->tile_free, w.slabs, g->L, g->state, w.cnt, w.sh, vec_ok,
+                     (int)CNT_SITEMS, w.pieces, w.tile_count, g->tile_free, w.slabs, g->L, g->state, w.cnt, w.sh, vec_ok,
                      w.heavy_list, g->fuse_heavy ? w.heavy_done : nullptr, g->fe_flag + kHaltWord);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
@@ -1189,7 +1279,8 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   }
   dm_timer_begin(g, "fmask", &t);
   DM_LAUNCH(k_fmask_items, dim3(grid_for(g->hitem_cap + g->act_cap, 4, 8192)), dim3(256), 0, g->stream,
-                     ge, w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS, w.cnt, g->state, g->fmask,
+                     ge, w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS, (int)CNT_SITEMS, w.cnt,
+                     g->state, g->fmask,
                      g->fe_flag + kHaltWord);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());

@@ -43,7 +43,8 @@ enum {
   CNT_LITEMS = 14,  // light work items (= light tiles)
   CNT_IOVERFLOW = 15,  // integrate capacity overflow flags (1 first-touch list, 2 pieces, 4 work lists)
   CNT_BIG = 16,     // frontier tiles with more runs than a tile-wave holds (big-tile list length)
-  CNT_N = 17
+  CNT_SITEMS = 17,  // sparse light work items (<= sparse_pieces pieces; stored from the top of litems)
+  CNT_N = 18
 };
 // CNT_OVERFLOW bits of a frontier pass
 constexpr unsigned long long kOvSlots = 4ull;      // a slot shard region overflowed
@@ -67,7 +68,7 @@ constexpr int kStampWord = 8;  // bits_flag: the last frontier pass's stamp (k_f
 // frontier pass, which may still be running when the next call's front-end
 // starts (dm_set_overlap), so the integrate reset never touches them.
 constexpr int kIntegrateCounters[] = {CNT_ACTIVE, CNT_U, CNT_T, CNT_SEGS, CNT_ITEMS,
-                                      CNT_HEAVY, CNT_TH, CNT_LITEMS, CNT_IOVERFLOW};
+                                      CNT_HEAVY, CNT_TH, CNT_LITEMS, CNT_IOVERFLOW, CNT_SITEMS};
 
 // k_plan's work-item classes (dm_integrate.hip): tiles with more pieces than
 // kIntegrateChunk are split into items of kIntegrateChunk pieces, tiles with
@@ -341,6 +342,9 @@ struct dm_grid {
   // beams are split into k-ranges below this many threads per CU
   // (dm_integrate_chunks; DM_CHUNK_THREADS, A/B)
   int chunk_threads_per_cu = 512;
+  // light tiles with at most this many pieces are sparse work items: walked
+  // first, then only their touched cells are loaded (DM_SPARSE_PIECES, A/B)
+  int sparse_pieces = 8;
 
   // cross-band merge workspace (dm_merge.hip), sized nranks * rec_cap
   int64_t m_cap = 0;

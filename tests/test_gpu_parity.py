@@ -415,3 +415,25 @@ def test_heavy_ticket_under_uneven_load(oracle_lib):
             np.testing.assert_array_equal(m.logodds().view(np.uint32), om.L.view(np.uint32))
         torch.cuda.synchronize()
         assert_map_equal(m, om)
+
+
+@pytest.mark.parametrize("sparse", ["0", "8", "256"])
+def test_sparse_items_threshold(oracle_lib, monkeypatch, sparse):
+    """Light tiles with at most DM_SPARSE_PIECES pieces are sparse items
+    (walk first, then load only the touched cells; listed from the top of the
+    light list).  0: none, 256: every light tile.  1 cm map with few beams per
+    scan (C5's sparse end) and ragged edge tiles; fmask records forced on so
+    k_fmask_items covers the sparse range too."""
+    monkeypatch.setenv("DM_SPARSE_PIECES", sparse)
+    monkeypatch.setenv("DM_FMASK", "on")
+    for W, H, S, N, res, seed in [(1000, 900, 16, 12, 0.01, 41), (130, 70, 5, 64, 0.05, 42),
+                                  (2050, 1030, 32, 48, 0.01, 43)]:
+        p = cases.make_params(W, H, resolution=res)
+        om = oracle_lib.OracleMap(p)
+        with dm.OccupancyMapper(p) as m:
+            for k in range(4):
+                poses, ranges, amin, inc = cases.random_scans(seed * 100 + k, p, S, N)
+                assert m.integrate(poses, ranges, amin, inc) == om.integrate(poses, ranges, amin, inc)
+            assert_map_equal(m, om)
+            fr = m.frontiers(want_mask=True, want_labels=True)
+            assert_frontiers_equal(fr, *om.frontiers())

@@ -30,8 +30,8 @@ NAMES = {
               16: "#tiles", 17: "#tiles with F", 18: "#runs"},
     "integrate": {0: "item setup (pieces, prefetch)", 1: "heavy accum", 2: "heavy slab flush",
                   3: "light accum", 5: "light: wait for cell loads", 4: "light apply", 8: "heavy_apply loads", 9: "heavy_apply apply", 10: "heavy_apply finish", 11: "plan: shard offsets",
-                  12: "plan: list loads", 13: "plan: scans", 14: "plan: writes", 16: "#light items",
-                  17: "#heavy items", 18: "#light pieces", 19: "#heavy pieces", 20: "#heavy tiles applied"},
+                  12: "plan: list loads", 13: "plan: scans", 14: "plan: writes", 6: "sparse walk", 7: "sparse load + apply", 16: "#light items",
+                  17: "#heavy items", 18: "#light pieces", 19: "#heavy pieces", 20: "#heavy tiles applied", 21: "#sparse items", 22: "#sparse pieces"},
 }
 
 
