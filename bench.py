@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--depth", type=int, default=2,
                     help="frontier passes in flight in the pipelined steps (1 or 2; libdm keeps 2 readback slots)")
+    ap.add_argument("--order", default="eb", choices=["eb", "be"],
+                    help="host order per pipelined step after integrate(k): 'eb' collects pass "
+                         "k-depth then starts pass k; 'be' starts pass k then collects pass "
+                         "k-depth (depth + 1 passes in flight)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the steps back to back without overlapping step k+1's integrate "
                          "front-end with step k's frontier pass")
@@ -210,6 +214,11 @@ def main():
             if marks is not None:
                 marks.append(time.perf_counter())
             integ(k0 + k)
+            if args.order == "be":
+                mapper.frontiers_begin()
+                if k >= depth:
+                    mapper.frontiers_end()
+                continue
             if k >= depth:
                 mapper.frontiers_end()
             mapper.frontiers_begin()

@@ -493,15 +493,21 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
 constexpr int kFW = 4;            // tile-waves per workgroup
 constexpr int64_t kDenseRuns = 48;  // runs per frontier tile above which a pass is "dense"
 constexpr int64_t kDenseMaxTiles = 4096;  // ... if it has at most this many tiles with frontier cells
+// 384 runs (18.7 KB of LDS per 4-wave workgroup) lets 7 workgroups share a
+// CU (<= 72 VGPRs): at C5's sparse scans the pass is 28 tile-waves per CU of
+// latency chains, not bytes, so occupancy is what moves it (r02 A/B,
+// profiles/r02_frontier_occupancy_ab.log: C5 48 beams k_frontier_tile 165 ->
+// 135 us, 192 beams tile + big 369 -> 350 us; 256 runs sends too many 1 cm
+// tiles to k_frontier_tile_big, 512 runs fits only 6 workgroups)
 #ifndef DM_FL_RUNS
-#define DM_FL_RUNS 512
+#define DM_FL_RUNS 384
 #endif
 constexpr int kRunsFast = DM_FL_RUNS;  // runs a tile-wave keeps in LDS
 #ifndef DM_FL_STRIDED
 #define DM_FL_STRIDED 0
 #endif
 #ifndef DM_FL_OCC
-#define DM_FL_OCC 6               // workgroups per CU (LDS 24.3 KB each, <= 80 VGPRs)
+#define DM_FL_OCC 7               // workgroups per CU (LDS 18.7 KB each, <= 72 VGPRs)
 #endif
 
 // Orders this wave's LDS accesses across lanes (LDS executes one wave's
