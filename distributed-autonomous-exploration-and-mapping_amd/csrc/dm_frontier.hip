@@ -57,6 +57,8 @@ struct FGeom {
   int64_t min_size;
 };
 
+constexpr int kPrepIters = 16;  // k_frontier_prep: 256-tile rows per workgroup chunk
+
 // Per-call preparation in one launch: reset the frontier counters, slot
 // shards and edge slots, and list the tiles holding >= 1 free cell (only
 // free cells can be frontier cells; tile_free is maintained by the
@@ -71,7 +73,7 @@ __global__ __launch_bounds__(256) void k_frontier_prep(int64_t NT, const int32_t
                                                        int32_t* __restrict__ edge_slot,
                                                        int32_t* __restrict__ slot_parent, int64_t slot_cap,
                                                        const unsigned long long* __restrict__ halt,
-                                                       unsigned long long* stamp_word) {
+                                                       unsigned long long* stamp_word, int iters) {
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int lane = __lane_id();
@@ -91,25 +93,47 @@ __global__ __launch_bounds__(256) void k_frontier_prep(int64_t NT, const int32_t
   // kernel's in-kernel unions: their CASes and (possibly stale, L2-served)
   // finds then only ever see a slot as a root or as hooked (dm_uf.h)
   for (int64_t i = i0; i < slot_cap; i += stride) slot_parent[i] = (int32_t)i;
-  // ballot compaction, one list_n atomic per workgroup and round (the
-  // loop bound is uniform within the workgroup: its barriers are safe)
-  __shared__ int32_t s_wn[4];
+  // ballot compaction over a contiguous chunk of `iters` x 256 tiles per
+  // workgroup and round, ONE list_n atomic per chunk: every workgroup with a
+  // listed tile bumps the same word, and those memory-side atomics
+  // serialise (a 1 M-tile C5 map took 29 us over 4096 one-row chunks; the
+  // host picks iters so there are ~256 chunks: 1 at C3, 16 at C5); each
+  // thread keeps its tiles' bits between the count and the placement (the
+  // loop bounds are uniform within the workgroup: its barriers are safe)
+  __shared__ int32_t s_wn[kPrepIters][4];
   __shared__ unsigned long long s_base;
   const int w = threadIdx.x >> 6;
-  for (int64_t b0 = (int64_t)blockIdx.x * blockDim.x; b0 < NT; b0 += stride) {
-    const int64_t t = b0 + threadIdx.x;
-    const bool f = t < NT && tile_free[t] > 0;
-    const unsigned long long bal = __ballot(f);
-    if (lane == 0) s_wn[w] = __popcll(bal);
-    __syncthreads();
-    int before = 0, total = 0;
-    for (int q = 0; q < 4; ++q) {
-      before += q < w ? s_wn[q] : 0;
-      total += s_wn[q];
+  const int64_t chunk = (int64_t)iters * blockDim.x;
+  for (int64_t c0 = (int64_t)blockIdx.x * chunk; c0 < NT; c0 += (int64_t)gridDim.x * chunk) {
+    // this thread's tiles of the chunk as a bit mask (the ballots' own bits)
+    uint32_t mine = 0u;
+#pragma unroll 4
+    for (int i = 0; i < iters; ++i) {  // loads first (several in flight), ballots after
+      const int64_t t = c0 + (int64_t)i * blockDim.x + threadIdx.x;
+      mine |= (t < NT && tile_free[t] > 0 ? 1u : 0u) << i;
     }
-    if (threadIdx.x == 0 && total) s_base = atomicAdd(list_n, (unsigned long long)total);
+    for (int i = 0; i < iters; ++i) {
+      const unsigned long long bal = __ballot((mine >> i) & 1u);
+      if (lane == 0) s_wn[i][w] = __popcll(bal);
+    }
     __syncthreads();
-    if (f) ftiles[s_base + before + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)t;
+    if (threadIdx.x == 0) {
+      int total = 0;
+      for (int i = 0; i < iters; ++i) total += s_wn[i][0] + s_wn[i][1] + s_wn[i][2] + s_wn[i][3];
+      s_base = total ? atomicAdd(list_n, (unsigned long long)total) : 0ull;
+    }
+    __syncthreads();
+    int64_t pre = (int64_t)s_base;
+    for (int i = 0; i < iters; ++i) {
+      const bool f = (mine >> i) & 1u;
+      const unsigned long long bal = __ballot(f);
+      int before = 0;
+      for (int q = 0; q < w; ++q) before += s_wn[i][q];
+      if (f)
+        ftiles[pre + before + __popcll(bal & ((1ull << lane) - 1ull))] =
+            (int32_t)(c0 + (int64_t)i * blockDim.x + threadIdx.x);
+      pre += s_wn[i][0] + s_wn[i][1] + s_wn[i][2] + s_wn[i][3];
+    }
     __syncthreads();  // s_wn / s_base are rewritten next round
   }
 }
@@ -1543,10 +1567,12 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   unsigned long long* zero_n = g->fl_n + 16 * ((g->fr_pass + 1) % 3);  // last used by pass fr_pass - 2
   KernelTimer t;
   dm_timer_begin(g, "frontier_prep", &t);
-  DM_LAUNCH(k_frontier_prep, dim3(grid_for(std::max<int64_t>(std::max<int64_t>(g->NT, 2 * g->W), kShards * kShardWords), 256, 1024)), dim3(256), 0,
+  // ~256 chunks of prep_iters x 256 tiles, at least 256 workgroups for the resets
+  const int prep_iters = (int)std::min<int64_t>(kPrepIters, std::max<int64_t>(1, (g->NT + 65535) / 65536));
+  DM_LAUNCH(k_frontier_prep, dim3(grid_for(std::max<int64_t>((g->NT + prep_iters - 1) / prep_iters, 256 * 256), 256, 1024)), dim3(256), 0,
                      g->stream, g->NT, g->tile_free, g->ftiles, list_n, zero_n, 2 * g->W, g->cnt, g->fsh,
                      g->edge_slot, g->slot_parent, g->slot_cap, g->fe_flag + kHaltWord,
-                     g->bits_flag + kStampWord);
+                     g->bits_flag + kStampWord, prep_iters);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (want_mask || want_labels) DM_HIP(dm_batch_flush_all());

@@ -96,9 +96,22 @@ def test_bucket_sort_merge(oracle_lib, P):
         rec_cap = 1 << 17
         nb = bands[0].export_bytes(rec_cap)
         g = torch.zeros(P * nb, dtype=torch.uint8, device="cuda:0")
-        for r, b in enumerate(bands):
-            b.frontiers_export_device(g.data_ptr() + r * nb, rec_cap)
-            b.synchronize()
+
+        def export_all():
+            for r, b in enumerate(bands):
+                b.frontiers_export_device(g.data_ptr() + r * nb, rec_cap)
+                b.synchronize()
+
+        export_all()
+        # ~52 k tile-local components per band against the initial 65 536
+        # slots in 32 shard regions: which tiles share a region depends on
+        # the order the big-tile kernel takes them, so a region can overflow
+        # (flag 1, no result).  dm/sharded.py then falls back to the bands'
+        # synchronous passes, which grow the slot arrays: the same here.
+        if bands[0].merge_bands(g.data_ptr(), P, rec_cap, 1)[0] is None:
+            for b in bands:
+                b.frontiers()
+            export_all()
         for _ in range(3):
             got, _ = bands[0].merge_bands(g.data_ptr(), P, rec_cap, 1)
             np.testing.assert_array_equal(got, exp)
