@@ -593,6 +593,38 @@ __device__ inline int32_t walk_piece_plain(uint32_t* tl, const PackedPiece& mine
   return len;
 }
 
+// Sparse items: the same walk into a byte-packed count tile (pitch 64, one
+// byte per cell: hits << 4 | misses, +1 per cell and +0x0F at the hit cell,
+// which turns that miss into a hit).  A cell of a tile with at most 15
+// pieces is visited at most 15 times, so the final byte 16·hits + misses is
+// at most 255 and no partial sum carries into the next cell.
+constexpr int kSparseMax = 15;
+
+__device__ inline int32_t to_pitch64(int32_t a) {  // pitch-65 address or step -> pitch 64
+  return a >= 0 ? a - a / kLdsPitch : -((-a) - (-a) / kLdsPitch);
+}
+
+__device__ inline int32_t walk_piece_bytes(uint32_t* tq, const PackedPiece& mine, bool valid) {
+  TilePiece tp = dm_unpack_piece(mine.x, mine.y, mine.z, mine.w);
+  const int32_t len = valid ? tp.len : 0;
+  int32_t wl = len;
+  for (int o = 32; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o));
+  tp.addr0 = to_pitch64(tp.addr0);
+  tp.da = to_pitch64(tp.da);
+  tp.db = to_pitch64(tp.db);
+  PieceCursor cur;
+  cur.init(tp);
+  for (int32_t st = 0; st < wl; ++st) {
+    if (st < len) atomicAdd(&tq[cur.addr >> 2], 1u << (8 * (cur.addr & 3)));
+    cur.step(tp);
+  }
+  if (len > 0 && tp.addr_end >= 0) {
+    const int32_t e = to_pitch64(tp.addr_end);
+    atomicAdd(&tq[e >> 2], 0x0Fu << (8 * (e & 3)));
+  }
+  return len;
+}
+
 __device__ inline PackedPiece no_piece() {
   PackedPiece q;
   q.x = 0u; q.y = 0u; q.z = 0u; q.w = 1u;
@@ -718,7 +750,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
   // sparse items (litems from the top, cnt_c of them): a second loop
   const int64_t SI = cnt_c >= 0 ? min((int64_t)cnt[cnt_c], (int64_t)g.act_cap) : 0;
   const int64_t G = gridDim.x;
-  if ((int64_t)blockIdx.x >= n_items && (int64_t)blockIdx.x >= SI) return;
+  if ((int64_t)blockIdx.x >= n_items && 2 * (int64_t)blockIdx.x >= SI) return;
   auto item_of = [&](int64_t it) {
     int4 d = it < n_items ? (it < HI ? list_a[it] : list_b[it - HI]) : make_int4(0, 0, 0, -1);
     // an item never reads past the piece array (k_plan keeps p0 + c <= seg_cap)
@@ -878,49 +910,64 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
   // then load and apply only the touched 4-cell groups.  A loop of its own
   // (after the dense items), so none of its registers are live across the
   // dense walk.  The LDS tile is zero here: every dense item clears it.
-  for (int64_t it = blockIdx.x; it < SI; it += G) {
-    int4 d = list_b[(int64_t)g.act_cap - 1 - it];
+  // Two sparse items per workgroup, one per 128-thread half: with at most
+  // kSparseMax pieces a cell is visited at most 15 times, so its counts fit
+  // one byte (hits << 4 | misses: walk_piece_bytes), a tile's counts 4 KiB,
+  // and both halves' tiles share the LDS of one dense count tile.
+  __shared__ int32_t s_hT[2], s_hfree[2];
+  __shared__ uint32_t s_hU[2];
+  const int half = tid >> 7, ht = tid & 127;
+  uint32_t* tq = tl + half * (DM_TS * DM_TS / 4);
+  const int hcx = (ht & 15) * 4;
+  if (tid < 2) { s_hT[tid] = 0; s_hfree[tid] = 0; s_hU[tid] = 0u; }
+  __syncthreads();
+  for (int64_t it2 = blockIdx.x; 2 * it2 < SI; it2 += G) {
+    const int64_t it = 2 * it2 + half;
+    const bool have = it < SI;  // uniform in each half
+    int4 d = have ? list_b[(int64_t)g.act_cap - 1 - it] : make_int4(0, 0, 0, 0);
     d.z = (int64_t)d.y + d.z <= g.seg_cap ? d.z : 0;  // never past the piece array
-    const int32_t tile = __builtin_amdgcn_readfirstlane(d.x);
-    const int32_t c0 = __builtin_amdgcn_readfirstlane(d.y);
-    const int32_t c = __builtin_amdgcn_readfirstlane(d.z);
+    const int32_t tile = d.x, c0 = d.y, c = d.z;
     const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
-    const PackedPiece sp = tid < c ? pieces[c0 + tid] : no_piece();
-    const int32_t sfree = tile_free[tile];
-    int32_t u = walk_piece_plain(tl, sp, tid < c, lane);
-    const bool inside = tx0 + DM_TS <= g.r.W && ty0 + DM_TS <= g.r.R;  // workgroup-uniform
+    const PackedPiece sp = ht < c ? pieces[c0 + ht] : no_piece();
+    const int32_t sfree = have ? tile_free[tile] : 0;
+    int32_t u = walk_piece_bytes(tq, sp, ht < c);
+    const bool inside = tx0 + DM_TS <= g.r.W && ty0 + DM_TS <= g.r.R;  // uniform in the half
     if (inside) {
       for (int o = 32; o > 0; o >>= 1) u += __shfl_xor(u, o);
-      if (lane == 0) atomicAdd(&s_U, (uint32_t)u);
+      if (lane == 0 && u) atomicAdd(&s_hU[half], (uint32_t)u);
     }
     __syncthreads();
     DM_PH(dm_phase_acc_integrate, 6);
-    CellRows<4> sc;
-    sc.load_touched(g, tx0, ty0, tid >> 4, 16, cx, L, state, vec_ok, [&](int ly) {
-      const uint32_t* w = tl + ly * kLdsPitch + cx;
-      return (w[0] | w[1] | w[2] | w[3]) != 0u;
-    });
-    sc.apply(g, p, tx0, ty0, tid >> 4, 16, cx, L, state,
-             [&](int ly, uint32_t* h4, uint32_t* m4) {
-               for (int e = 0; e < 4; ++e) {
-                 const uint32_t v = tl[ly * kLdsPitch + cx + e];
-                 h4[e] = v >> 16;
-                 m4[e] = v & 0xFFFFu;
-               }
-             },
-             &s_T, &s_free, inside ? nullptr : &s_U);
+    // the half's 128 threads cover the tile in two passes of 32 rows (a
+    // thread: one 4-cell group of rows ly0, ly0 + 8, ly0 + 16, ly0 + 24)
+    for (int pass = 0; pass < 2 && have; ++pass) {
+      const int ly0 = (ht >> 4) + 32 * pass;
+      CellRows<4> sc;
+      sc.load_touched(g, tx0, ty0, ly0, 8, hcx, L, state, vec_ok,
+                      [&](int ly) { return tq[ly * 16 + (hcx >> 2)] != 0u; });
+      sc.apply(g, p, tx0, ty0, ly0, 8, hcx, L, state,
+               [&](int ly, uint32_t* h4, uint32_t* m4) {
+                 const uint32_t w = tq[ly * 16 + (hcx >> 2)];
+                 for (int e = 0; e < 4; ++e) {
+                   const uint32_t v = (w >> (8 * e)) & 0xFFu;
+                   h4[e] = v >> 4;
+                   m4[e] = v & 0xFu;
+                 }
+               },
+               &s_hT[half], &s_hfree[half], inside ? nullptr : &s_hU[half]);
+    }
     DM_PH(dm_phase_acc_integrate, 7);
-    DM_PH_COUNT(dm_phase_acc_integrate, 21, 1);
+    DM_PH_COUNT(dm_phase_acc_integrate, 21, have ? 1 : 0);
     DM_PH_COUNT(dm_phase_acc_integrate, 22, c);
     __syncthreads();
-    if (tid == 0) {
-      s_accT += (unsigned long long)s_T;
-      s_accU += (unsigned long long)s_U;
-      if (s_free) tile_free[tile] = sfree + s_free;
+    if (ht == 0 && have) {
+      atomicAdd(&s_accT, (unsigned long long)s_hT[half]);
+      atomicAdd(&s_accU, (unsigned long long)s_hU[half]);
+      if (s_hfree[half]) tile_free[tile] = sfree + s_hfree[half];
       tile_count[tile] = 0;  // ready for the next call
-      s_T = 0; s_free = 0; s_U = 0u;
     }
-    for (int e = tid; e < kTileWords; e += kQuarter) tl[e] = 0u;
+    if (ht == 0) { s_hT[half] = 0; s_hfree[half] = 0; s_hU[half] = 0u; }
+    for (int e = ht; e < DM_TS * DM_TS / 4; e += 128) tq[e] = 0u;
     __syncthreads();
   }
   if (tid == 0) {
@@ -1145,7 +1192,7 @@ Geom make_geom(const dm_grid* g) {
   ge.nb = 0;
   ge.chunks = 1;
   ge.chunk_len = 0;
-  ge.sparse_pieces = g->sparse_pieces;
+  ge.sparse_pieces = std::min(g->sparse_pieces, kSparseMax);  // byte-packed counts (walk_piece_bytes)
   ge.pad = 0;
   return ge;
 }

@@ -417,11 +417,13 @@ def test_heavy_ticket_under_uneven_load(oracle_lib):
         assert_map_equal(m, om)
 
 
-@pytest.mark.parametrize("sparse", ["0", "8", "256"])
+@pytest.mark.parametrize("sparse", ["0", "8", "15", "256"])
 def test_sparse_items_threshold(oracle_lib, monkeypatch, sparse):
     """Light tiles with at most DM_SPARSE_PIECES pieces are sparse items
-    (walk first, then load only the touched cells; listed from the top of the
-    light list).  0: none, 256: every light tile.  1 cm map with few beams per
+    (two per workgroup, byte-packed counts; walk first, then load only the
+    touched cells; listed from the top of the light list).  0: none; the
+    library caps the threshold at 15 pieces (one byte of counts per cell), so
+    256 behaves as 15.  1 cm map with few beams per
     scan (C5's sparse end) and ragged edge tiles; fmask records forced on so
     k_fmask_items covers the sparse range too."""
     monkeypatch.setenv("DM_SPARSE_PIECES", sparse)
