@@ -344,7 +344,7 @@ struct dm_grid {
   int chunk_threads_per_cu = 512;
   // light tiles with at most this many pieces are sparse work items: walked
   // first, then only their touched cells are loaded (DM_SPARSE_PIECES, A/B)
-  int sparse_pieces = 8;
+  int sparse_pieces = 15;
 
   // cross-band merge workspace (dm_merge.hip), sized nranks * rec_cap
   int64_t m_cap = 0;
