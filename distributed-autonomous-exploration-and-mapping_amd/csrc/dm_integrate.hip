@@ -215,25 +215,47 @@ static_assert(kChunk == kQuarter, "one piece per thread");
 
 constexpr int kPlanThreads = 256;
 
-// Wave-aggregated bump allocation: every active lane gets v lane-exclusive
-// units from *counter; one atomic per wave (returns the wave's base).
-__device__ inline unsigned long long wave_alloc(unsigned long long* counter, unsigned long long v) {
+// Wave-aggregated bump allocation of K counters at once: every active lane
+// gets v[k] lane-exclusive units of counter k (out[k]: its first unit), with
+// ONE atomic instruction per wave for all K counters.
+template <int K>
+__device__ inline void wave_alloc_n(unsigned long long* const (&counter)[K], const unsigned long long (&v)[K],
+                                    unsigned long long (&out)[K]) {
   const int lane = __lane_id();
-  unsigned long long incl = v;
-  for (int d = 1; d < 64; d <<= 1) {
-    const unsigned long long t = __shfl_up(incl, d);
-    if (lane >= d) incl += t;
+  unsigned long long incl[K], total[K], base[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    incl[k] = v[k];
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long t = __shfl_up(incl[k], d);
+      if (lane >= d) incl[k] += t;
+    }
+    total[k] = __shfl(incl[k], 63);
+    base[k] = 0ull;
   }
-  const unsigned long long total = __shfl(incl, 63);
-  unsigned long long base = 0;
-  if (lane == 63 && total) base = atomicAdd(counter, total);
-  return __shfl(base, 63) + incl - v;
+  // lane 63 - k adds counter k's total: K lanes, K different addresses, ONE
+  // atomic instruction (a uniform-address atomic per counter would each be
+  // expanded by the compiler's atomic optimizer and waited for in turn)
+  const int kk = 63 - lane;
+  unsigned long long* addr = counter[0];
+  unsigned long long mine = 0ull;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (kk == k) { addr = counter[k]; mine = total[k]; }
+  unsigned long long got = 0ull;
+  if (kk < K) got = atomicAdd(addr, mine);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    base[k] = __shfl(got, 63 - k);
+    out[k] = base[k] + incl[k] - v[k];
+  }
 }
 
 // Work plan for the apply phase, one thread per active tile and no global
 // scan: bin order does not matter, so each tile's bin (its pieces' range in
 // `pieces`) and its work items are bump-allocated with wave-aggregated
-// atomics (wave_alloc).  Writes k_scatter's bin cursor per tile and the
+// atomics (wave_alloc_n: one round trip for all five counters; the former
+// one-call-per-counter form waited for each in turn, k_plan 9.8 -> 8.4 us at C3).  Writes k_scatter's bin cursor per tile and the
 // items; counters: pieces, heavy + medium items, light items, sparse items, heavy tiles.
 __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __restrict__ act_raw,
                                                        const unsigned long long* __restrict__ ish,
@@ -275,11 +297,13 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __
     const bool sparse = t >= 0 && c <= g.sparse_pieces;
     const bool light = t >= 0 && c <= kChunk && !sparse;
     const int32_t nh_items = heavy ? (c + kChunk - 1) / kChunk : (medium ? 1 : 0);
-    const unsigned long long p0 = wave_alloc(&cnt[CNT_SEGS], (unsigned long long)c);
-    const unsigned long long hi = wave_alloc(&cnt[CNT_ITEMS], (unsigned long long)nh_items);
-    const unsigned long long li = wave_alloc(&cnt[CNT_LITEMS], light ? 1ull : 0ull);
-    const unsigned long long si = wave_alloc(&cnt[CNT_SITEMS], sparse ? 1ull : 0ull);
-    const unsigned long long ho = wave_alloc(&cnt[CNT_HEAVY], heavy ? 1ull : 0ull);
+    unsigned long long* const ctr[5] = {&cnt[CNT_SEGS], &cnt[CNT_ITEMS], &cnt[CNT_LITEMS], &cnt[CNT_SITEMS],
+                                        &cnt[CNT_HEAVY]};
+    const unsigned long long want[5] = {(unsigned long long)c, (unsigned long long)nh_items, light ? 1ull : 0ull,
+                                        sparse ? 1ull : 0ull, heavy ? 1ull : 0ull};
+    unsigned long long got[5];
+    wave_alloc_n<5>(ctr, want, got);
+    const unsigned long long p0 = got[0], hi = got[1], li = got[2], si = got[3], ho = got[4];
     if (t < 0) continue;
     tile_cur[t] = (int32_t)p0;  // k_scatter's cursor: the tile's bin start
     // the host sizes every list for the worst case (grow_integrate); a write
