@@ -1121,6 +1121,10 @@ __global__ __launch_bounds__(256) void k_recount(Geom g, const int8_t* __restric
   if (threadIdx.x == 0) tile_free[tile] = acc;
 }
 
+__device__ inline uint64_t upto_rows(int p) {  // bits 0..p inclusive
+  return p >= 63 ? ~0ull : ((2ull << p) - 1ull);
+}
+
 // fmask records of the tiles this call's map update touched (its work items:
 // heavy chunks and medium tiles, then light tiles; a heavy tile appears once
 // per chunk and is rewritten with the same bytes), one wave per item, after
@@ -1131,6 +1135,7 @@ __global__ __launch_bounds__(256) void k_recount(Geom g, const int8_t* __restric
 // measured 6-14 us slower per call).
 __global__ __launch_bounds__(256) void k_fmask_items(Geom g, const int4* __restrict__ list_a, int cnt_a,
                                                      const int4* __restrict__ list_b, int cnt_b, int cnt_c,
+                                                     const PackedPiece* __restrict__ pieces,
                                                      const unsigned long long* __restrict__ cnt,
                                                      const int8_t* __restrict__ state, uint8_t* __restrict__ fmask,
                                                      const unsigned long long* __restrict__ halt) {
@@ -1141,15 +1146,38 @@ __global__ __launch_bounds__(256) void k_fmask_items(Geom g, const int4* __restr
   const int lane = __lane_id();
   for (int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); it < HI + LI + SI;
        it += (int64_t)gridDim.x * 4) {
-    const int32_t tile = __builtin_amdgcn_readfirstlane(
-        it < HI ? list_a[it].x
-                : (it < HI + LI ? list_b[it - HI].x : list_b[(int64_t)g.act_cap - 1 - (it - HI - LI)].x));
+    const int4 d = it < HI ? list_a[it]
+                           : (it < HI + LI ? list_b[it - HI] : list_b[(int64_t)g.act_cap - 1 - (it - HI - LI)]);
+    const int32_t tile = __builtin_amdgcn_readfirstlane(d.x);
+    // a sparse item (<= kSparseMax pieces) rewrites only the rows its pieces
+    // cross: a piece is a monotone line inside the tile, so it visits every
+    // row between its first and last cell's and no other (the others' state
+    // did not change); every other item its whole record
+    uint64_t rows = ~0ull;
+    if (it >= HI + LI) {
+      const int32_t c0 = __builtin_amdgcn_readfirstlane(d.y);
+      const int32_t c = __builtin_amdgcn_readfirstlane(d.z);
+      uint64_t mine = 0ull;
+      if (lane < c && (int64_t)c0 + c <= g.seg_cap) {
+        const PackedPiece q = pieces[c0 + lane];
+        const TilePiece tp = dm_unpack_piece(q.x, q.y, q.z, q.w);
+        if (tp.len > 0) {
+          const int32_t ya = tp.addr0 / kLdsPitch;
+          const int32_t yb = dm_piece_addr(tp, tp.len - 1, __builtin_amdgcn_rcpf((float)tp.two_n)) / kLdsPitch;
+          const int lo = min(ya, yb), hi = max(ya, yb);
+          mine = upto_rows(hi) & ~(lo > 0 ? upto_rows(lo - 1) : 0ull);
+        }
+      }
+      for (int o = 32; o > 0; o >>= 1) mine |= __shfl_xor(mine, o);
+      rows = mine;
+    }
     const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
     const int32_t x0 = tx0 + (lane & 3) * 16;
     uint8_t* tm = fmask + (int64_t)tile * (DM_TS * 16);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int ly = 16 * q + (lane >> 2);
+      if (!((rows >> ly) & 1ull)) continue;
       const int32_t y = ty0 + ly;
       uint32_t out = 0u;
       if (y < g.r.R) {
@@ -1350,7 +1378,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   }
   dm_timer_begin(g, "fmask", &t);
   DM_LAUNCH(k_fmask_items, dim3(grid_for(g->hitem_cap + g->act_cap, 4, 8192)), dim3(256), 0, g->stream,
-                     ge, w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS, (int)CNT_SITEMS, w.cnt,
+                     ge, w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS, (int)CNT_SITEMS, w.pieces, w.cnt,
                      g->state, g->fmask,
                      g->fe_flag + kHaltWord);
   dm_timer_end(g, &t);
