@@ -60,6 +60,8 @@ def parse():
                     help="run the steps back to back without overlapping step k+1's integrate "
                          "front-end with step k's frontier pass")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1")
+    ap.add_argument("--collective-timeout", type=float, default=300.0,
+                    help="N>1: seconds a collective may take before the job fails (DM_ERR_COLLECTIVE)")
     ap.add_argument("--device-override", type=int, default=None,
                     help="put every rank on this GPU (rehearsal with --backend gloo)")
     ap.add_argument("--config", default="C3", choices=["C3", "C1", "C2", "C4", "C5"],
@@ -96,14 +98,26 @@ def main():
         local_rank = args.device_override
     torch.cuda.set_device(local_rank)
     if world_size > 1:
+        import datetime
+
+        # a dead peer ends the job with an error instead of a hang: the
+        # process-group timeout bounds RCCL's watchdog, ShardedMapper's own
+        # deadline (DM_ERR_COLLECTIVE) bounds every exchange it waits for
+        pg_timeout = datetime.timedelta(seconds=args.collective_timeout)
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), timeout=pg_timeout)
         else:
-            dist.init_process_group(args.backend)
+            dist.init_process_group(args.backend, timeout=pg_timeout)
 
     import dm
     from dm import synth
     from dm.sharded import ShardedMapper
+
+    ring = int(dm.load_library().dm_max_passes_in_flight())
+    if args.order == "be" and args.depth + 1 > ring:
+        # 'be' starts pass k before collecting pass k-depth: depth + 1 in flight
+        raise SystemExit(f"--order be --depth {args.depth} needs {args.depth + 1} readback slots; "
+                         f"libdm has {ring} (DM_RB_SLOTS): use --depth {ring - 1} or more slots")
 
     res = 0.05
     if c4:  # BASELINE C4: one 32768² map, 32 robots anywhere in it, bands = ranks
@@ -162,7 +176,8 @@ def main():
     params.origin_x = -half_w
     params.origin_y = oy_global
     mapper = ShardedMapper(params, rank=rank, world_size=world_size, device=local_rank,
-                           group=dist.group.WORLD if world_size > 1 else None)
+                           group=dist.group.WORLD if world_size > 1 else None,
+                           timeout=args.collective_timeout)
     band = mapper.band
     S, N = args.robots, args.beams
 
@@ -406,6 +421,10 @@ def main():
                 "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                # the same launch against the bytes it actually moved (PMC,
+                # per-shape calibrated factors): what the DRAM really did
+                "frac_traffic": (traffic / (t_accum_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS
+                                 if traffic and t_accum_ms > 0 else None),
                 "avg_launch_ms": t_accum_ms,
                 "algorithmic_bytes_per_launch": bytes_accum,
                 "bytes_model": ("8*U + 25*(T - T_heavy) per call" if TH_mean else "8*U + 25*T per call") + " (SURVEY.md §8(d) per-unit figures)",
@@ -454,7 +473,8 @@ def pmc_summary(workload):
     w = summ.get("workloads", {}).get(workload)
     if w is None:
         return None, f"profiles/pmc_latest.json has no {workload} workload"
-    return w, f"profiles/pmc_latest.json [{workload}] (2*FETCH_SIZE + WRITE_SIZE, KiB->B)"
+    return w, (f"profiles/pmc_latest.json [{workload}] (FETCH_SIZE, WRITE_SIZE KiB x per-shape factors of "
+               f"profiles/fetch_calibration.json, tools/pmc_summary.py)")
 
 
 def pmc_traffic(kernel, workload):
@@ -473,37 +493,39 @@ PMC_FRONTIER_KERNELS = ("k_frontier_prep", "k_frontier_bits", "k_frontier_tile",
 
 
 def frontier_roofline(avg, cells, F, K, tiles_visited, workload, wall_s=None):
-    """Frontier pass vs the HBM roofline.  Algorithmic bytes per pass
-    (SURVEY.md §8(d)): B_fr = 2*W*H (read state, write a byte mask) + 16*F
-    (int64 label write + read per frontier cell) + 48*K (cluster records),
-    over the pass's device time (sum of its kernels' HIP-event averages).
-    The kernels read only the tiles holding a free cell, so
-    `visited_bytes` restates B_fr over those tiles alone (4096 state bytes +
-    260 halo bytes + a 4096-byte mask each)."""
+    """Frontier pass vs the HBM roofline, over the sum of its kernels'
+    HIP-event averages (device time).  SURVEY.md §8(d) prices a pass at
+    B_fr = 2*W*H (read state, write a byte mask) + 16*F (int64 label write +
+    read per frontier cell) + 48*K (cluster records); the kernels read only
+    the tiles holding a free cell, so `frac` is that model
+    over the tiles the pass actually lists (4096 state bytes + 260 halo bytes
+    + a 4096-byte mask each: `visited_bytes`), `frac_full_map` the whole-map
+    model (it charges bytes a sparse pass never touches), and
+    `frac_traffic` the PMC-measured bytes."""
     t_ms = sum(avg.get(k, 0.0) for k in FRONTIER_KERNELS)
     B = 2.0 * cells + 16.0 * F + 48.0 * K
-    ach = B / (t_ms * 1e-3) / 1e9 if t_ms > 0 else None
-    out = {"bound": "hbm", "bytes_model": "2*W*H + 16*F + 48*K per pass (SURVEY.md §8(d))",
-           "algorithmic_bytes": B, "frontier_cells": F, "clusters": K, "device_ms": t_ms,
-           "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-           "frac": ach / HBM_PEAK_GBPS if ach else None,
+    ach_full = B / (t_ms * 1e-3) / 1e9 if t_ms > 0 else None
+    out = {"bound": "hbm", "bytes_model": "(4096 + 260 + 4096)*tiles_visited + 16*F + 48*K per pass "
+                                          "(SURVEY.md §8(d)'s 2*W*H + 16*F + 48*K over the listed tiles)",
+           "full_map_bytes": B, "frontier_cells": F, "clusters": K, "device_ms": t_ms,
+           "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+           "frac_full_map": ach_full / HBM_PEAK_GBPS if ach_full else None,
            "kernels_ms": {k: avg[k] for k in FRONTIER_KERNELS if k in avg}}
     if wall_s:
         out["wall_ms"] = wall_s * 1e3
-    if tiles_visited is not None:
-        vb = (4096.0 + 260.0 + 4096.0) * tiles_visited + 16.0 * F + 48.0 * K
-        out["tiles_visited"] = tiles_visited
-        out["visited_bytes"] = vb
-        out["frac_visited"] = vb / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if t_ms > 0 else None
+    vb = (4096.0 + 260.0 + 4096.0) * (tiles_visited or 0) + 16.0 * F + 48.0 * K
+    ach = vb / (t_ms * 1e-3) / 1e9 if t_ms > 0 else None
+    out.update({"tiles_visited": tiles_visited, "algorithmic_bytes": vb, "achieved": ach,
+                "frac": ach / HBM_PEAK_GBPS if ach else None})
     w, src = pmc_summary(workload)
+    out["traffic"] = None
+    out["traffic_source"] = src
     if w is not None:
         ks = w.get("kernels", {})
         tr = [ks[k]["traffic_bytes"] for k in PMC_FRONTIER_KERNELS if "traffic_bytes" in ks.get(k, {})]
         out["traffic"] = sum(tr) if tr else None
-        out["traffic_source"] = src
-    else:
-        out["traffic"] = None
-        out["traffic_source"] = src
+        if out["traffic"] and t_ms > 0:
+            out["frac_traffic"] = out["traffic"] / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS
     return out
 
 
@@ -567,6 +589,7 @@ def cpu_baseline(params, pool, amin, inc, budget_s):
     a = time.perf_counter()
     om.frontiers(want_mask=False, want_labels=False)
     t_fr = time.perf_counter() - a
+    del om
     return {
         "value": U / t_int,
         "unit": "beam-cell updates/s",
@@ -576,7 +599,47 @@ def cpu_baseline(params, pool, amin, inc, budget_s):
                    f"{params.width}x{params.height} map + 1 frontier pass"),
         "frontier_ms": t_fr * 1e3,
         "cpu": _cpu_model(),
+        "strong": cpu_baseline_strong(params, pool, amin, inc, budget_s),
     }
+
+
+def host_threads():
+    """Host cores this process may use: the CPU share the GPU box gives a
+    job (OMP_NUM_THREADS is set to it there) within the affinity mask."""
+    n = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    return min(n, int(env)) if env.isdigit() and int(env) > 0 else n
+
+
+def cpu_baseline_strong(params, pool, amin, inc, budget_s):
+    """The "strong CPU" line: the same SPEC restated with
+    OpenMP on every host core this job may use (oracle/dm_oracle_mt.c, -O3;
+    the build's own code, bit-identical to the 1-thread port by
+    tests/test_oracle.py), on the same bounded sample."""
+    import oracle
+
+    threads = host_threads()
+    om = oracle.OracleMapMT(params, threads=threads)
+    om.integrate(*pool[0], amin, inc)  # warm-up (untimed): first-touch page faults of the map and counters
+    U = 0
+    t_int = 0.0
+    done = 0
+    for k in range(1, max(1, len(pool)) * 8):
+        poses, ranges = pool[k % len(pool)]
+        a = time.perf_counter()
+        u, _ = om.integrate(poses, ranges, amin, inc)
+        t_int += time.perf_counter() - a
+        U += u
+        done += 1
+        if t_int > budget_s * 0.3:
+            break
+    a = time.perf_counter()
+    om.frontiers(want_mask=False, want_labels=False)
+    t_fr = time.perf_counter() - a
+    return {"value": U / t_int, "unit": "beam-cell updates/s", "cores": om.threads, "kind": "port (OpenMP)",
+            "sample": (f"{done} batch(es) after 1 untimed warm-up batch into a fresh {params.width}x"
+                       f"{params.height} map + 1 frontier pass"),
+            "frontier_ms": t_fr * 1e3}
 
 
 def _cpu_model():

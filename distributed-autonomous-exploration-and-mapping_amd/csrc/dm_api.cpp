@@ -320,6 +320,15 @@ int check_grid(const dm_grid* g) {
   return DM_OK;
 }
 
+// The building blocks of the multi-process exchange are not calls of a
+// sharded parent: it runs that exchange itself (dm_sharded.cpp).
+int not_on_sharded(const dm_grid* g, const char* what) {
+  if (g && g->sh)
+    return dm_set_error(DM_ERR_INVALID_ARG, "%s is not available on a sharded handle (dm_create_sharded runs "
+                                            "the band exchange itself)", what);
+  return DM_OK;
+}
+
 int use_device(const dm_grid* g) {
   DM_HIP(hipSetDevice(g->device));
   return DM_OK;
@@ -480,9 +489,11 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     // cross-stream hand-offs (C3 A/B): the front-end ->
     // map update by a device-side seq gate (DM_FE_GATE=0: an event wait;
     // gate 215-218 vs event 211-213 x 10^9, profiles/r02_fe_gate_ab.log), the
-    // bit rows -> pass stream by an event wait, which also frees the
-    // integrate workspaces early (DM_PASS_GATE=1: a seq gate, and the
-    // workspaces wait for the pass's readback event: 179-183 x 10^9)
+    // bit rows -> pass stream by an event wait (DM_PASS_GATE=1: a seq gate,
+    // 179-183 x 10^9 when it still freed the integrate workspaces by the
+    // readback event).  Either way the workspaces are freed by an event on
+    // the grid stream after the bit rows (a timed-out pass gate cannot free
+    // them before the accumulation that reads them)
     g->fe_gate = !dm_env_off("DM_FE_GATE");
     g->pass_gate = dm_env_on("DM_PASS_GATE");
     if (const char* ag = getenv("DM_ACCUM_GRID")) g->accum_grid = std::max(1, atoi(ag));
@@ -551,13 +562,31 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     p_fe = pr[1] == 'h' ? prio_hi : prio_lo;
     p_pass = pr[2] == 'h' ? prio_hi : prio_lo;
   }
-  e = hipStreamCreateWithPriority(&g->stream, hipStreamNonBlocking, p_grid);
-  if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate"));
-  g->own_stream = true;
-  e = hipStreamCreateWithPriority(&g->fe_stream, hipStreamNonBlocking, p_fe);
-  if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(front-end)"));
-  e = hipStreamCreateWithPriority(&g->pass_stream, hipStreamNonBlocking, p_pass);
-  if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(pass)"));
+  // DM_FE_CUS=n (A/B): the integrate front-end's stream runs
+  // on CUs [0, n) of the CU mask and the map / pass streams on the rest, so
+  // batch k+1's front-end runs beside accumulation k instead of after its
+  // last dispatch (KFD spreads a contiguous range of mask bits evenly over
+  // the shader engines).  CU-masked streams carry no priority.
+  const int fe_cus = getenv("DM_FE_CUS") ? atoi(getenv("DM_FE_CUS")) : 0;
+  if (fe_cus > 0 && fe_cus < g->n_cu) {
+    std::vector<uint32_t> fe_mask((size_t)(g->n_cu + 31) / 32, 0u), map_mask(fe_mask.size(), 0u);
+    for (int c = 0; c < g->n_cu; ++c) (c < fe_cus ? fe_mask : map_mask)[(size_t)c / 32] |= 1u << (c % 32);
+    e = hipExtStreamCreateWithCUMask(&g->stream, (uint32_t)map_mask.size(), map_mask.data());
+    if (e != hipSuccess) return fail(dm_hip_check(e, "hipExtStreamCreateWithCUMask"));
+    g->own_stream = true;
+    e = hipExtStreamCreateWithCUMask(&g->fe_stream, (uint32_t)fe_mask.size(), fe_mask.data());
+    if (e != hipSuccess) return fail(dm_hip_check(e, "hipExtStreamCreateWithCUMask(front-end)"));
+    e = hipExtStreamCreateWithCUMask(&g->pass_stream, (uint32_t)map_mask.size(), map_mask.data());
+    if (e != hipSuccess) return fail(dm_hip_check(e, "hipExtStreamCreateWithCUMask(pass)"));
+  } else {
+    e = hipStreamCreateWithPriority(&g->stream, hipStreamNonBlocking, p_grid);
+    if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate"));
+    g->own_stream = true;
+    e = hipStreamCreateWithPriority(&g->fe_stream, hipStreamNonBlocking, p_fe);
+    if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(front-end)"));
+    e = hipStreamCreateWithPriority(&g->pass_stream, hipStreamNonBlocking, p_pass);
+    if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(pass)"));
+  }
   // ev_fe / ev_free only order the two streams on the device: no system-
   // scope fence (no host-visible cache writeback at every step).  The host
   // waits on a readback slot's event and then reads mapped host memory:
@@ -580,6 +609,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
 }
 
 int dm_destroy(dm_grid* g) {
+  if (g && g->sh) return dm_sh_destroy(g);
   if (!g) return DM_OK;
   (void)hipSetDevice(g->device);
   (void)dm_sync_all(g);
@@ -630,6 +660,7 @@ int dm_destroy(dm_grid* g) {
 }
 
 int dm_reset(dm_grid* g) {
+  if (g && g->sh) return dm_sh_reset(g);
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   const int64_t cells = g->W * g->R;
@@ -709,9 +740,11 @@ int enqueue_host_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N
   // last call's reads are ahead of these copies in stream order
   if (S > 0)
     DM_HIP(hipMemcpyAsync(g->pose4, hp, sizeof(double) * 4 * (size_t)S, hipMemcpyHostToDevice, fs));
-  DM_HIP(hipEventRecord(g->ev_pose[slot], fs));
   if (nb > 0)
     DM_HIP(hipMemcpyAsync(g->ranges, ranges, sizeof(float) * (size_t)nb, hipMemcpyHostToDevice, fs));
+  // after BOTH copies: two calls later this event proves the caller's ranges
+  // buffer has been read too (dm.h: reusable after the second call that follows)
+  DM_HIP(hipEventRecord(g->ev_pose[slot], fs));
   if ((rc = dm_launch_integrate(g, S, g->pose4, N, g->ranges, g->trig))) return rc;
   g->last_S = S;
   g->last_N = N;
@@ -727,6 +760,7 @@ extern "C" {
 int dm_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N, const float* ranges,
                  float angle_min, float angle_increment, uint64_t* out_updates,
                  uint64_t* out_touched) {
+  if (g && g->sh) return dm_sh_integrate(g, S, poses, N, ranges, angle_min, angle_increment, out_updates, out_touched);
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if ((rc = enqueue_host_integrate(g, S, poses, N, ranges, angle_min, angle_increment))) return rc;
@@ -735,6 +769,7 @@ int dm_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N, const fl
 
 int dm_integrate_async(dm_grid* g, int32_t S, const double* poses, int32_t N, const float* ranges,
                        float angle_min, float angle_increment) {
+  if (g && g->sh) return dm_sh_integrate_async(g, S, poses, N, ranges, angle_min, angle_increment);
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   return enqueue_host_integrate(g, S, poses, N, ranges, angle_min, angle_increment);
@@ -742,6 +777,7 @@ int dm_integrate_async(dm_grid* g, int32_t S, const double* poses, int32_t N, co
 
 int dm_integrate_device(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                         const float* d_ranges, float angle_min, float angle_increment) {
+  if (g && g->sh) return dm_sh_integrate_device(g, S, d_pose4, N, d_ranges, angle_min, angle_increment);
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if ((rc = check_integrate_args(S, N, d_pose4, d_ranges))) return rc;
@@ -756,12 +792,14 @@ int dm_integrate_device(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
 }
 
 int dm_last_counts(dm_grid* g, uint64_t* updates, uint64_t* touched) {
+  if (g && g->sh) return dm_sh_last_counts(g, updates, touched);
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   return finish_counts(g, updates, touched);
 }
 
 int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out) {
+  if (g && g->sh) return dm_sh_last_stats(g, out, cap, n_out);
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (cap > 0 && !out) return dm_set_error(DM_ERR_INVALID_ARG, "out is NULL");
@@ -782,6 +820,7 @@ int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out) {
 }
 
 int dm_get_state(dm_grid* g, int8_t* out) {
+  if (g && g->sh) return (out ? dm_sh_get_state(g, out) : dm_set_error(DM_ERR_INVALID_ARG, "out is NULL"));
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (!out) return dm_set_error(DM_ERR_INVALID_ARG, "out is NULL");
@@ -791,6 +830,7 @@ int dm_get_state(dm_grid* g, int8_t* out) {
 }
 
 int dm_get_logodds(dm_grid* g, float* out) {
+  if (g && g->sh) return (out ? dm_sh_get_logodds(g, out) : dm_set_error(DM_ERR_INVALID_ARG, "out is NULL"));
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (!out) return dm_set_error(DM_ERR_INVALID_ARG, "out is NULL");
@@ -801,6 +841,7 @@ int dm_get_logodds(dm_grid* g, float* out) {
 }
 
 int dm_set_logodds(dm_grid* g, const float* in) {
+  if (g && g->sh) return (in ? dm_sh_set_logodds(g, in) : dm_set_error(DM_ERR_INVALID_ARG, "in is NULL"));
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (!in) return dm_set_error(DM_ERR_INVALID_ARG, "in is NULL");
@@ -814,6 +855,7 @@ int dm_set_logodds(dm_grid* g, const float* in) {
 }
 
 int dm_set_state(dm_grid* g, const int8_t* in) {
+  if (g && g->sh) return (in ? dm_sh_set_state(g, in) : dm_set_error(DM_ERR_INVALID_ARG, "in is NULL"));
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (!in) return dm_set_error(DM_ERR_INVALID_ARG, "in is NULL");
@@ -835,6 +877,7 @@ int dm_set_state(dm_grid* g, const int8_t* in) {
 
 int dm_frontiers(dm_grid* g, uint8_t* mask, int64_t* labels, dm_cluster* out, int64_t cap,
                  int64_t* n_out) {
+  if (g && g->sh) return dm_sh_frontiers(g, mask, labels, out, cap, n_out);
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (cap < 0 || (cap > 0 && !out)) return dm_set_error(DM_ERR_INVALID_ARG, "bad cluster buffer");
@@ -871,6 +914,7 @@ int dm_frontiers(dm_grid* g, uint8_t* mask, int64_t* labels, dm_cluster* out, in
 }
 
 int dm_export_bytes(const dm_grid* g, int64_t rec_cap, int64_t* bytes) {
+  if (int rc0 = not_on_sharded(g, "dm_export_bytes")) return rc0;
   int rc = check_grid(g);
   if (rc) return rc;
   if (!bytes || rec_cap < 0) return dm_set_error(DM_ERR_INVALID_ARG, "bytes is NULL or rec_cap < 0");
@@ -879,6 +923,7 @@ int dm_export_bytes(const dm_grid* g, int64_t rec_cap, int64_t* bytes) {
 }
 
 int dm_frontiers_export_device(dm_grid* g, void* d_export, int64_t rec_cap) {
+  if (int rc0 = not_on_sharded(g, "dm_frontiers_export_device")) return rc0;
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (!d_export || rec_cap < 0) return dm_set_error(DM_ERR_INVALID_ARG, "d_export is NULL or rec_cap < 0");
@@ -886,9 +931,11 @@ int dm_frontiers_export_device(dm_grid* g, void* d_export, int64_t rec_cap) {
     return dm_set_error(DM_ERR_INVALID_ARG,
                         "export needs a band handle with min_frontier_size <= 1 (the size filter "
                         "applies to merged clusters)");
-  if (g->rb_count == dm_grid::kRbSlots)
-    return dm_set_error(DM_ERR_INVALID_ARG, "%d passes in flight: end one first", dm_grid::kRbSlots);
-  dm_select_slot(g, (g->rb_head + g->rb_count) % dm_grid::kRbSlots);
+  // the band's sorted records go to a readback slot no pending pass holds
+  // (the synchronous slot when the ring is full: a merge of a sharded parent
+  // can have every ring slot pending on its band 0)
+  dm_select_slot(g, g->rb_count < dm_grid::kRbSlots ? (g->rb_head + g->rb_count) % dm_grid::kRbSlots
+                                                    : dm_grid::kRbSync);
   if ((rc = dm_enqueue_frontiers(g, false, false))) return rc;
   if ((rc = dm_launch_export(g, d_export, rec_cap))) return rc;
   DM_HIP(dm_mark_ws_free(g));
@@ -965,6 +1012,7 @@ int merge_readback(dm_grid* g, int slot, int64_t n, dm_cluster* out, int64_t cap
 
 int dm_merge_bands_begin(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap,
                          int64_t min_size) {
+  if (int rc0 = not_on_sharded(g, "dm_merge_bands_begin")) return rc0;
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (!d_gathered || nranks < 1 || rec_cap < 1)
@@ -986,6 +1034,7 @@ int dm_merge_bands_begin(dm_grid* g, const void* d_gathered, int32_t nranks, int
 }
 
 int dm_merge_bands_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out) {
+  if (int rc0 = not_on_sharded(g, "dm_merge_bands_end")) return rc0;
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (cap < 0 || (cap > 0 && !out)) return dm_set_error(DM_ERR_INVALID_ARG, "bad cluster buffer");
@@ -998,6 +1047,7 @@ int dm_merge_bands_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out)
 
 int dm_merge_bands(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap, int64_t min_size,
                    dm_cluster* out, int64_t cap, int64_t* n_out) {
+  if (int rc0 = not_on_sharded(g, "dm_merge_bands")) return rc0;
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (!d_gathered || nranks < 1 || rec_cap < 1)
@@ -1014,6 +1064,7 @@ int dm_merge_bands(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t r
 }
 
 int dm_frontiers_begin(dm_grid* g) {
+  if (g && g->sh) return dm_sh_frontiers_begin(g);
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   int slot = 0;
@@ -1046,6 +1097,7 @@ int dm_frontiers_begin(dm_grid* g) {
 }
 
 int dm_frontiers_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out) {
+  if (g && g->sh) return dm_sh_frontiers_end(g, out, cap, n_out);
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (cap < 0 || (cap > 0 && !out)) return dm_set_error(DM_ERR_INVALID_ARG, "bad cluster buffer");
@@ -1086,8 +1138,26 @@ int dm_frontiers_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out) {
   return grow_host_out(g, slot, n + n / 4 + 64);
 }
 
+int dm_frontiers_poll(dm_grid* g, int32_t* ready) {
+  if (g && g->sh) return dm_sh_frontiers_poll(g, ready);
+  int rc = check_grid(g);
+  if (rc || (rc = use_device(g))) return rc;
+  if (!ready) return dm_set_error(DM_ERR_INVALID_ARG, "ready is NULL");
+  *ready = 0;
+  if (!g->rb_count) return dm_set_error(DM_ERR_INVALID_ARG, "no asynchronous pass in flight");
+  const hipError_t e = hipEventQuery(g->rb[g->rb_head].ev);
+  if (e == hipSuccess) {
+    *ready = 1;
+    return DM_OK;
+  }
+  if (e == hipErrorNotReady) return DM_OK;
+  DM_HIP(e);
+  return DM_OK;
+}
+
 int dm_assign_goals(dm_grid* g, const double* robots_xy, int32_t n_robots, int64_t min_size,
                     double distance_weight, double min_distance, int64_t* out_index, double* out_xy) {
+  if (g && g->sh) return dm_sh_assign_goals(g, robots_xy, n_robots, min_size, distance_weight, min_distance, out_index, out_xy);
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (n_robots < 0 || n_robots > 256)
@@ -1096,6 +1166,10 @@ int dm_assign_goals(dm_grid* g, const double* robots_xy, int32_t n_robots, int64
     return dm_set_error(DM_ERR_INVALID_ARG, "robots_xy / out_index / out_xy is NULL");
   if (!isfinite(distance_weight) || !isfinite(min_distance))
     return dm_set_error(DM_ERR_INVALID_ARG, "distance_weight / min_distance must be finite");
+  // the device ranks by the util's IEEE bits, an order that holds for util > 0
+  // only: w >= 0 keeps util = size / (1 + w*dist) positive and finite
+  if (distance_weight < 0.0)
+    return dm_set_error(DM_ERR_INVALID_ARG, "distance_weight must be >= 0");
   const int s = g->goal_slot;
   if (s < 0 || g->goal_gen != g->rb_gen ||
       (g->goal_kind == 1 ? g->rb[s].wepoch : g->rb[s].mepoch) != g->goal_epoch)
@@ -1149,6 +1223,7 @@ int dm_assign_goals(dm_grid* g, const double* robots_xy, int32_t n_robots, int64
 }
 
 int dm_set_overlap(dm_grid* g, int32_t on) {
+  if (g && g->sh) return dm_sh_set_overlap(g, on);
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   DM_HIP(dm_sync_all(g));
@@ -1161,6 +1236,7 @@ int dm_set_overlap(dm_grid* g, int32_t on) {
 }
 
 int dm_set_halo(dm_grid* g, const int8_t* before, const int8_t* after) {
+  if (int rc0 = not_on_sharded(g, "dm_set_halo")) return rc0;
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   DM_HIP(hipStreamSynchronize(g->stream));
@@ -1174,6 +1250,7 @@ int dm_set_halo(dm_grid* g, const int8_t* before, const int8_t* after) {
 }
 
 int dm_set_halo_device(dm_grid* g, const int8_t* before, const int8_t* after) {
+  if (int rc0 = not_on_sharded(g, "dm_set_halo_device")) return rc0;
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (before) DM_HIP(hipMemcpyAsync(g->halo, before, (size_t)g->W, hipMemcpyDeviceToDevice, g->stream));
@@ -1187,6 +1264,7 @@ int dm_set_halo_device(dm_grid* g, const int8_t* before, const int8_t* after) {
 }
 
 int dm_get_edge_rows(dm_grid* g, int8_t* first_row, int8_t* last_row) {
+  if (int rc0 = not_on_sharded(g, "dm_get_edge_rows")) return rc0;
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (first_row)
@@ -1199,6 +1277,7 @@ int dm_get_edge_rows(dm_grid* g, int8_t* first_row, int8_t* last_row) {
 }
 
 int dm_get_edge_rows_device(dm_grid* g, int8_t* first_row, int8_t* last_row) {
+  if (int rc0 = not_on_sharded(g, "dm_get_edge_rows_device")) return rc0;
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (first_row)
@@ -1210,6 +1289,7 @@ int dm_get_edge_rows_device(dm_grid* g, int8_t* first_row, int8_t* last_row) {
 }
 
 int dm_get_edge_labels(dm_grid* g, int64_t* first_row, int64_t* last_row) {
+  if (int rc0 = not_on_sharded(g, "dm_get_edge_labels")) return rc0;
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (!g->frontier_valid)
@@ -1235,6 +1315,7 @@ static int check_ld06_args(int32_t S, int32_t N, const void* pts, const void* of
 int dm_ld06_to_scans_device(dm_grid* g, int32_t S, const dm_ld06_point* d_points,
                             const int64_t* d_offsets, int32_t N, int laser_scan_dir,
                             float* d_ranges_out, float* d_intensities_out) {
+  if (g && g->sh) return dm_sh_ld06_to_scans_device(g, S, d_points, d_offsets, N, laser_scan_dir, d_ranges_out, d_intensities_out);
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if ((rc = check_ld06_args(S, N, d_points, d_offsets, d_ranges_out))) return rc;
@@ -1244,6 +1325,7 @@ int dm_ld06_to_scans_device(dm_grid* g, int32_t S, const dm_ld06_point* d_points
 
 int dm_ld06_to_scans(dm_grid* g, int32_t S, const dm_ld06_point* points, const int64_t* offsets,
                      int32_t N, int laser_scan_dir, float* ranges_out, float* intensities_out) {
+  if (g && g->sh) return dm_sh_ld06_to_scans(g, S, points, offsets, N, laser_scan_dir, ranges_out, intensities_out);
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if ((rc = check_ld06_args(S, N, points, offsets, ranges_out))) return rc;
@@ -1319,6 +1401,7 @@ int dm_load(dm_grid* g, const char* path) {
 }
 
 int dm_set_stream(dm_grid* g, void* stream) {
+  if (int rc0 = not_on_sharded(g, "dm_set_stream")) return rc0;
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   DM_HIP(dm_sync_all(g));
@@ -1334,6 +1417,7 @@ int dm_set_stream(dm_grid* g, void* stream) {
 }
 
 int dm_synchronize(dm_grid* g) {
+  if (g && g->sh) return dm_sh_synchronize(g);
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   DM_HIP(dm_sync_all(g));
@@ -1341,6 +1425,7 @@ int dm_synchronize(dm_grid* g) {
 }
 
 int dm_profile_enable(dm_grid* g, int enable) {
+  if (g && g->sh) return dm_sh_profile_enable(g, enable);
   int rc = check_grid(g);
   if (rc) return rc;
   g->profile = enable != 0;
@@ -1348,6 +1433,7 @@ int dm_profile_enable(dm_grid* g, int enable) {
 }
 
 int dm_profile_read(dm_grid* g, dm_kernel_stat* out, int32_t cap, int32_t* n_out) {
+  if (g && g->sh) return dm_sh_profile_read(g, out, cap, n_out);
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   DM_HIP(hipStreamSynchronize(g->stream));
@@ -1377,6 +1463,7 @@ int dm_profile_read(dm_grid* g, dm_kernel_stat* out, int32_t cap, int32_t* n_out
 }
 
 int dm_profile_reset(dm_grid* g) {
+  if (g && g->sh) return dm_sh_profile_reset(g);
   int rc = check_grid(g);
   if (rc) return rc;
   int32_t n = 0;
@@ -1386,6 +1473,7 @@ int dm_profile_reset(dm_grid* g) {
 }
 
 int dm_map_image(dm_grid* g, uint8_t* out) {
+  if (g && g->sh) return (out ? dm_sh_map_image(g, out) : dm_set_error(DM_ERR_INVALID_ARG, "out is NULL"));
   int rc = check_grid(g);
   if (rc || (rc = use_device(g))) return rc;
   if (!out) return dm_set_error(DM_ERR_INVALID_ARG, "out is NULL");

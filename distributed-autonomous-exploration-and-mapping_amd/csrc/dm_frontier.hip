@@ -1605,17 +1605,19 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   hipStream_t ps = g->stream;
   if (split) {
     ps = g->pass_stream;
+    DM_HIP(dm_batch_flush_all());
+    hipEvent_t eb = g->ev_bits[g->fparity];
+    DM_HIP(hipEventRecord(eb, g->stream));
+    // the integrate workspaces are free once the grid stream is past the
+    // accumulations (both hand-off forms: a timed-out gate below must not
+    // free them early).  (Re-recorded two passes later: a front-end waiting
+    // on it then waits longer than needed, never too little -- every record
+    // follows the accumulations it frees in stream order.)
+    DM_HIP(dm_mark_ws_free(g, eb));
     if (g->pass_gate) {
       if (int rc = dm_launch_signal(g->stream, g->bits_flag)) return rc;
       if (int rc = dm_launch_gate(ps, g->bits_flag, g->cnt + CNT_OVERFLOW, kOvGate)) return rc;
     } else {
-      DM_HIP(dm_batch_flush_all());
-      hipEvent_t eb = g->ev_bits[g->fparity];
-      DM_HIP(hipEventRecord(eb, g->stream));
-      // (re-recorded two passes later: a front-end waiting on it then waits
-      // longer than needed, never too little -- every record follows the
-      // accumulations it frees in stream order)
-      DM_HIP(dm_mark_ws_free(g, eb));
       DM_HIP(hipStreamWaitEvent(ps, eb, 0));
     }
   }

@@ -118,8 +118,13 @@ struct KernelTimer {
   hipStream_t stream = nullptr;
 };
 
+struct dm_shard_set;  // dm_sharded.cpp
+
 struct dm_grid {
   dm_params p;
+  // non-null: a sharded parent (dm_create_sharded); every call runs on its
+  // band handles (dm_sharded.cpp) and none of the fields below is allocated
+  dm_shard_set* sh = nullptr;
   int device = 0;
   int n_cu = 256;  // compute units of the device: sizes the resident (one-pass) grids
   hipStream_t stream = nullptr;
@@ -494,6 +499,38 @@ int dm_launch_goal_topk(dm_grid* g, const dm_cluster* d_recs, int64_t K, const d
 int dm_launch_goal_gather(dm_grid* g, const dm_cluster* d_recs, const int64_t* d_idx, int32_t R, double* d_xy);
 int dm_launch_ld06(dm_grid* g, int32_t S, const dm_ld06_point* d_pts, const int64_t* d_offsets,
                    int32_t N, int dir, float* d_ranges, float* d_intensities);
+
+// sharded parents (dm_sharded.cpp): the public calls dispatch here
+int dm_sh_destroy(dm_grid* g);
+int dm_sh_reset(dm_grid* g);
+int dm_sh_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N, const float* ranges, float amin,
+                    float inc, uint64_t* U, uint64_t* T);
+int dm_sh_integrate_async(dm_grid* g, int32_t S, const double* poses, int32_t N, const float* ranges,
+                          float amin, float inc);
+int dm_sh_integrate_device(dm_grid* g, int32_t S, const double* d_pose4, int32_t N, const float* d_ranges,
+                           float amin, float inc);
+int dm_sh_last_counts(dm_grid* g, uint64_t* U, uint64_t* T);
+int dm_sh_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out);
+int dm_sh_get_state(dm_grid* g, int8_t* out);
+int dm_sh_get_logodds(dm_grid* g, float* out);
+int dm_sh_set_logodds(dm_grid* g, const float* in);
+int dm_sh_set_state(dm_grid* g, const int8_t* in);
+int dm_sh_frontiers(dm_grid* g, uint8_t* mask, int64_t* labels, dm_cluster* out, int64_t cap, int64_t* n_out);
+int dm_sh_frontiers_begin(dm_grid* g);
+int dm_sh_frontiers_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out);
+int dm_sh_frontiers_poll(dm_grid* g, int32_t* ready);
+int dm_sh_assign_goals(dm_grid* g, const double* robots_xy, int32_t n_robots, int64_t min_size, double w,
+                       double min_distance, int64_t* out_index, double* out_xy);
+int dm_sh_set_overlap(dm_grid* g, int32_t on);
+int dm_sh_synchronize(dm_grid* g);
+int dm_sh_profile_enable(dm_grid* g, int enable);
+int dm_sh_profile_read(dm_grid* g, dm_kernel_stat* out, int32_t cap, int32_t* n_out);
+int dm_sh_profile_reset(dm_grid* g);
+int dm_sh_map_image(dm_grid* g, uint8_t* out);
+int dm_sh_ld06_to_scans(dm_grid* g, int32_t S, const dm_ld06_point* points, const int64_t* offsets, int32_t N,
+                        int dir, float* ranges, float* intensities);
+int dm_sh_ld06_to_scans_device(dm_grid* g, int32_t S, const dm_ld06_point* d_points, const int64_t* d_offsets,
+                               int32_t N, int dir, float* d_ranges, float* d_intensities);
 
 // error plumbing (dm_api.cpp)
 int dm_set_error(int code, const char* fmt, ...);

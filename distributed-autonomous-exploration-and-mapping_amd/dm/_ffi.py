@@ -24,6 +24,7 @@ DM_ERR_IO = -6
 DM_ERR_STATE = -7
 DM_ERR_INCOMPLETE = -8
 DM_ERR_PIPELINE = -9
+DM_ERR_COLLECTIVE = -10
 DM_TILE = 64
 
 _ERR_NAMES = {
@@ -36,6 +37,7 @@ _ERR_NAMES = {
     DM_ERR_STATE: "DM_ERR_STATE",
     DM_ERR_INCOMPLETE: "DM_ERR_INCOMPLETE",
     DM_ERR_PIPELINE: "DM_ERR_PIPELINE",
+    DM_ERR_COLLECTIVE: "DM_ERR_COLLECTIVE",
 }
 
 
@@ -126,6 +128,9 @@ _f32 = ctypes.c_float
 SIGNATURES = {
     "dm_default_params": [ctypes.POINTER(DmParams), _i64, _i64],
     "dm_create": [ctypes.POINTER(_vp), ctypes.POINTER(DmParams), ctypes.c_int],
+    "dm_create_sharded": [ctypes.POINTER(_vp), ctypes.POINTER(DmParams), _i32, ctypes.POINTER(_i32)],
+    "dm_sharded_band_rows": [_i64, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_i64)],
+    "dm_sharded_info": [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i64)],
     "dm_destroy": [_vp],
     "dm_reset": [_vp],
     "dm_get_params": [_vp, ctypes.POINTER(DmParams)],
@@ -162,6 +167,7 @@ SIGNATURES = {
     "dm_frontiers_begin": [_vp],
     "dm_max_passes_in_flight": [],
     "dm_frontiers_end": [_vp, _vp, _i64, ctypes.POINTER(_i64)],
+    "dm_frontiers_poll": [_vp, ctypes.POINTER(_i32)],
     "dm_set_overlap": [_vp, _i32],
     "dm_atomic_peak": [ctypes.c_int, _vp, _i32, ctypes.POINTER(_i32)],
     "dm_assign_goals": [_vp, _vp, _i32, ctypes.c_int64, ctypes.c_double, ctypes.c_double, _vp, _vp],
@@ -199,6 +205,11 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
             fn.restype = ctypes.c_char_p
         _lib = lib
         return lib
+
+
+def last_error() -> str:
+    v = load_library().dm_last_error()
+    return v.decode() if isinstance(v, bytes) else str(v)
 
 
 def check(rc: int) -> int:

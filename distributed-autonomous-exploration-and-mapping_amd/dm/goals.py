@@ -46,6 +46,8 @@ def assign_goals(clusters: np.ndarray, robots_xy, min_size: int = 8, distance_we
     (cluster index, (x, y)) or None per robot.  The device path is
     OccupancyMapper.assign_goals (dm_assign_goals); this is its host
     restatement, used by the tests."""
+    if not float(distance_weight) >= 0.0:
+        raise ValueError("distance_weight must be >= 0 (dm_assign_goals rejects it too)")
     robots = list(robots_xy)
     if clusters is None or len(clusters) == 0:
         return [None] * len(robots)

@@ -78,11 +78,20 @@ def _vp(a: np.ndarray | None):
 class OccupancyMapper:
     """One device-resident map (or one row band of a sharded map)."""
 
-    def __init__(self, params: DmParams, device: int = 0):
+    def __init__(self, params: DmParams, device: int = 0, devices=None):
+        """`devices`: a list of HIP devices to shard the map over in row bands
+        (dm_create_sharded; a device may repeat); the handle then takes the
+        same calls, with results identical to one handle."""
         self._lib = load_library()
         self._lock = threading.RLock()
         self._h = ctypes.c_void_p()
-        check(self._lib.dm_create(ctypes.byref(self._h), ctypes.byref(params), int(device)))
+        if devices is not None:
+            devs = (ctypes.c_int32 * len(devices))(*[int(d) for d in devices])
+            check(self._lib.dm_create_sharded(ctypes.byref(self._h), ctypes.byref(params), len(devices), devs))
+            device = int(devices[0])
+        else:
+            check(self._lib.dm_create(ctypes.byref(self._h), ctypes.byref(params), int(device)))
+        self.devices = list(devices) if devices is not None else [int(device)]
         out = DmParams()
         check(self._lib.dm_get_params(self._h, ctypes.byref(out)))
         self.params = out
@@ -91,6 +100,7 @@ class OccupancyMapper:
         self.rows = int(out.band_rows)
         self.row0 = int(out.band_row0)
         self._cap = 1 << 12  # cluster records per frontiers() buffer (grown on demand)
+        self.last_incomplete = None  # dm_last_error() of the last pass that returned no result
 
     # -- lifetime ---------------------------------------------------------
     def close(self):
@@ -279,6 +289,15 @@ class OccupancyMapper:
         with self._lock:
             check(self._lib.dm_frontiers_begin(self._handle()))
 
+    def frontiers_ready(self) -> bool:
+        """True when the oldest frontiers_begin() pass has completed, so
+        frontiers_end() returns without waiting (dm_frontiers_poll; never
+        blocks)."""
+        r = ctypes.c_int32(0)
+        with self._lock:
+            check(self._lib.dm_frontiers_poll(self._handle(), ctypes.byref(r)))
+        return bool(r.value)
+
     def frontiers_end(self) -> Frontiers | None:
         """Clusters of the pass started by frontiers_begin(), as frontiers()
         would have returned them on the map at that time; None if the pass
@@ -292,6 +311,7 @@ class OccupancyMapper:
                     self._cap = int(n.value) * 2  # the pass stays pending: read it again
                     continue
                 if rc == _ffi.DM_ERR_INCOMPLETE:
+                    self.last_incomplete = _ffi.last_error()
                     return None
                 check(rc)
                 return Frontiers(clusters=buf[: int(n.value)])
@@ -361,6 +381,7 @@ class OccupancyMapper:
                                               ctypes.byref(n))
                 self._mbuf = buf
                 if rc == _ffi.DM_ERR_INCOMPLETE:
+                    self.last_incomplete = _ffi.last_error()
                     return None, int(n.value)
                 if rc == _ffi.DM_ERR_CAPACITY and n.value > buf.shape[0]:
                     self._mbuf = np.empty(int(n.value) * 2, dtype=np.dtype(CLUSTER_DTYPE))
@@ -385,6 +406,7 @@ class OccupancyMapper:
                 rc = self._lib.dm_merge_bands_end(self._handle(), _vp(buf), buf.shape[0], ctypes.byref(n))
                 self._mbuf = buf
                 if rc == _ffi.DM_ERR_INCOMPLETE:
+                    self.last_incomplete = _ffi.last_error()
                     return None, int(n.value)
                 if rc == _ffi.DM_ERR_CAPACITY and n.value > buf.shape[0]:
                     self._mbuf = np.empty(int(n.value) * 2, dtype=np.dtype(CLUSTER_DTYPE))

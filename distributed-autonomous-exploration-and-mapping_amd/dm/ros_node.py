@@ -12,20 +12,28 @@ callback signatures:
   laser pose ``map -> base_laser`` through a pose provider (tf2 in ROS; any
   callable in tests);
 * gates scans the way the stage it replaces does (``ScanGate``: slam_toolbox's
-  ``throttle_scans`` / ``minimum_time_interval`` and Karto's
-  ``minimum_travel_distance`` / ``minimum_travel_heading``,
+  ``shouldProcessScan`` front gate, then Karto's ``HasMovedEnough``;
   slam_config.yaml:23,28,37-38) and integrates the accepted ones with libdm on
   the GPU (``dm_integrate``);
-* every ``map_update_interval`` seconds (slam_config.yaml:25) publishes
-  ``/map`` as ``nav_msgs/OccupancyGrid`` (frame ``map_frame``, resolution and
-  origin from the grid, int8 -1/0/100 row-major, ``data`` handed over as an
-  ``array('b')`` built from the device copy's bytes — no per-cell Python
-  objects), the frontier clusters on ``/frontiers``
-  (``geometry_msgs/PoseArray`` of centroids) and, with exploration enabled,
-  the chosen frontier goal on ``/goal_pose`` (``geometry_msgs/PoseStamped``,
-  the topic Nav2's navigator and RViz's "2D Goal Pose" use) — the map-based
-  replacement of the reactive IR/LiDAR policy (main.py:123-188) that the
-  report lists as future work (report.pdf p.5 §VI-2).
+* on a timer of ``map_update_interval`` seconds (slam_config.yaml:25) —
+  like slam_toolbox's map-publishing loop, whether or not scans were accepted
+  in between, so a robot that stopped moving still republishes and a late
+  subscriber gets a map — publishes ``/map`` as ``nav_msgs/OccupancyGrid``
+  (frame ``map_frame``, ``header.stamp`` and ``info.map_load_time`` = the
+  tick's time, resolution and origin from the grid, int8 -1/0/100 row-major,
+  ``data`` handed over as an ``array('b')`` built from the device copy's bytes
+  — no per-cell Python objects) and starts a frontier pass on the GPU
+  (``dm_frontiers_begin``).  The pass is collected without blocking the
+  callback thread (``dm_frontiers_poll`` from the scan / timer callbacks) and
+  then published: the clusters on ``/frontiers`` (``geometry_msgs/PoseArray``
+  of centroids) and, with exploration enabled, the chosen frontier goal on
+  ``/goal_pose`` (``geometry_msgs/PoseStamped``, the topic Nav2's navigator
+  and RViz's "2D Goal Pose" use) — the map-based replacement of the reactive
+  IR/LiDAR policy (main.py:123-188) that the report lists as future work
+  (report.pdf p.5 §VI-2);
+* with ``dm_devices`` naming several GPUs, the map is one sharded handle
+  (``dm_create_sharded``: row bands over those devices, the exchange inside
+  libdm) behind the same calls.
 
 All parameters come from the slam_toolbox parameter file the reference
 launches (``SlamParams.from_yaml``), plus the fixed grid size this build needs
@@ -176,6 +184,7 @@ class SlamParams:
     dm_origin_x: float = float("nan")     # NaN: map centred on the world origin
     dm_origin_y: float = float("nan")
     dm_device: int = 0
+    dm_devices: str = ""                  # e.g. "0,1,2,3": one map sharded in row bands over these GPUs
     dm_explore: bool = False              # publish /goal_pose after each map update
     dm_goal_min_size: int = 8
     dm_goal_distance_weight: float = 1.0
@@ -210,23 +219,35 @@ class SlamParams:
 
 
 class ScanGate:
-    """Which scans the mapping stage integrates, as slam_toolbox decides it
-    (slam_toolbox is not vendored and its version is not pinned — README.md:28
-    names the apt package ros-jazzy-slam-toolbox — so this restates its
-    published behaviour):
+    """Which scans the mapping stage integrates, as slam_toolbox decides it.
+    slam_toolbox is not vendored and its version is not pinned (README.md:28
+    names the apt package ros-jazzy-slam-toolbox), so this restates its
+    published sources (SlamToolbox::shouldProcessScan in
+    slam_toolbox_common.cpp, then the Karto mapper's Mapper::HasMovedEnough in
+    lib/karto_sdk/src/Mapper.cpp); parity with them is unpinned (SURVEY.md
+    §8(c)).  Two layers, in this order:
 
-    * the first scan is always processed;
-    * ``throttle_scans``: only every n-th scan is considered
-      (SlamToolbox::shouldProcessScan's scan counter);
-    * ``minimum_time_interval``: a scan closer in time than this to the last
-      processed one is dropped (shouldProcessScan);
-    * Karto's ``Mapper::HasMovedEnough``: the rest is processed only if the
-      laser turned by at least ``minimum_travel_heading`` (normalised angle)
-      or moved at least ``minimum_travel_distance`` since the last processed
-      scan.
+    1. slam_toolbox's front gate (``shouldProcessScan``; its scan counter counts
+       every scan offered, the first included):
+       * the first scan is always processed;
+       * ``throttle_scans``: dropped unless counter % throttle_scans == 0;
+       * ``minimum_time_interval``: dropped if closer in time than this to the
+         last scan that passed this gate;
+       * dropped if it moved less than ``0.8 * minimum_travel_distance²``
+         (squared, "within 10 % for correction error") from that scan's
+         pose, or while the counter is below 5 (warm-up).  A robot turning
+         in place is therefore never integrated, whatever it turned.
+    2. Karto's ``HasMovedEnough`` against the last *processed* scan: processed
+       if ``minimum_time_interval`` has passed, or the laser turned by
+       ``minimum_travel_heading`` (normalised angle), or moved
+       ``minimum_travel_distance`` (squared, less Karto's KT_TOLERANCE 1e-9).
+       After layer 1 the time test already holds, so this layer only matters
+       when the thresholds are configured differently for the two.
 
     The values of the reference's slam_config.yaml (lines 23, 28, 37, 38) are
     ``SlamParams``' defaults."""
+
+    KT_TOLERANCE = 1e-9
 
     def __init__(self, throttle_scans=1, minimum_time_interval=0.5, minimum_travel_distance=0.1,
                  minimum_travel_heading=0.1):
@@ -235,39 +256,70 @@ class ScanGate:
         self.min_d2 = float(minimum_travel_distance) ** 2
         self.min_heading = float(minimum_travel_heading)
         self.counter = 0
-        self.last = None  # (stamp, x, y, yaw) of the last processed scan
+        self.front = None  # (stamp, x, y) of the last scan past slam_toolbox's gate
+        self.last = None   # (stamp, x, y, yaw) of the last processed scan (Karto)
 
     @classmethod
     def from_params(cls, p: SlamParams) -> "ScanGate":
         return cls(p.throttle_scans, p.minimum_time_interval, p.minimum_travel_distance,
                    p.minimum_travel_heading)
 
-    def accept(self, stamp: float, pose) -> bool:
-        x, y, yaw = (float(v) for v in pose)
+    def _front(self, stamp: float, x: float, y: float) -> bool:
         self.counter += 1
-        if self.last is None:
-            self.last = (stamp, x, y, yaw)
+        if self.front is None:
+            self.front = (stamp, x, y)
             return True
         if self.counter % self.throttle != 0:
             return False
-        t0, x0, y0, yaw0 = self.last
+        t0, x0, y0 = self.front
         if stamp - t0 < self.min_dt:
             return False
-        turned = abs(math.remainder(yaw - yaw0, 2.0 * math.pi)) >= self.min_heading
-        moved = (x - x0) ** 2 + (y - y0) ** 2 >= self.min_d2 - 1e-9  # Karto's KT_TOLERANCE
-        if not (turned or moved):
+        if (x - x0) ** 2 + (y - y0) ** 2 < 0.8 * self.min_d2 or self.counter < 5:
+            return False
+        self.front = (stamp, x, y)
+        return True
+
+    def _moved_enough(self, stamp: float, x: float, y: float, yaw: float) -> bool:
+        if self.last is None:
+            return True
+        t0, x0, y0, yaw0 = self.last
+        if stamp - t0 >= self.min_dt:
+            return True
+        if abs(math.remainder(yaw - yaw0, 2.0 * math.pi)) >= self.min_heading:
+            return True
+        return (x - x0) ** 2 + (y - y0) ** 2 >= self.min_d2 - self.KT_TOLERANCE
+
+    def accept(self, stamp: float, pose) -> bool:
+        x, y, yaw = (float(v) for v in pose)
+        if not self._front(stamp, x, y):
+            return False
+        if not self._moved_enough(stamp, x, y, yaw):
             return False
         self.last = (stamp, x, y, yaw)
         return True
 
 
+def parse_devices(spec) -> list[int]:
+    """dm_devices: "0,1,2,3" (or a list) -> [0, 1, 2, 3]; "" -> []."""
+    if isinstance(spec, (list, tuple)):
+        return [int(d) for d in spec]
+    return [int(d) for d in str(spec).replace(" ", "").split(",") if d != ""]
+
+
 class MappingNode:
-    """GPU mapping stage: /scan (+TF) -> /map + /frontiers (+ /goal_pose)."""
+    """GPU mapping stage: /scan (+TF) -> /map + /frontiers (+ /goal_pose).
+
+    Callbacks (all non-blocking on the GPU except the /map readback itself):
+    ``scan_cb`` per LaserScan, ``timer_cb`` every ``map_update_interval``
+    seconds, ``poll_frontiers`` whenever convenient (the rclpy wiring in
+    ``main`` runs it on a short timer)."""
 
     def __init__(self, params: SlamParams | None = None, pose_provider=None, map_publisher=None,
                  frontier_publisher=None, goal_publisher=None, clock=time.monotonic, gate: bool = True,
-                 **overrides):
-        """`overrides` set SlamParams fields (tests: dm_width=..., ...)."""
+                 mapper=None, **overrides):
+        """`overrides` set SlamParams fields (tests: dm_width=..., ...).
+        `mapper`: an object with OccupancyMapper's interface to use instead of
+        creating one (tests inject CPU stand-ins)."""
         p = params or SlamParams()
         for k, v in overrides.items():
             if not hasattr(p, k):
@@ -275,7 +327,13 @@ class MappingNode:
             setattr(p, k, v)
         self.slam = p
         self.params = p.grid_params()
-        self.mapper = OccupancyMapper(self.params, device=int(p.dm_device))
+        if mapper is None:
+            devices = parse_devices(p.dm_devices)
+            if len(devices) > 1:
+                mapper = OccupancyMapper(self.params, devices=devices)
+            else:
+                mapper = OccupancyMapper(self.params, device=devices[0] if devices else int(p.dm_device))
+        self.mapper = mapper
         self.map_update_interval = float(p.map_update_interval)
         self.gate = ScanGate.from_params(p) if gate else None
         self.pose_provider = pose_provider
@@ -284,6 +342,7 @@ class MappingNode:
         self.goal_pub = goal_publisher or ListPublisher("/goal_pose")
         self.clock = clock
         self._last_publish = -math.inf
+        self._pass_stamp = None  # stamp of the frontier pass in flight (None: none)
         self.latest_scan = None
         self.latest_pose = None
         self.scans_seen = 0
@@ -295,6 +354,7 @@ class MappingNode:
     def scan_cb(self, msg):
         self.latest_scan = msg
         self.scans_seen += 1
+        self.poll_frontiers()
         pose = self.pose_provider(msg) if self.pose_provider is not None else None
         if pose is None:
             return  # no transform yet: slam_toolbox drops such scans too
@@ -305,9 +365,16 @@ class MappingNode:
         u, _ = self.mapper.integrate_scan(msg, pose)
         self.updates += u
         self.scans_integrated += 1
-        now = self.clock()
-        if now - self._last_publish >= self.map_update_interval:
-            self.publish_map(stamp=now)
+
+    def timer_cb(self):
+        """The map_update_interval timer: publish /map and start a frontier
+        pass, independent of scan gating.  Before the first integrated scan
+        there is no map (slam_toolbox has no grid before its first processed
+        scan either)."""
+        self.poll_frontiers()
+        if self.scans_integrated == 0:
+            return
+        self.publish_map(stamp=self.clock())
 
     def occupancy_grid(self, stamp: float = 0.0):
         st = self.mapper.state()
@@ -317,6 +384,8 @@ class MappingNode:
         if HAVE_ROS:  # pragma: no cover
             msg = _RosOccupancyGrid()
             msg.header.frame_id = self.slam.map_frame
+            msg.header.stamp = time_msg(stamp)
+            msg.info.map_load_time = time_msg(stamp)
             msg.info.resolution = float(p.resolution)
             msg.info.width = int(p.width)
             msg.info.height = int(p.height)
@@ -333,12 +402,17 @@ class MappingNode:
             data=data)
 
     def frontier_clusters(self) -> list:
+        """Synchronous frontier extraction of the map as it is now."""
         fr = self.mapper.frontiers()
         self.last_frontiers = fr.clusters
-        return [FrontierCluster(int(c["label"]), int(c["size"]), float(c["cx_m"]), float(c["cy_m"]))
-                for c in fr.clusters]
+        return self._cluster_msgs(fr.clusters)
 
-    def choose_goal(self):
+    @staticmethod
+    def _cluster_msgs(clusters) -> list:
+        return [FrontierCluster(int(c["label"]), int(c["size"]), float(c["cx_m"]), float(c["cy_m"]))
+                for c in clusters]
+
+    def choose_goal(self, stamp: float | None = None):
         """The frontier goal for the robot at its latest pose, chosen on the
         device over the last published frontier clusters (dm_assign_goals;
         policy: dm.goals): PoseStamped in the map frame facing the goal, or
@@ -353,19 +427,39 @@ class MappingNode:
         if g is None:
             return None
         gx, gy = g[1]
-        msg = PoseStamped(header=Header(stamp=self._last_publish, frame_id=s.map_frame))
+        msg = PoseStamped(header=Header(stamp=self._last_publish if stamp is None else stamp,
+                                        frame_id=s.map_frame))
         msg.pose.position = Point(gx, gy, 0.0)
         msg.pose.orientation = quaternion_from_yaw(math.atan2(gy - y, gx - x))
         return msg
 
     def publish_map(self, stamp: float = 0.0):
+        """Publish /map now and start the frontier pass of this map (its
+        clusters are published by poll_frontiers once the GPU is done)."""
         self._last_publish = stamp
         self.map_pub.publish(self.occupancy_grid(stamp))
-        self.frontier_pub.publish(self.frontier_clusters())
+        if self._pass_stamp is not None:
+            self.poll_frontiers(wait=True)  # the previous tick's pass (long done by now)
+        self.mapper.frontiers_begin()
+        self._pass_stamp = stamp
+
+    def poll_frontiers(self, wait: bool = False) -> bool:
+        """Publish the frontier pass in flight if the GPU has finished it
+        (never blocks unless `wait`).  Returns True if it published."""
+        if self._pass_stamp is None:
+            return False
+        if not wait and not self.mapper.frontiers_ready():
+            return False
+        stamp, self._pass_stamp = self._pass_stamp, None
+        fr = self.mapper.frontiers_end()
+        clusters = fr.clusters if fr is not None else self.mapper.frontiers().clusters  # overflowed: rerun
+        self.last_frontiers = clusters
+        self.frontier_pub.publish(self._cluster_msgs(clusters))
         if self.slam.dm_explore:
-            goal = self.choose_goal()
+            goal = self.choose_goal(stamp)
             if goal is not None:
                 self.goal_pub.publish(goal)
+        return True
 
     def map_image_png(self) -> bytes:
         """What get_map_image serves (main.py:256-273), rendered on the GPU
@@ -379,6 +473,14 @@ class MappingNode:
 
     def destroy_node(self):
         self.mapper.close()
+
+
+def time_msg(t: float):  # pragma: no cover - needs ROS 2
+    """Seconds -> builtin_interfaces/Time."""
+    from builtin_interfaces.msg import Time
+
+    sec = int(math.floor(t))
+    return Time(sec=sec, nanosec=int(round((t - sec) * 1e9)) % 1_000_000_000)
 
 
 def main(args=None):  # pragma: no cover - needs ROS 2
@@ -421,6 +523,7 @@ def main(args=None):  # pragma: no cover - needs ROS 2
         def publish(self, clusters):
             pa = PoseArray()
             pa.header.frame_id = sp.map_frame
+            pa.header.stamp = node.get_clock().now().to_msg()
             for c in clusters:
                 ps = RosPose()
                 ps.position.x, ps.position.y = c.x, c.y
@@ -440,6 +543,9 @@ def main(args=None):  # pragma: no cover - needs ROS 2
     mn = MappingNode(sp, pose_provider=lookup, map_publisher=map_pub, frontier_publisher=_FrontierAdapter(),
                      goal_publisher=_GoalAdapter(), clock=lambda: node.get_clock().now().nanoseconds * 1e-9)
     node.create_subscription(RosLaserScan, sp.scan_topic, mn.scan_cb, 10)
+    # slam_toolbox publishes the map on its own period, not per scan
+    node.create_timer(sp.map_update_interval, mn.timer_cb)
+    node.create_timer(0.01, mn.poll_frontiers)  # frontiers go out as soon as the GPU pass is done
     try:
         rclpy.spin(node)
     finally:

@@ -29,14 +29,26 @@ the global map, rows_r a multiple of 64 except for the last band.
      all-gathered (counts first, then padded records), merged by final
      label with exact int64 sums, filtered by min_frontier_size and sorted.
 All messages are KB-MB: latency-bound on xGMI, no ring all-reduce needed.
+
+Failure handling (the reference's analogue is the bounded
+connect thread, pi/src/thymio_project/thymio_project/main.py:138-148): every
+collective is issued with ``async_op=True`` and waited for at most
+``timeout`` seconds; on the device path the host polls an event recorded
+after the collectives instead of blocking in the merge's synchronisation.
+A peer that died, raised or stalled therefore surfaces on every other rank
+as ``DmError(DM_ERR_COLLECTIVE)`` within the timeout, never as a hang; the
+error is sticky (the communicator may hold a half-finished collective), so
+every later call on that mapper raises it again.
 """
 from __future__ import annotations
 
 import collections
+import time
+from datetime import timedelta
 
 import numpy as np
 
-from ._ffi import CLUSTER_DTYPE, DM_TILE, DmParams, load_library
+from ._ffi import CLUSTER_DTYPE, DM_ERR_COLLECTIVE, DM_TILE, DmError, DmParams, load_library
 from .grid import Frontiers, OccupancyMapper
 
 
@@ -147,9 +159,13 @@ class ShardedMapper:
     rank `rank`'s part.  With world_size == 1 it is a plain OccupancyMapper."""
 
     def __init__(self, params: DmParams, rank: int = 0, world_size: int = 1, device: int = 0,
-                 group=None, band=None):
+                 group=None, band=None, timeout: float = 300.0):
+        """`timeout`: seconds any collective (or the device work queued behind
+        one) may take before this rank gives up with DM_ERR_COLLECTIVE."""
         self.params = DmParams.from_buffer_copy(params)
         self.rank, self.world_size, self.group = rank, world_size, group
+        self.timeout = float(timeout)
+        self.failed = None  # sticky DM_ERR_COLLECTIVE message
         self.min_size = int(params.min_frontier_size)
         if world_size == 1:
             bp = DmParams.from_buffer_copy(params)
@@ -189,6 +205,51 @@ class ShardedMapper:
                 self._bufs = {}
                 self.fallbacks = 0
 
+    # -- collective failure handling ----------------------------------------
+    def _check(self):
+        if self.failed is not None:
+            raise DmError(DM_ERR_COLLECTIVE, self.failed)
+
+    def _fail(self, what: str):
+        self.failed = f"rank {self.rank}/{self.world_size}: {what} (sharded map unusable; recreate it)"
+        raise DmError(DM_ERR_COLLECTIVE, self.failed)
+
+    def _wait(self, work, what: str):
+        """Wait for one async collective at most self.timeout seconds (gloo:
+        host-side; RCCL: orders the current stream, the host deadline is
+        enforced by _drain)."""
+        try:
+            ok = work.wait(timeout=timedelta(seconds=self.timeout))
+        except Exception as e:  # gloo: a timed-out or aborted peer raises here
+            self._fail(f"{what} failed: {e}")
+        if ok is False:
+            self._fail(f"{what} did not complete within {self.timeout:g} s")
+
+    def _all_gather(self, out, t, what: str):
+        self._check()
+        try:
+            work = self._dist.all_gather_into_tensor(out, t, group=self.group, async_op=True)
+        except Exception as e:
+            self._fail(f"{what} failed: {e}")
+        self._wait(work, what)
+
+    def _poll(self, ev, what: str):
+        """Wait (host side, at most self.timeout) for a CUDA/HIP event recorded
+        after collectives, so no later blocking synchronisation can wait on a
+        collective a dead peer never joins."""
+        deadline = time.monotonic() + self.timeout
+        while not ev.query():
+            if time.monotonic() > deadline:
+                self._fail(f"{what}: device exchange did not complete within {self.timeout:g} s")
+            time.sleep(2e-5)
+
+    def _drain(self, what: str, stream=None):
+        import torch
+
+        ev = torch.cuda.Event()
+        ev.record(stream if stream is not None else self.stream)
+        self._poll(ev, what)
+
     # -- integration ------------------------------------------------------
     def scan_mask(self, poses) -> np.ndarray:
         """Scans whose max-range disk reaches this band's rows."""
@@ -201,6 +262,7 @@ class ShardedMapper:
         return ~((y < ylo) | (y > yhi))  # NaN poses are kept (libdm skips them)
 
     def integrate(self, poses, ranges, angle_min, angle_increment):
+        self._check()
         poses = np.asarray(poses, np.float64).reshape(-1, 3)
         ranges = np.asarray(ranges, np.float32)
         if ranges.ndim != 2:
@@ -220,7 +282,9 @@ class ShardedMapper:
             t = t.to(self._device)
         t = t.reshape(1, -1)
         out = torch.empty((self.world_size, t.shape[1]), dtype=t.dtype, device=t.device)
-        self._dist.all_gather_into_tensor(out, t, group=self.group)
+        self._all_gather(out, t, "all-gather")
+        if self._nccl:
+            self._drain("all-gather", torch.cuda.current_stream(self._device))
         return out.cpu().numpy().reshape((self.world_size,) + arr.shape)
 
     def exchange_halos(self):
@@ -241,10 +305,10 @@ class ShardedMapper:
     def _gather_dev(self, t, out):
         """all-gather a device tensor into out ([P * n], rank order)."""
         if self._nccl:
-            self._dist.all_gather_into_tensor(out, t, group=self.group)
+            self._all_gather(out, t, "device all-gather")
         else:  # gloo rehearsal on GPUs: host-staged
             o = self._torch.empty(out.numel(), dtype=t.dtype)
-            self._dist.all_gather_into_tensor(o, t.cpu(), group=self.group)
+            self._all_gather(o, t.cpu(), "all-gather")
             out.copy_(o)
 
     def _device_enqueue(self):
@@ -284,6 +348,7 @@ class ShardedMapper:
 
     def _frontiers_device(self):
         gexp = self._device_enqueue()
+        self._drain("frontier exchange")
         with self._torch.cuda.stream(self.stream):
             res = self.band.merge_bands(gexp.data_ptr(), self.world_size, self.rec_cap, self.min_size)
         fr = self._device_finish(res)
@@ -294,6 +359,7 @@ class ShardedMapper:
     def frontiers(self, want_mask=False, want_labels=False) -> Frontiers:
         """Frontiers of the map as it is now (synchronous; passes started with
         frontiers_begin() may still be in flight)."""
+        self._check()
         if self.world_size == 1:
             return self.band.frontiers(want_mask=want_mask, want_labels=want_labels)
         if self._dev_path and not (want_mask or want_labels):
@@ -313,6 +379,7 @@ class ShardedMapper:
         would have), and integrate calls may be made in between.  Up to
         dm_max_passes_in_flight() passes may be in flight (libdm's readback
         ring); frontiers_end() collects the oldest."""
+        self._check()
         if len(self._pending) >= self.max_in_flight:
             raise RuntimeError(f"{len(self._pending)} frontiers_begin() passes are in flight: "
                                "call frontiers_end() first")
@@ -323,7 +390,9 @@ class ShardedMapper:
             gexp = self._device_enqueue()
             with self._torch.cuda.stream(self.stream):
                 self.band.merge_bands_begin(gexp.data_ptr(), self.world_size, self.rec_cap, self.min_size)
-            self._pending.append(("merge", None))
+            ev = self._torch.cuda.Event()
+            ev.record(self.stream)  # after this pass's collectives and merge
+            self._pending.append(("merge", ev))
         else:  # host exchange (or a non-libdm band): computed now
             self._pending.append(("done", self.frontiers()))
 
@@ -334,10 +403,12 @@ class ShardedMapper:
         record overflowed: capacities are grown now).  A None pass is not
         recomputed here — the map may have changed since it started; call
         frontiers() for the map as it is now."""
+        self._check()
         kind, res = self._pending.popleft()
         if kind == "band":
             return self.band.frontiers_end()
         if kind == "merge":
+            self._poll(res, "frontier exchange")
             return self._device_finish(self.band.merge_bands_end())
         return res
 

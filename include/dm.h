@@ -51,6 +51,10 @@ extern "C" {
 #define DM_ERR_PIPELINE (-9)   /* a cross-stream hand-off of the overlapped pipeline (dm_set_overlap)
                                   timed out: the map update it guarded was skipped, so the map
                                   misses batches; sticky until dm_reset */
+#define DM_ERR_COLLECTIVE (-10) /* a cross-device exchange of a sharded map failed or did not finish
+                                  within its timeout (a peer copy of a dm_create_sharded handle; the
+                                  RCCL collectives of the multi-process layer, dm/sharded.py);
+                                  sticky: the sharded map must be recreated */
 
 /* Tile edge (cells) used by the kernels; band_row0 must be a multiple of it. */
 #define DM_TILE 64
@@ -187,6 +191,12 @@ int dm_frontiers(dm_grid* g, uint8_t* mask, int64_t* labels, dm_cluster* out,
  * integrating scans while the last frontier request completes. */
 int dm_frontiers_begin(dm_grid* g);
 int dm_frontiers_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out);
+/* Non-blocking test of the oldest asynchronous pass (dm_frontiers_begin or
+ * dm_merge_bands_begin): *ready = 1 when it has completed (its _end call then
+ * returns without waiting), else 0.  DM_ERR_INVALID_ARG if no pass is in
+ * flight.  Lets a ROS callback thread publish frontiers without ever
+ * blocking on the GPU. */
+int dm_frontiers_poll(dm_grid* g, int32_t* ready);
 /* The number of asynchronous passes (dm_frontiers_begin /
  * dm_merge_bands_begin) a handle holds in flight: the readback ring's size. */
 int dm_max_passes_in_flight(void);
@@ -205,6 +215,35 @@ int dm_max_passes_in_flight(void);
  * can cause it) skips the map update it guarded and every later call that
  * reads results returns DM_ERR_PIPELINE until dm_reset. */
 int dm_set_overlap(dm_grid* g, int32_t on);
+
+/* ---- One map sharded over several devices of this process (SURVEY.md §8(b)
+ * "sharded variants: dm_create_sharded(..., int nranks, const int* devices)
+ * with the same calls"; §8(e) row bands).  Band r (rows from
+ * dm_sharded_band_rows: equal multiples of 64, the last ragged) lives on
+ * HIP device devices[r]; a device may repeat (tests run {0, 0, ...} on one
+ * GPU).  p covers the whole grid (band_row0 = 0, band_rows = 0).  The handle
+ * takes the calls of a dm_create handle — dm_integrate(_async / _device),
+ * dm_last_counts / _stats, dm_get_state / _logodds, dm_set_state / _logodds,
+ * dm_frontiers (mask and labels are whole-map arrays with global min-index
+ * labels), dm_frontiers_begin / _end / _poll, dm_assign_goals,
+ * dm_map_image, dm_save / dm_load (the same checkpoint format as one
+ * full-map handle), dm_reset, dm_set_overlap, dm_synchronize, dm_profile_*,
+ * dm_ld06_to_scans(_device), dm_destroy — with results identical to one
+ * dm_create handle of the same params.  Integration sends each band the
+ * scans whose max-range disk reaches it; frontier extraction exchanges halo
+ * rows and band export records between the devices with peer copies (xGMI)
+ * and merges on band 0's device (dm_merge_bands).  The multi-process building
+ * blocks below (halos, edge rows / labels, exports, merges, dm_set_stream)
+ * return DM_ERR_INVALID_ARG on such a handle.  Replaces: slam_toolbox's
+ * single map thread for a map too large (or too many robots) for one GPU;
+ * the caller is the ROS node wired at pc_server.launch.py:12-19. */
+int dm_create_sharded(dm_grid** out, const dm_params* p, int32_t nranks, const int32_t* devices);
+/* The rows [*row0, *row0 + *rows) of band `rank` of `nranks` (the partition
+ * of dm_create_sharded and of the multi-process layer, dm/sharded.py). */
+int dm_sharded_band_rows(int64_t height, int32_t nranks, int32_t rank, int64_t* row0, int64_t* rows);
+/* nranks of a handle (1 for dm_create handles) and the export record
+ * capacity its exchange uses now (0 for dm_create handles). */
+int dm_sharded_info(const dm_grid* g, int32_t* nranks, int64_t* rec_cap);
 
 /* Sharding support (row bands).  Halo rows are the global
  * rows band_row0-1 (top, "above" = lower row index) and band_row0+band_rows
@@ -304,7 +343,8 @@ int dm_map_image(dm_grid* g, uint8_t* out);
  * first, ties to the smaller label; robots choose in order, each skipping the
  * clusters earlier robots took.  out_index[r] = index into that result's
  * label-sorted list (-1: none), out_xy[2r], [2r+1] = its centroid (NaN if
- * none).  n_robots <= 256.  DM_ERR_INVALID_ARG if no result is on the device
+ * none).  n_robots <= 256; distance_weight >= 0 (DM_ERR_INVALID_ARG otherwise).
+ * DM_ERR_INVALID_ARG if no result is on the device
  * (none collected yet, or a later pass reused its readback slot). */
 int dm_assign_goals(dm_grid* g, const double* robots_xy, int32_t n_robots, int64_t min_size,
                     double distance_weight, double min_distance, int64_t* out_index, double* out_xy);

@@ -23,7 +23,9 @@ if _PKG not in sys.path:
 from dm._ffi import CLUSTER_DTYPE, DmCluster, DmParams  # noqa: E402  (types only)
 
 LIB_PATH = os.path.join(_HERE, "liboracle.so")
+LIB_MT_PATH = os.path.join(_HERE, "liboracle_mt.so")
 _lib = None
+_lib_mt = None
 
 
 def build() -> str:
@@ -54,6 +56,28 @@ def lib() -> ctypes.CDLL:
         L.or_ld06_to_scan.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int, vp, vp]
         _lib = L
     return _lib
+
+
+def lib_mt() -> ctypes.CDLL:
+    """The OpenMP restatement (dm_oracle_mt.c): bench.py's strong-CPU line."""
+    global _lib_mt
+    if _lib_mt is None:
+        if not os.path.exists(LIB_MT_PATH):
+            build()
+        L = ctypes.CDLL(LIB_MT_PATH)
+        vp = ctypes.c_void_p
+        P = ctypes.POINTER(DmParams)
+        L.or_mt_create.argtypes = [P, ctypes.c_int]
+        L.or_mt_create.restype = vp
+        L.or_mt_destroy.argtypes = [vp]
+        L.or_mt_destroy.restype = None
+        L.or_mt_threads.argtypes = [vp]
+        L.or_mt_integrate.argtypes = [vp, P, vp, vp, ctypes.c_int32, vp, ctypes.c_int32, vp,
+                                      ctypes.c_float, ctypes.c_float, vp, vp]
+        L.or_mt_frontiers.argtypes = [vp, P, vp, vp, vp, vp, vp, vp, ctypes.c_int64,
+                                      ctypes.POINTER(ctypes.c_int64)]
+        _lib_mt = L
+    return _lib_mt
 
 
 def _ptr(a: np.ndarray | None):
@@ -137,6 +161,57 @@ class OracleMap:
         img = np.zeros((R, W), np.uint8)
         lib().or_map_image(_ptr(self.state), R, W, _ptr(img))
         return img
+
+
+class OracleMapMT(OracleMap):
+    """OracleMap on every host core (dm_oracle_mt.c, OpenMP): the same
+    results bit for bit, for the strong-CPU baseline."""
+
+    def __init__(self, p: DmParams, threads: int = 0):
+        super().__init__(p)
+        self._h = lib_mt().or_mt_create(ctypes.byref(self.p), int(threads))
+        if not self._h:
+            raise MemoryError("or_mt_create")
+        self.threads = int(lib_mt().or_mt_threads(self._h))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib_mt().or_mt_destroy(self._h)
+            self._h = None
+
+    def integrate(self, poses, ranges, angle_min, angle_increment):
+        poses = np.ascontiguousarray(poses, dtype=np.float64).reshape(-1, 3)
+        ranges = np.ascontiguousarray(ranges, dtype=np.float32)
+        if ranges.ndim != 2:
+            ranges = ranges.reshape(poses.shape[0], -1)
+        S, N = ranges.shape
+        U = ctypes.c_uint64(0)
+        T = ctypes.c_uint64(0)
+        rc = lib_mt().or_mt_integrate(self._h, ctypes.byref(self.p), _ptr(self.L), _ptr(self.state), S,
+                                      _ptr(poses), N, _ptr(ranges), float(angle_min), float(angle_increment),
+                                      ctypes.byref(U), ctypes.byref(T))
+        if rc != 0:
+            raise MemoryError(f"or_mt_integrate rc={rc}")
+        return int(U.value), int(T.value)
+
+    def frontiers(self, halo_before=None, halo_after=None, want_mask=True, want_labels=True,
+                  cap=1 << 20):
+        R, W = self.state.shape
+        mask = np.zeros((R, W), np.uint8) if want_mask else None
+        labels = np.zeros((R, W), np.int64) if want_labels else None
+        hb = None if halo_before is None else np.ascontiguousarray(halo_before, np.int8)
+        ha = None if halo_after is None else np.ascontiguousarray(halo_after, np.int8)
+        out = (DmCluster * max(1, cap))()
+        n = ctypes.c_int64(0)
+        rc = lib_mt().or_mt_frontiers(self._h, ctypes.byref(self.p), _ptr(self.state), _ptr(hb), _ptr(ha),
+                                      _ptr(mask), _ptr(labels), ctypes.cast(out, ctypes.c_void_p), cap,
+                                      ctypes.byref(n))
+        if rc not in (0, -5):
+            raise MemoryError(f"or_mt_frontiers rc={rc}")
+        k = min(int(n.value), cap)
+        clusters = np.frombuffer(bytes(out)[: k * ctypes.sizeof(DmCluster)],
+                                 dtype=np.dtype(CLUSTER_DTYPE)).copy()
+        return mask, labels, clusters
 
 
 def ld06_to_scans(points, offsets, n_beams, laser_scan_dir=True):

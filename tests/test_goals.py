@@ -29,3 +29,14 @@ def test_assign_distinct_goals():
     c = clusters([(1, 40, 0.0, 5.0), (2, 40, 0.0, -5.0), (3, 1, 9.0, 9.0)])
     goals = assign_goals(c, [(0.0, 4.0), (0.0, -4.0), (0.0, 0.0)], min_size=8)
     assert goals[0][0] == 0 and goals[1][0] == 1 and goals[2] is None
+
+
+def test_negative_distance_weight_refused():
+    """A negative weight makes util negative or infinite; dm_assign_goals
+    refuses it (its device keys order positive utils only), and so does the
+    host restatement."""
+    import pytest
+
+    c = clusters([(10, 5, 1.0, 1.0)])
+    with pytest.raises(ValueError):
+        assign_goals(c, [(0.0, 0.0)], distance_weight=-1.0)

@@ -87,5 +87,9 @@ def test_goals_need_a_collected_result():
         assert m.assign_goals([(0.0, 0.0), (1.0, 1.0)]) == [None, None]
         with pytest.raises(dm.DmError):
             m.assign_goals(np.zeros((257, 2)))
+        # util ranks by IEEE bits, valid for util > 0 only: w < 0 is refused
+        # (the host restatement refuses it the same way)
+        with pytest.raises(dm.DmError):
+            m.assign_goals([(0.0, 0.0)], distance_weight=-0.5)
     finally:
         m.close()

@@ -211,6 +211,37 @@ def test_async_host_inputs_pipelined(oracle_lib, overlap):
         assert m.last_counts() == om2.integrate(*batches[-1], amin, inc)  # U, T of the last call
 
 
+@pytest.mark.parametrize("overlap", [False, True])
+def test_async_host_inputs_reused_without_sync(oracle_lib, overlap):
+    """dm.h's staging contract without any synchronising call in between:
+    each pinned ranges buffer is overwritten as soon as the second
+    dm_integrate_async after the one that used it has returned (no
+    frontiers_end, no dm_synchronize in between), so a copy still pending
+    then would read a later batch's ranges; the final map must equal the
+    oracle's (the staging event once covered only the pose copy)."""
+    import torch
+
+    p, batches, amin, inc = cases.world_case(53, 1200, 1100, 0.05, 8, 1024, 9, region_frac=0.6)
+    om = oracle_lib.OracleMap(p)
+    for poses, ranges in batches:
+        om.integrate(poses, ranges, amin, inc)
+    S, N = batches[0][1].shape
+    # three buffers: call k's ranges must stay unchanged until call k+2 has
+    # returned, so pinned[k % 3] (last read by call k-3) is free once call k-1
+    # has returned; a copy of call k-3 still pending would read batch k
+    pinned = [torch.empty((S, N), dtype=torch.float32).pin_memory() for _ in range(3)]
+    with dm.OccupancyMapper(p) as m:
+        m.set_overlap(overlap)
+        for k, (poses, ranges) in enumerate(batches):
+            buf = pinned[k % 3]
+            buf.numpy()[...] = ranges
+            m.integrate_async(poses, buf.data_ptr(), S, N, amin, inc)
+        m.synchronize()  # the contract's other release point
+        for b in pinned:
+            b.numpy()[...] = np.nan
+        assert_map_equal(m, om)
+
+
 def test_front_end_gate_timeout_is_a_sticky_error(oracle_lib, monkeypatch):
     """A timed-out front-end hand-off (fault injection: DM_FAULT_GATE=1 makes
     the gate wait for a sequence number that never comes, ~10 us) must not

@@ -40,9 +40,12 @@ def test_mapping_node_publishes_oracle_map(oracle_lib):
             t[0] = 0.7 * k
             node.scan_cb(msg)
             om.integrate(poses, ranges, amin, inc)
-        node.publish_map(stamp=t[0])
-        assert len(node.map_pub.messages) >= 2  # interval-driven + explicit
+        assert node.map_pub.messages == []  # /map comes from the timer, not from scans
+        node.timer_cb()  # the map_update_interval tick
+        assert node.poll_frontiers(wait=True)  # the GPU frontier pass the tick started
+        assert len(node.map_pub.messages) == 1
         grid = node.map_pub.messages[-1]
+        assert grid.header.stamp == t[0] and grid.info.map_load_time == t[0]
         assert (grid.info.width, grid.info.height) == (400, 400)
         assert grid.info.resolution == 0.05 and grid.header.frame_id == "map"
         assert grid.data.typecode == "b" and len(grid.data) == 400 * 400
@@ -105,6 +108,8 @@ def test_exploration_goal_topic(oracle_lib):
             node.scan_cb(msg)
             om.integrate(poses, ranges, amin, inc)
         node.publish_map(stamp=1.0)
+        while not node.poll_frontiers():  # frontiers_ready() polls the GPU pass, never blocks
+            pass
         clusters = om.frontiers(want_mask=False, want_labels=False)[2]
         x, y, _ = batches[-1][0][0]
         exp = select_goal(clusters, (x, y), min_size=4, min_distance=0.3)

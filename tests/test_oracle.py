@@ -138,3 +138,31 @@ def test_oracle_golden_fixtures(oracle_lib):
         np.testing.assert_array_equal(mask, c["mask"])
         np.testing.assert_array_equal(labels, c["labels"])
         np.testing.assert_array_equal(clusters, c["clusters"])
+
+
+@pytest.mark.parametrize("seed,W,H,S,N,threads", [(31, 300, 260, 8, 720, 4), (32, 1000, 700, 16, 2048, 8),
+                                                  (33, 130, 70, 5, 500, 3)])
+def test_openmp_restatement_equals_single_thread(oracle_lib, seed, W, H, S, N, threads):
+    """dm_oracle_mt.c (bench.py's strong-CPU line) gives dm_oracle.c's
+    results bit for bit: U / T, L, state, mask, labels, clusters; also on a
+    band with halo rows and with a size filter."""
+    p = cases.make_params(W, H, min_frontier_size=1 + seed % 3)
+    one = oracle_lib.OracleMap(p)
+    mt = oracle_lib.OracleMapMT(p, threads=threads)
+    assert mt.threads == threads
+    for k in range(3):
+        poses, ranges, amin, inc = cases.random_scans(seed * 10 + k, p, S, N)
+        assert mt.integrate(poses, ranges, amin, inc) == one.integrate(poses, ranges, amin, inc)
+    np.testing.assert_array_equal(mt.L.view(np.uint32), one.L.view(np.uint32))
+    np.testing.assert_array_equal(mt.state, one.state)
+    for a, b in zip(mt.frontiers(), one.frontiers()):
+        np.testing.assert_array_equal(a, b)
+    # a band of the same map with halo rows
+    bp = cases.make_params(W, H, band_row0=64, band_rows=min(128, H - 64))
+    ob, mb = oracle_lib.OracleMap(bp), oracle_lib.OracleMapMT(bp, threads=threads)
+    st = one.state
+    ob.state[...] = st[64:64 + ob.state.shape[0]]
+    mb.state[...] = ob.state
+    ha = st[64 + ob.state.shape[0]] if 64 + ob.state.shape[0] < H else None
+    for a, b in zip(mb.frontiers(st[63], ha), ob.frontiers(st[63], ha)):
+        np.testing.assert_array_equal(a, b)

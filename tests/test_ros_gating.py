@@ -1,7 +1,8 @@
 """CPU: the ROS drop-in's parameters and scan gating (dm/ros_node.py) — the
-decisions of the stage it replaces (slam_toolbox's throttle_scans and
-minimum_time_interval, Karto's minimum_travel_distance / _heading;
-server/thymio_project/config/slam_config.yaml:23,28,37-38) on fake message
+decisions of the stage it replaces (slam_toolbox's shouldProcessScan front
+gate and Karto's HasMovedEnough over throttle_scans, minimum_time_interval,
+minimum_travel_distance / _heading; server/thymio_project/config/
+slam_config.yaml:23,28,37-38; restated, parity unpinned) on fake message
 streams, the parameter file, and the launch file's wiring."""
 import ast
 import math
@@ -43,23 +44,40 @@ def test_parameter_file_overrides(tmp_path):
 
 
 def test_gate_time_distance_heading():
-    g = ScanGate()  # slam_config.yaml values
+    """slam_toolbox's front gate, then Karto's HasMovedEnough (ScanGate's
+    docstring); the slam_config.yaml thresholds 0.5 s / 0.1 m / 0.1 rad."""
+    g = ScanGate()
     assert g.accept(0.0, (0, 0, 0))            # the first scan always
     assert not g.accept(0.3, (1.0, 0, 0))      # moved, but too soon (< 0.5 s)
-    assert not g.accept(0.6, (0.05, 0, 0))     # in time, but moved 5 cm, turned 0
-    assert g.accept(0.7, (0.1, 0, 0))          # moved the minimum 0.1 m
-    assert not g.accept(1.3, (0.1, 0.05, 0.05))  # 5 cm and 0.05 rad: neither enough
-    assert g.accept(1.4, (0.1, 0.0, 0.1))      # turned 0.1 rad
-    assert g.accept(2.0, (0.1, 0.0, 0.1 + 2 * math.pi - 0.15))  # heading difference wraps: 0.15 rad
-    assert not g.accept(2.6, (0.1, 0.0, 0.1 + 2 * math.pi - 0.1))  # 0.05 rad after wrapping
+    assert not g.accept(0.6, (0.05, 0, 0))     # in time, moved 5 cm < sqrt(0.8) * 0.1 m
+    assert not g.accept(0.7, (0.1, 0, 0))      # enough, but the 4th scan: warm-up (counter < 5)
+    assert g.accept(0.8, (0.1, 0, 0))          # 5th scan, 0.1 m, 0.8 s
+    assert not g.accept(1.5, (0.1, 0, 1.0))    # turned 1 rad in place: no translation, rejected
+    assert not g.accept(2.0, (0.1 + 0.0894, 0, 1.0))  # 0.0894^2 < 0.8 * 0.01
+    assert g.accept(2.1, (0.1 + 0.0895, 0, 1.0))      # 0.0895^2 >= 0.8 * 0.01 (within 10 %)
+
+
+def test_karto_layer_heading_and_wrap():
+    """Karto's HasMovedEnough on its own (it only decides when its thresholds
+    differ from the front gate's): time, or heading (normalised), or
+    distance (less KT_TOLERANCE)."""
+    g = ScanGate()
+    g.last = (0.0, 0.0, 0.0, 0.1)
+    assert g._moved_enough(0.5, 0.0, 0.0, 0.1)                          # 0.5 s passed
+    assert not g._moved_enough(0.4, 0.05, 0.0, 0.15)                    # 5 cm, 0.05 rad
+    assert g._moved_enough(0.4, 0.0, 0.0, 0.2)                          # turned 0.1 rad
+    assert g._moved_enough(0.4, 0.0, 0.0, 0.1 + 2 * math.pi - 0.15)     # wraps: 0.15 rad
+    assert not g._moved_enough(0.4, 0.0, 0.0, 0.1 + 2 * math.pi - 0.05)  # wraps: 0.05 rad
+    assert g._moved_enough(0.4, 0.1, 0.0, 0.1)                          # 0.1 m
 
 
 def test_gate_throttle():
     g = ScanGate(throttle_scans=3, minimum_time_interval=0.0, minimum_travel_distance=0.0,
                  minimum_travel_heading=0.0)
     got = [g.accept(float(k), (k, 0, 0)) for k in range(10)]
-    # first scan, then every third scan of the counter (3, 6, 9 -> calls 2, 5, 8)
-    assert got == [True, False, True, False, False, True, False, False, True, False]
+    # first scan, then every third scan of the counter once past the warm-up
+    # (counter 3 < 5 is dropped; 6 and 9 pass -> calls 5 and 8)
+    assert got == [True, False, False, False, False, True, False, False, True, False]
 
 
 def test_gate_stream_rate():

@@ -84,3 +84,90 @@ def test_merge_clusters_units():
     assert m["label"].tolist() == [1] and m["size"].tolist() == [8]
     assert m["sum_x"].tolist() == [12] and m["sum_y"].tolist() == [11]
     assert len(merge_clusters(recs, edges, p, 9)) == 0
+
+
+def _failing_worker(rank, world, port, mode, timeout, out):
+    """Rank 1 fails before the frontier exchange (raises and exits, or
+    stalls); rank 0 must get DmError(DM_ERR_COLLECTIVE) within the timeout,
+    and keep getting it (sticky)."""
+    import sys
+    import time
+    for p in (HERE, os.path.join(os.path.dirname(HERE), "oracle"),
+              os.path.join(os.path.dirname(HERE), "distributed-autonomous-exploration-and-mapping_amd")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    import cases as cs
+    from dm import DmError
+    from dm._ffi import DM_ERR_COLLECTIVE
+    from dm.sharded import ShardedMapper, band_params
+    from oracle_band import OracleBand
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    p = cs.make_params(200, 256)
+    sm = ShardedMapper(p, rank=rank, world_size=world, band=OracleBand(band_params(p, world, rank)),
+                       group=dist.group.WORLD, timeout=timeout)
+    poses, ranges, amin, inc = cs.random_scans(5, p, 4, 200)
+    sm.integrate(poses, ranges, amin, inc)
+    if rank == 1:
+        if mode == "raise":
+            raise RuntimeError("rank 1 fails before the all-gather")  # the process exits
+        time.sleep(4 * timeout)  # stalls past rank 0's deadline
+        os._exit(0)
+    t0 = time.monotonic()
+    try:
+        sm.frontiers()
+        out[rank] = ("no error", 0.0, 0)
+    except DmError as e:
+        dt = time.monotonic() - t0
+        try:
+            sm.frontiers()
+            sticky = False
+        except DmError as e2:
+            sticky = e2.code == DM_ERR_COLLECTIVE
+        out[rank] = (e.code == DM_ERR_COLLECTIVE, dt, sticky)
+    os._exit(0)  # a half-finished collective is pending: no orderly teardown
+
+
+@pytest.mark.parametrize("mode", ["raise", "stall"])
+def test_collective_failure_is_a_bounded_dm_error(mode):
+    """SURVEY §5 failure detection: a dead or stalled peer makes the other
+    rank's frontier exchange fail with DM_ERR_COLLECTIVE within the timeout
+    (reference analogue: the bounded join(timeout=3) connect pattern,
+    pi/src/thymio_project/thymio_project/main.py:138-148)."""
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    port = _free_port()
+    timeout = 2.0
+    procs = [ctx.Process(target=_failing_worker, args=(r, 2, port, mode, timeout, out)) for r in range(2)]
+    for q in procs:
+        q.start()
+    procs[0].join(60)
+    for q in procs:
+        if q.is_alive():
+            q.kill()
+        q.join(10)
+    assert 0 in out, "rank 0 did not report (hung?)"
+    is_collective, dt, sticky = out[0]
+    assert is_collective is True, out[0]
+    assert dt < timeout + 5.0, dt
+    assert sticky
+
+
+def test_band_partition_matches_libdm():
+    """dm_create_sharded (libdm) and the multi-process layer split rows the
+    same way (no GPU needed: dm_sharded_band_rows is pure host code)."""
+    import ctypes
+
+    from dm import load_library
+    from dm.sharded import band_rows
+
+    lib = load_library()
+    for H in (64, 100, 640, 1000, 32768, 65536):
+        for P in (1, 2, 3, 5, 8, 26):
+            r0, n = ctypes.c_int64(), ctypes.c_int64()
+            for r in range(P):
+                assert lib.dm_sharded_band_rows(H, P, r, ctypes.byref(r0), ctypes.byref(n)) == 0
+                assert (r0.value, n.value) == band_rows(H, P, r)
