@@ -21,7 +21,7 @@
 
 // Wait for all three streams; nothing of this handle is in flight afterwards.
 hipError_t dm_sync_all(dm_grid* g) {
-  for (hipStream_t s : {g->stream, g->fe_stream, g->pass_stream}) {
+  for (hipStream_t s : {g->stream, g->fe_stream, g->pass_stream, g->big_stream}) {
     if (!s) continue;
     const hipError_t e = hipStreamSynchronize(s);
     if (e != hipSuccess) return e;
@@ -198,8 +198,11 @@ int ensure_trig(dm_grid* g, int32_t N, float amin, float inc) {
 // sort may be asked to order (band slot_cap, merge m_cap).
 int dm_grow_bucket_sort(dm_grid* g, int64_t n) {
   if (n <= g->bs_cap) return DM_OK;
-  int rc = dev_alloc(&g->bs_key, n, "bucket-sort keys");
-  if (!rc) rc = dev_alloc(&g->bs_idx, n, "bucket-sort indices");
+  int rc = dev_alloc(&g->bs_key, n, "radix-sort keys");
+  if (!rc) rc = dev_alloc(&g->bs_key2, n, "radix-sort keys");
+  if (!rc) rc = dev_alloc(&g->bs_idx, n, "radix-sort indices");
+  if (!rc) rc = dev_alloc(&g->bs_idx2, n, "radix-sort indices");
+  if (!rc) rc = dev_alloc(&g->bs_hist, 256 * (ceil_div(n, 2048) + 1), "radix-sort histograms");  // k_rx_*: 2048 keys per block
   if (rc) { g->bs_cap = 0; return rc; }
   g->bs_cap = n;
   return DM_OK;
@@ -529,8 +532,6 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   DM_HIP(hipMemset(g->rel, 0, sizeof(unsigned long long) * 4 * (size_t)g->NT));
   if ((rc = dev_alloc(&g->edge_label, 2 * g->W, "edge labels"))) return fail(rc);
   if ((rc = dev_alloc(&g->halo, 2 * g->W, "halo rows"))) return fail(rc);
-  if ((rc = dev_alloc(&g->bs_rows, 3 * (kBuckets + 1), "bucket-sort buckets"))) return fail(rc);
-  DM_HIP(hipMemset(g->bs_rows, 0, sizeof(int32_t) * 3 * (kBuckets + 1)));  // counts start at zero
   if ((rc = grow_slots(g, 1 << 16))) return fail(rc);
   dm_select_fw(g, g->fparity);
   for (int sl = 0; sl <= dm_grid::kRbSlots; ++sl)
@@ -578,6 +579,8 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipExtStreamCreateWithCUMask(front-end)"));
     e = hipExtStreamCreateWithCUMask(&g->pass_stream, (uint32_t)map_mask.size(), map_mask.data());
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipExtStreamCreateWithCUMask(pass)"));
+    e = hipExtStreamCreateWithCUMask(&g->big_stream, (uint32_t)map_mask.size(), map_mask.data());
+    if (e != hipSuccess) return fail(dm_hip_check(e, "hipExtStreamCreateWithCUMask(big)"));
   } else {
     e = hipStreamCreateWithPriority(&g->stream, hipStreamNonBlocking, p_grid);
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate"));
@@ -586,12 +589,15 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(front-end)"));
     e = hipStreamCreateWithPriority(&g->pass_stream, hipStreamNonBlocking, p_pass);
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(pass)"));
+    e = hipStreamCreateWithPriority(&g->big_stream, hipStreamNonBlocking, p_pass);
+    if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(big)"));
   }
   // ev_fe / ev_free only order the two streams on the device: no system-
   // scope fence (no host-visible cache writeback at every step).  The host
   // waits on a readback slot's event and then reads mapped host memory:
   // default fences.
-  for (hipEvent_t* ev : {&g->ev_fe, &g->ev_bits[0], &g->ev_bits[1], &g->iw[0].ev_free, &g->iw[1].ev_free}) {
+  for (hipEvent_t* ev : {&g->ev_fe, &g->ev_bits[0], &g->ev_bits[1], &g->iw[0].ev_free, &g->iw[1].ev_free,
+                         &g->ev_bigfork, &g->ev_big}) {
     e = hipEventCreateWithFlags(ev, hipEventDisableTiming | hipEventDisableSystemFence);
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
   }
@@ -615,7 +621,8 @@ int dm_destroy(dm_grid* g) {
   (void)dm_sync_all(g);
   dm_batch_release(&g->batch);
   for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
-  for (hipEvent_t ev : {g->ev_fe, g->ev_bits[0], g->ev_bits[1], g->iw[0].ev_free, g->iw[1].ev_free})
+  for (hipEvent_t ev : {g->ev_fe, g->ev_bits[0], g->ev_bits[1], g->iw[0].ev_free, g->iw[1].ev_free,
+                        g->ev_bigfork, g->ev_big})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& r : g->rb) {
     if (r.ev) (void)hipEventDestroy(r.ev);
@@ -625,6 +632,7 @@ int dm_destroy(dm_grid* g) {
   }
   if (g->fe_stream) (void)hipStreamDestroy(g->fe_stream);
   if (g->pass_stream) (void)hipStreamDestroy(g->pass_stream);
+  if (g->big_stream) (void)hipStreamDestroy(g->big_stream);
   for (auto& f : g->fw) {
     dev_free(f.cnt); dev_free(f.fsh); dev_free(f.ftiles); dev_free(f.big_tiles); dev_free(f.fbits);
     dev_free(f.edge_slot); dev_free(f.slot_parent);
@@ -640,7 +648,7 @@ int dm_destroy(dm_grid* g) {
   dev_free(g->tile_free); dev_free(g->beams); dev_free(g->blk_hist); dev_free(g->blk_n);
   dev_free(g->trig);
   dev_free(g->pose4); dev_free(g->ranges); 
-  dev_free(g->bs_rows); dev_free(g->bs_key); dev_free(g->bs_idx);
+  dev_free(g->bs_key); dev_free(g->bs_key2); dev_free(g->bs_idx); dev_free(g->bs_idx2); dev_free(g->bs_hist);
   dev_free(g->border); dev_free(g->rel); dev_free(g->slot_label); dev_free(g->slot_root);
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
   dev_free(g->edge_label); dev_free(g->mask); dev_free(g->labels);

@@ -208,10 +208,12 @@ __device__ inline int root_rank(const uint64_t* s_root, const int32_t* pre, int 
 //     the component's min linear index);
 //  4. per-component sums from run lengths, one slot per component;
 //  5. unions across the tile's edges (below).
-// Tiles come from the pass's list (jlist == nullptr: list position kk), or
-// from jlist, the list positions k_frontier_tile left over.
+// Tiles come from the pass's list (bflag == nullptr: every list position),
+// or only the positions bflag marks (k_frontier_bits: too run-rich for the
+// wave kernel); a workgroup then gathers the flags of its next 64 positions
+// in one load round and works through the marked ones.
 __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
-    FGeom g, const uint64_t* __restrict__ fbits, const int32_t* __restrict__ jlist,
+    FGeom g, const uint64_t* __restrict__ fbits, const int32_t* __restrict__ bflag,
     const int32_t* __restrict__ ftiles, const unsigned long long* __restrict__ list_n,
     int32_t* border, unsigned long long* rel,
     long long* __restrict__ slot_label, int32_t* slot_parent,
@@ -233,9 +235,23 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
   const int tid = threadIdx.x, lane = __lane_id();
   const int64_t nft = (int64_t)*list_n;
   const int64_t G = gridDim.x;
+  __shared__ uint64_t s_todo;
   DM_PH_INIT();
-  for (int64_t kk = blockIdx.x; kk < nft; kk += G) {  // one tile per workgroup at C3
-    const int64_t jj = jlist ? (int64_t)jlist[kk] : kk;
+  for (int64_t kb = blockIdx.x; kb < nft; kb += bflag ? 64 * G : G) {  // one tile per workgroup at C3
+  uint64_t todo = 1ull;
+  if (bflag) {
+    if (tid < 64) {
+      const int64_t q = kb + (int64_t)tid * G;
+      const uint64_t m = __ballot(q < nft && bflag[q] != 0);
+      if (tid == 0) s_todo = m;
+    }
+    __syncthreads();
+    todo = s_todo;
+    __syncthreads();
+  }
+  while (todo) {
+    const int64_t jj = bflag ? kb + (int64_t)(__ffsll((unsigned long long)todo) - 1) * G : kb;
+    todo &= todo - 1;
     const int32_t tile = ftiles[jj];
     const uint64_t F = tid < DM_TS ? fbits[jj * DM_TS + tid] : 0ull;
     const int64_t j = tile;  // border records are indexed by tile
@@ -499,6 +515,7 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
     __syncthreads();
     DM_PH(dm_phase_acc_frontier, 7);
   }
+  }
   DM_PH_FLUSH(dm_phase_acc_frontier);
 }
 
@@ -699,7 +716,8 @@ __global__ __launch_bounds__(kFW * 64) void k_frontier_bits(FGeom g, const int8_
                                                             const int32_t* __restrict__ ftiles,
                                                             const unsigned long long* __restrict__ list_n,
                                                             uint64_t* __restrict__ fbits,
-                                                            unsigned long long* cnt, int use_fmask) {
+                                                            unsigned long long* cnt, int use_fmask,
+                                                            int32_t* __restrict__ big_flag) {
   const int w = threadIdx.x >> 6, lane = __lane_id();
   const int64_t nft = (int64_t)*list_n;
   if (blockIdx.x == 0 && threadIdx.x == 0) cnt[CNT_FL0] = (unsigned long long)nft;
@@ -743,7 +761,17 @@ __global__ __launch_bounds__(kFW * 64) void k_frontier_bits(FGeom g, const int8_
     uint64_t hd = __shfl_down(h, 1);
     if (lane == 0) hu = he;
     if (lane == 63) hd = he;
-    fbits[jj * DM_TS + lane] = Fr & (h | hu | hd);
+    const uint64_t F = Fr & (h | hu | hd);
+    fbits[jj * DM_TS + lane] = F;
+    // a tile with more runs than a tile-wave keeps is flagged for
+    // k_frontier_tile_big, which runs beside the wave kernel:
+    // a plain store per listed tile (an append to one shared list was a
+    // same-address atomic per run-rich tile: +90 us at C5's 192 beams)
+    if (big_flag) {
+      int nr = __popcll(run_starts(F));
+      for (int o = 32; o > 0; o >>= 1) nr += __shfl_xor(nr, o);
+      if (lane == 0) big_flag[jj] = nr > kRunsFast ? 1 : 0;
+    }
   }
 }
 
@@ -804,8 +832,8 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
       atomicAdd(&fsh[shard * kShardWords + SH_RUNS], (unsigned long long)nruns);
       atomicAdd(&fsh[shard * kShardWords + SH_FTF], 1ull);
     }
-    if (nruns > kRunsFast) {  // too many for this wave's LDS: the big kernel's
-      if (lane == 0) big_list[atomicAdd(&cnt[CNT_BIG], 1ull)] = (int32_t)jj;
+    if (nruns > kRunsFast) {  // too many for this wave's LDS: flagged for the big kernel by k_frontier_bits
+      if (lane == 0) atomicAdd(&fsh[shard * kShardWords + SH_BIG], 1ull);
       continue;
     }
     for (int r = lane; r < nruns; r += 64) {
@@ -1164,15 +1192,17 @@ __device__ inline void write_rb_header(int64_t K, int64_t cap, unsigned long lon
   unsigned long long* header = dm_rb_header(host_out);
   if (tid < ncnt) header[tid] = tid == sorted_idx ? (K <= cap ? 1ull : 0ull) : cnt[tid];
   if (tid == ncnt && fsh) {
-    unsigned long long most = 0, runs = 0, ftf = 0;
+    unsigned long long most = 0, runs = 0, ftf = 0, big = 0;
     for (int i = 0; i < kShards; ++i) {
       most = max(most, fsh[i * kShardWords + SH_SLOT]);
       runs += fsh[i * kShardWords + SH_RUNS];
       ftf += fsh[i * kShardWords + SH_FTF];
+      big += fsh[i * kShardWords + SH_BIG];
     }
     header[ncnt] = most;
     header[ncnt + 1] = runs;
     header[ncnt + 2] = ftf;
+    header[ncnt + 3] = big;
   }
 }
 
@@ -1327,112 +1357,209 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
   }
 }
 
-// ---- row-bucket sort for many clusters (K > kBucketSortMin) ---------------
+// ---- LSD radix sort for many clusters (K > kBucketSortMin) ----------------
 // The rank sort is O(K^2): ~0.1 ms at 23k clusters, far more at the 2e5+
-// clusters of a sparse 1 cm map (C5).  Labels are row-major cell indices, so
-// sorting by label = counting sort by row, then by column inside the row:
-// Buckets are runs of 2^shift consecutive labels (at most kBuckets of them
-// over the label range of the rows sorted):
-//   k_bs_count  per-bucket cluster counts (one atomic per record)
-//   k_bs_scan   one workgroup: exclusive offsets per bucket, cursors, counts
-//               zeroed again for the next sort
-//   k_bs_place  each label to its bucket's segment (atomic cursor: unordered)
-//   k_bs_rank   position = bucket offset + labels of the same segment that
-//               are smaller (a bucket holds few components), then the same
-//               record write + readback header as k_rank_sort.
-// Every kernel reads the device-side count; K > cap leaves the result
-// unsorted (flag 0), as the rank sort does.
-__global__ __launch_bounds__(256) void k_bs_count(const long long* __restrict__ clusters,
-                                                  const long long* __restrict__ labels,
-                                                  const unsigned long long* __restrict__ count, int64_t cap,
-                                                  long long base, int shift,
-                                                  int32_t* __restrict__ rcnt) {
-  const int64_t K = (int64_t)*count;
-  if (K > cap) return;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < K; i += (int64_t)gridDim.x * blockDim.x)
-    atomicAdd(&rcnt[(record_key(clusters, labels, i) - base) >> shift], 1);
-}
+// clusters of a sparse 1 cm map (C5).  Labels are unique row-major cell
+// indices in [base, base + span) (span = rows * W: the band's or the map's
+// label range), so the sort key is label - base, `bits` = ceil(log2 span)
+// wide: ceil(bits / 8) stable counting passes of db = ceil(bits / passes)
+// bits each (C5's 2^32 labels: 4 x 8 bits; C3's 2^28: 4 x 7), each pass
+// (a block's kRxItems keys are loaded into registers in one round, so a
+// pass is a few load latencies, not one per key):
+//   k_rx_hist     per block of kRxItems keys: LDS digit histogram ->
+//                 hist[digit][block] (digit-major, so one linear exclusive
+//                 scan gives every (digit, block) its output offset)
+//   k_rx_scan     one workgroup: that exclusive scan
+//   k_rx_scatter  the block's keys again, in order, 256 per round: rank
+//                 among equal digits by wave ballots (db ballots give each
+//                 lane its peers), across the block's 4 waves by LDS counts,
+//                 across rounds by a running LDS count: a STABLE placement
+// then k_rx_emit writes every record at its sorted position (the same record
+// write + readback header as k_rank_sort).  The round-2 bucket sort (4096
+// label buckets, O(b^2) ranking inside a bucket, same-address atomics per
+// record) took 0.31 ms at C5's 219k clusters: robots cluster their
+// frontiers in a few buckets.  Every kernel reads the device-side count;
+// K > cap leaves the result unsorted (flag 0), as the rank sort does.
+constexpr int kRxThreads = 256;
+constexpr int kRxRounds = 8;                      // keys per thread, all loaded up front
+constexpr int kRxItems = kRxThreads * kRxRounds;  // keys per block
+constexpr int kRxMaxRadix = 256;
+constexpr int kRxScanThreads = 1024;
 
-constexpr int kScanThreads = 1024;
-static_assert(kBuckets == 4 * kScanThreads, "k_bs_scan loads 4 buckets per thread");
-
-// One workgroup, every bucket count loaded at once (4 contiguous per
-// thread): exclusive offsets and cursors, counts zeroed for the next sort.
-__global__ __launch_bounds__(kScanThreads) void k_bs_scan(const unsigned long long* __restrict__ count,
-                                                          int64_t cap, int nbk, int32_t* __restrict__ rcnt,
-                                                          int32_t* __restrict__ roff, int32_t* __restrict__ rcur) {
-  __shared__ int32_t wsum[kScanThreads / 64];
-  if ((int64_t)*count > cap) return;
-  const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
-  int32_t c[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) c[q] = 4 * tid + q < nbk ? rcnt[4 * tid + q] : 0;
-  const int32_t s = c[0] + c[1] + c[2] + c[3];
-  int32_t incl = s;  // inclusive wave scan, then across the 16 waves
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int32_t v = __shfl_up(incl, d);
-    if (lane >= d) incl += v;
-  }
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  int32_t run = incl - s;
-  for (int q = 0; q < w; ++q) run += wsum[q];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int b = 4 * tid + q;
-    if (b < nbk) {
-      roff[b] = run;
-      rcur[b] = run;
-      rcnt[b] = 0;
-    }
-    run += c[q];
-  }
-  if (tid == kScanThreads - 1) roff[nbk] = run;
-}
-
-__global__ __launch_bounds__(256) void k_bs_place(const long long* __restrict__ clusters,
-                                                  const long long* __restrict__ labels,
-                                                  const unsigned long long* __restrict__ count, int64_t cap,
-                                                  long long base, int shift,
-                                                  int32_t* __restrict__ rcur, long long* __restrict__ bkey,
-                                                  int32_t* __restrict__ bidx) {
+__global__ __launch_bounds__(kRxThreads) void k_rx_init(const long long* __restrict__ clusters,
+                                                        const long long* __restrict__ labels,
+                                                        const unsigned long long* __restrict__ count, int64_t cap,
+                                                        long long base, unsigned long long* __restrict__ keys,
+                                                        int32_t* __restrict__ vals) {
   const int64_t K = (int64_t)*count;
   if (K > cap) return;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < K; i += (int64_t)gridDim.x * blockDim.x) {
-    const long long key = record_key(clusters, labels, i);
-    const int32_t p = atomicAdd(&rcur[(key - base) >> shift], 1);
-    bkey[p] = key;
-    bidx[p] = (int32_t)i;
+    keys[i] = (unsigned long long)(record_key(clusters, labels, i) - base);
+    vals[i] = (int32_t)i;
   }
 }
 
-__global__ __launch_bounds__(256) void k_bs_rank(double ox, double oy, double res,
-                                                 long long* clusters, const long long* sums,
-                                                 const long long* labels,
-                                                 const unsigned long long* __restrict__ count, int64_t cap,
-                                                 long long base, int shift,
-                                                 const int32_t* __restrict__ roff,
-                                                 const long long* __restrict__ bkey,
-                                                 const int32_t* __restrict__ bidx, dm_cluster* __restrict__ out,
-                                                 int32_t* __restrict__ rank_of, unsigned long long* sorted,
-                                                 const unsigned long long* __restrict__ cnt, int ncnt,
-                                                 int sorted_idx, const unsigned long long* __restrict__ fsh,
-                                                 dm_cluster* __restrict__ host_out, int64_t host_cap) {
+// Block blk's keys, thread t's q-th key = blk * kRxItems + q * kRxThreads + t
+// (coalesced; this order is also the stable order the scatter keeps).
+__global__ __launch_bounds__(kRxThreads) void k_rx_hist(const unsigned long long* __restrict__ count, int64_t cap,
+                                                        const unsigned long long* __restrict__ keys, int shift,
+                                                        int db, int32_t* __restrict__ hist) {
+  __shared__ int32_t h[kRxMaxRadix];
+  const int64_t K = (int64_t)*count;
+  if (K > cap) return;
+  const int64_t nblk = (K + kRxItems - 1) / kRxItems;
+  const int R = 1 << db;
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    unsigned long long k[kRxRounds];
+    const int64_t i0 = blk * kRxItems + threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < kRxRounds; ++q) k[q] = i0 + q * kRxThreads < K ? keys[i0 + q * kRxThreads] : ~0ull;
+    for (int d = threadIdx.x; d < R; d += kRxThreads) h[d] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kRxRounds; ++q)
+      if (i0 + q * kRxThreads < K) atomicAdd(&h[(int)((k[q] >> shift) & (unsigned long long)(R - 1))], 1);
+    __syncthreads();
+    for (int d = threadIdx.x; d < R; d += kRxThreads) hist[(int64_t)d * nblk + blk] = h[d];
+    __syncthreads();
+  }
+}
+
+// Exclusive scan of hist[0, R * nblk) in place, one workgroup: the entries
+// are staged in LDS with coalesced loads (up to kRxScanLds of them: 128 KiB,
+// a single workgroup may declare 160 KiB on gfx950), each thread scans a
+// contiguous segment there, the segment sums are scanned across the
+// workgroup, and the result goes back with coalesced stores.  More entries
+// (more than 2^18 keys at 8-bit digits) take the same steps in chunks of
+// kRxScanLds with a carry.
+constexpr int kRxScanLds = 32768;
+__global__ __launch_bounds__(kRxScanThreads) void k_rx_scan(const unsigned long long* __restrict__ count,
+                                                            int64_t cap, int db, int32_t* __restrict__ hist) {
+  __shared__ int32_t sv[kRxScanLds];
+  __shared__ int32_t wsum[kRxScanThreads / 64];
+  const int64_t K = (int64_t)*count;
+  if (K > cap) return;
+  const int64_t nblk = (K + kRxItems - 1) / kRxItems;
+  const int64_t n = ((int64_t)1 << db) * nblk;
+  const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+  int32_t carry = 0;
+  for (int64_t c0 = 0; c0 < n; c0 += kRxScanLds) {
+    const int m = (int)min<int64_t>(kRxScanLds, n - c0);
+    for (int j = tid; j < m; j += kRxScanThreads) sv[j] = hist[c0 + j];
+    __syncthreads();
+    const int per = (m + kRxScanThreads - 1) / kRxScanThreads;
+    const int lo = min(m, tid * per), hi = min(m, lo + per);
+    int32_t seg = 0;
+    for (int j = lo; j < hi; ++j) seg += sv[j];
+    int32_t incl = seg;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t t = __shfl_up(incl, d);
+      if (lane >= d) incl += t;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int32_t run = carry + incl - seg, total = 0;
+#pragma unroll
+    for (int q = 0; q < kRxScanThreads / 64; ++q) {
+      const int32_t ws = wsum[q];
+      run += q < w ? ws : 0;
+      total += ws;
+    }
+    for (int j = lo; j < hi; ++j) {
+      const int32_t x = sv[j];
+      sv[j] = run;
+      run += x;
+    }
+    carry += total;
+    __syncthreads();
+    for (int j = tid; j < m; j += kRxScanThreads) hist[c0 + j] = sv[j];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kRxThreads) void k_rx_scatter(const unsigned long long* __restrict__ count, int64_t cap,
+                                                           const unsigned long long* __restrict__ keys_in,
+                                                           const int32_t* __restrict__ vals_in, int shift, int db,
+                                                           const int32_t* __restrict__ hist,
+                                                           unsigned long long* __restrict__ keys_out,
+                                                           int32_t* __restrict__ vals_out) {
+  __shared__ int32_t off[kRxMaxRadix];                    // the block's output offset per digit, advancing
+  __shared__ int32_t wcnt[kRxThreads / 64][kRxMaxRadix];  // this round's count per (wave, digit)
+  const int64_t K = (int64_t)*count;
+  if (K > cap) return;
+  const int64_t nblk = (K + kRxItems - 1) / kRxItems;
+  const int R = 1 << db;
+  const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    // every key and value of the block in registers first: one load round
+    unsigned long long k[kRxRounds];
+    int32_t v[kRxRounds];
+    const int64_t i0 = blk * kRxItems + tid;
+#pragma unroll
+    for (int q = 0; q < kRxRounds; ++q) {
+      const bool ok = i0 + q * kRxThreads < K;
+      k[q] = ok ? keys_in[i0 + q * kRxThreads] : 0ull;
+      v[q] = ok ? vals_in[i0 + q * kRxThreads] : 0;
+    }
+    for (int d = tid; d < R; d += kRxThreads) {
+      off[d] = hist[(int64_t)d * nblk + blk];
+#pragma unroll
+      for (int q = 0; q < kRxThreads / 64; ++q) wcnt[q][d] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRxRounds; ++r) {
+      const bool ok = i0 + r * kRxThreads < K;
+      const int dg = (int)((k[r] >> shift) & (unsigned long long)(R - 1));
+      // lanes of this wave holding the same digit (valid lanes only)
+      unsigned long long peers = __ballot(ok);
+      for (int b = 0; b < db; ++b) {
+        const unsigned long long m = __ballot((dg >> b) & 1);
+        peers &= ((dg >> b) & 1) ? m : ~m;
+      }
+      const int wrank = __popcll(peers & lt);
+      if (ok && wrank == 0) wcnt[w][dg] = __popcll(peers);
+      __syncthreads();
+      if (ok) {
+        int before = 0;
+        for (int q = 0; q < w; ++q) before += wcnt[q][dg];
+        const int64_t pos = (int64_t)off[dg] + before + wrank;
+        keys_out[pos] = k[r];
+        vals_out[pos] = v[r];
+      }
+      __syncthreads();
+      for (int d = tid; d < R; d += kRxThreads) {
+        int t = 0;
+#pragma unroll
+        for (int q = 0; q < kRxThreads / 64; ++q) {
+          t += wcnt[q][d];
+          wcnt[q][d] = 0;
+        }
+        off[d] += t;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ __launch_bounds__(kRxThreads) void k_rx_emit(double ox, double oy, double res, long long* clusters,
+                                                        const long long* sums, const long long* labels,
+                                                        const unsigned long long* __restrict__ count, int64_t cap,
+                                                        const int32_t* __restrict__ vals, dm_cluster* __restrict__ out,
+                                                        int32_t* __restrict__ rank_of, unsigned long long* sorted,
+                                                        const unsigned long long* __restrict__ cnt, int ncnt,
+                                                        int sorted_idx, const unsigned long long* __restrict__ fsh,
+                                                        dm_cluster* __restrict__ host_out, int64_t host_cap) {
   const int64_t K = (int64_t)*count;
   if (blockIdx.x == 0) write_rb_header(K, cap, sorted, cnt, ncnt, sorted_idx, fsh, host_out);
   if (K > cap) {
     fix_raw_records(clusters, sums, labels, K);
     return;
   }
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < K; p += (int64_t)gridDim.x * blockDim.x) {
-    const long long key = bkey[p];
-    const int64_t b = (key - base) >> shift;
-    const int32_t lo = roff[b], hi = roff[b + 1];
-    int64_t rank = lo;
-    for (int32_t j = lo; j < hi; ++j) rank += bkey[j] < key;
-    put_sorted(ox, oy, res, clusters, sums, labels, bidx[p], rank, out, rank_of, host_out, host_cap);
-  }
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < K; p += (int64_t)gridDim.x * blockDim.x)
+    put_sorted(ox, oy, res, clusters, sums, labels, vals[p], p, out, rank_of, host_out, host_cap);
 }
 
 // Cell slot -> final label (the root of a set is its min-label slot).
@@ -1514,30 +1641,42 @@ int dm_launch_bucket_sort(dm_grid* g, hipStream_t stream, long long* clusters, c
                           int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
                           int64_t host_cap) {
   if (max_records > g->bs_cap)
-    return dm_set_error(DM_ERR_INVALID_ARG, "bucket sort: %lld records exceed its workspace",
+    return dm_set_error(DM_ERR_INVALID_ARG, "radix sort: %lld records exceed its workspace",
                         (long long)max_records);
-  // buckets of 2^shift consecutive labels over the rows' label range
+  // key = label - base over [0, span)
   const long long base = row_base * g->W;
-  const int64_t span = rows * g->W;
-  int shift = 0;
-  while (((span - 1) >> shift) + 1 > kBuckets) ++shift;
-  const int nbk = (int)(((span - 1) >> shift) + 1);
-  int32_t* rcnt = g->bs_rows;
-  int32_t* roff = rcnt + (kBuckets + 1);
-  int32_t* rcur = roff + (kBuckets + 1);
-  const int eg = grid_for(max_records, 256, 2048);
-  DM_LAUNCH(k_bs_count, dim3(eg), dim3(256), 0, stream, clusters, labels, d_count, max_records, base,
-                     shift, rcnt);
+  const unsigned long long span = (unsigned long long)rows * (unsigned long long)g->W;
+  int bits = 1;
+  while (bits < 64 && (span - 1) >> bits) ++bits;
+  const int passes = (bits + 7) / 8;
+  const int db = (bits + passes - 1) / passes;
+  // grids follow the expected count (the kernels stride; blocks past the
+  // device-side count return)
+  const int64_t expect = std::min<int64_t>(max_records, std::max<int64_t>(2 * g->sort_hint, kRxItems));
+  const int eg = grid_for(expect, kRxThreads, 4096);
+  const int bg = grid_for(expect, kRxItems, 4096);
+  unsigned long long* ka = g->bs_key;
+  unsigned long long* kb = g->bs_key2;
+  int32_t* va = g->bs_idx;
+  int32_t* vb = g->bs_idx2;
+  DM_LAUNCH(k_rx_init, dim3(eg), dim3(kRxThreads), 0, stream, clusters, labels, d_count, max_records, base, ka, va);
   DM_HIP(hipGetLastError());
-  DM_LAUNCH(k_bs_scan, dim3(1), dim3(kScanThreads), 0, stream, d_count, max_records, nbk, rcnt,
-                     roff, rcur);
-  DM_HIP(hipGetLastError());
-  DM_LAUNCH(k_bs_place, dim3(eg), dim3(256), 0, stream, clusters, labels, d_count, max_records,
-                     base, shift, rcur, g->bs_key, g->bs_idx);
-  DM_HIP(hipGetLastError());
-  DM_LAUNCH(k_bs_rank, dim3(eg), dim3(256), 0, stream, g->p.origin_x, g->p.origin_y,
-                     g->p.resolution, clusters, sums, labels, d_count, max_records, base, shift, roff, g->bs_key,
-                     g->bs_idx, out, rank_of, d_sorted, cnt, ncnt, sorted_idx, fsh, host_out, host_cap);
+  for (int p = 0; p < passes; ++p) {
+    const int shift = p * db;
+    const int dbp = std::min(db, bits - shift);
+    DM_LAUNCH(k_rx_hist, dim3(bg), dim3(kRxThreads), 0, stream, d_count, max_records, ka, shift, dbp, g->bs_hist);
+    DM_HIP(hipGetLastError());
+    DM_LAUNCH(k_rx_scan, dim3(1), dim3(kRxScanThreads), 0, stream, d_count, max_records, dbp, g->bs_hist);
+    DM_HIP(hipGetLastError());
+    DM_LAUNCH(k_rx_scatter, dim3(bg), dim3(kRxThreads), 0, stream, d_count, max_records, ka, va, shift, dbp,
+              g->bs_hist, kb, vb);
+    DM_HIP(hipGetLastError());
+    std::swap(ka, kb);
+    std::swap(va, vb);
+  }
+  DM_LAUNCH(k_rx_emit, dim3(eg), dim3(kRxThreads), 0, stream, g->p.origin_x, g->p.origin_y, g->p.resolution,
+            clusters, sums, labels, d_count, max_records, va, out, rank_of, d_sorted, cnt, ncnt, sorted_idx, fsh,
+            host_out, host_cap);
   DM_HIP(hipGetLastError());
   return DM_OK;
 }
@@ -1595,9 +1734,25 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   } else if (g->fmask_on && want_off) {
     g->fmask_on = false;
   }
+  // Tile kernel, chosen from the last collected pass (both are exact for any
+  // map; they differ in speed): tiles whose frontiers are dense (more than
+  // kDenseRuns runs per tile with frontier cells on average, e.g. C3's ray
+  // fans, ~100) take the 256-thread kernel, one tile per workgroup; sparse
+  // ones (an explored map's few frontier tiles among many listed tiles, a
+  // 1 cm map's thin rays) the wave-per-tile kernel, which also screens the
+  // listed tiles without frontier cells at the rate of one 8-byte load per
+  // lane; tiles with more than kRunsFast runs are listed by k_frontier_bits
+  // for the 256-thread kernel, which runs beside it on big_stream.
+  // Dense only while the tiles fit about two rounds of the 256-thread
+  // kernel's slots: with tens of thousands of tiles (a 1 cm map's rays) the
+  // wave kernel's 4x more tiles in flight win even where runs are many.
+  const bool dense = g->frontier_kernel == 2 ||
+                     (g->frontier_kernel == 0 && g->ftf_hint > 0 && g->runs_hint > kDenseRuns * g->ftf_hint &&
+                      g->ftf_hint <= kDenseMaxTiles);
   dm_timer_begin(g, "frontier_bits", &t);
   DM_LAUNCH(k_frontier_bits, dim3(wave_grid), dim3(kFW * 64), 0, g->stream, fg, g->state, g->halo,
-                     g->fmask, g->ftiles, list_n, g->fbits, g->cnt, g->fmask_on ? 1 : 0);
+                     g->fmask, g->ftiles, list_n, g->fbits, g->cnt, g->fmask_on ? 1 : 0,
+                     dense ? nullptr : g->big_tiles);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   // the map has been read: with split, the rest runs on the pass stream,
@@ -1622,22 +1777,25 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
     }
   }
   if (end_stream) *end_stream = ps;
-  // Tile kernel, chosen from the last collected pass (both are exact for any
-  // map; they differ in speed): tiles whose frontiers are dense (more than
-  // kDenseRuns runs per tile with frontier cells on average, e.g. C3's ray
-  // fans, ~100) take the 256-thread kernel, one tile per workgroup; sparse
-  // ones (an explored map's few frontier tiles among many listed tiles, a
-  // 1 cm map's thin rays) the wave-per-tile kernel, which also screens the
-  // listed tiles without frontier cells at the rate of one 8-byte load per
-  // lane and leaves tiles with more than kRunsFast runs to the 256-thread
-  // kernel.
-  // Dense only while the tiles fit about two rounds of the 256-thread
-  // kernel's slots: with tens of thousands of tiles (a 1 cm map's rays) the
-  // wave kernel's 4x more tiles in flight win even where runs are many.
-  const bool dense = g->frontier_kernel == 2 ||
-                     (g->frontier_kernel == 0 && g->ftf_hint > 0 && g->runs_hint > kDenseRuns * g->ftf_hint &&
-                      g->ftf_hint <= kDenseMaxTiles);
   if (!dense) {
+    // the run-rich tiles (listed by k_frontier_bits) on big_stream, beside
+    // the wave kernel: the round-2 launch order ran them after it (C5 at 192
+    // beams: 157 us of big tiles behind 194 us of wave tiles).  The tile-edge
+    // hand-off unites tiles whatever kernel and order processed them.
+    DM_HIP(dm_batch_flush_all());
+    DM_HIP(hipEventRecord(g->ev_bigfork, ps));
+    DM_HIP(hipStreamWaitEvent(g->big_stream, g->ev_bigfork, 0));
+    dm_timer_begin(g, "frontier_big", &t, g->big_stream);
+    // the grid follows the last pass's count (the kernel grid-strides)
+    const int big_grid =
+        grid_for(std::min<int64_t>(g->NT, dm_quantize_up(g->big_hint + g->big_hint / 4 + 64)), 1, 8192);
+    DM_LAUNCH(k_frontier_tile_big, dim3(big_grid), dim3(kFT), 0, g->big_stream, fg, g->fbits, g->big_tiles,
+              g->ftiles, list_n, g->border, g->rel, g->slot_label, g->slot_parent, g->slot_own,
+              g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh, 0);
+    dm_timer_end(g, &t);
+    DM_HIP(hipGetLastError());
+    DM_HIP(dm_batch_flush_all());
+    DM_HIP(hipEventRecord(g->ev_big, g->big_stream));
     dm_timer_begin(g, "frontier_tile", &t, ps);
     DM_LAUNCH(k_frontier_tile, dim3(wave_grid), dim3(kFW * 64), 0, ps, fg, g->fbits,
                        g->ftiles, list_n, g->border, g->rel,
@@ -1645,22 +1803,20 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
                        g->edge_slot, g->cnt, g->fsh, g->big_tiles);
     dm_timer_end(g, &t);
     DM_HIP(hipGetLastError());
+    DM_HIP(dm_batch_flush_all());
+    DM_HIP(hipStreamWaitEvent(ps, g->ev_big, 0));
+  } else {
+    dm_timer_begin(g, "frontier_tile", &t, ps);
+    // one workgroup per listed tile of the last collected pass (+25 %; the
+    // kernel grid-strides): thousands of empty workgroups would only keep
+    // the dispatcher from the other streams' kernels
+    const int dense_grid = grid_for(std::min<int64_t>(g->NT, g->ftile_hint > 0 ? want_waves : g->NT), 1, 8192);
+    DM_LAUNCH(k_frontier_tile_big, dim3(dense_grid), dim3(kFT), 0, ps, fg, g->fbits, nullptr, g->ftiles, list_n,
+              g->border, g->rel, g->slot_label, g->slot_parent, g->slot_own, g->slot_acc, g->mask,
+              g->cell_slot, g->edge_slot, g->cnt, g->fsh, 1);
+    dm_timer_end(g, &t);
+    DM_HIP(hipGetLastError());
   }
-  dm_timer_begin(g, dense ? "frontier_tile" : "frontier_big", &t, ps);
-  // the leftover tiles of the wave kernel: the grid follows the last pass's
-  // count (the kernel grid-strides)
-  const int big_grid = grid_for(std::min<int64_t>(g->NT, dm_quantize_up(g->big_hint + g->big_hint / 4 + 64)), 1, 8192);
-  // dense: one workgroup per listed tile of the last collected pass (+25 %;
-  // the kernel grid-strides): thousands of empty workgroups would only keep
-  // the dispatcher from the other streams' kernels
-  const int dense_grid = grid_for(std::min<int64_t>(g->NT, g->ftile_hint > 0 ? want_waves : g->NT), 1, 8192);
-  DM_LAUNCH(k_frontier_tile_big, dim3(dense ? dense_grid : big_grid),
-                     dim3(kFT), 0, ps, fg, g->fbits, dense ? nullptr : g->big_tiles, g->ftiles,
-                     dense ? list_n : g->cnt + CNT_BIG, g->border, g->rel,
-                     g->slot_label, g->slot_parent, g->slot_own,
-                     g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh, dense ? 1 : 0);
-  dm_timer_end(g, &t);
-  DM_HIP(hipGetLastError());
   const int sgrid = grid_for(g->slot_cap, 256, 1024);
   dm_timer_begin(g, "frontier_resolve", &t, ps);
   // min_size <= 1: every root is a cluster, compacted by the resolve itself
@@ -1731,7 +1887,7 @@ int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied) {
   g->ftile_hint = (int64_t)g->h_cnt[CNT_FL0];
   g->runs_hint = (int64_t)hdr[CNT_N + 1];
   g->ftf_hint = (int64_t)hdr[CNT_N + 2];
-  g->big_hint = (int64_t)hdr[CNT_BIG];
+  g->big_hint = (int64_t)hdr[CNT_N + 3];
   return DM_OK;
 }
 

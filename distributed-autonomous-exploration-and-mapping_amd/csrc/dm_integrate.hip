@@ -623,6 +623,10 @@ __device__ inline int32_t walk_piece_plain(uint32_t* tl, const PackedPiece& mine
 // pieces is visited at most 15 times, so the final byte 16·hits + misses is
 // at most 255 and no partial sum carries into the next cell.
 constexpr int kSparseMax = 15;
+#ifndef DM_SPARSE_LIST
+#define DM_SPARSE_LIST 256  // touched 4-cell groups a wave lists (more: four row passes; 0 = always the passes, A/B)
+#endif
+constexpr int kSparseList = DM_SPARSE_LIST > 0 ? DM_SPARSE_LIST : 1;
 
 __device__ inline int32_t to_pitch64(int32_t a) {  // pitch-65 address or step -> pitch 64
   return a >= 0 ? a - a / kLdsPitch : -((-a) - (-a) / kLdsPitch);
@@ -934,66 +938,118 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
   // then load and apply only the touched 4-cell groups.  A loop of its own
   // (after the dense items), so none of its registers are live across the
   // dense walk.  The LDS tile is zero here: every dense item clears it.
-  // Two sparse items per workgroup, one per 128-thread half: with at most
-  // kSparseMax pieces a cell is visited at most 15 times, so its counts fit
-  // one byte (hits << 4 | misses: walk_piece_bytes), a tile's counts 4 KiB,
-  // and both halves' tiles share the LDS of one dense count tile.
-  __shared__ int32_t s_hT[2], s_hfree[2];
-  __shared__ uint32_t s_hU[2];
-  const int half = tid >> 7, ht = tid & 127;
-  uint32_t* tq = tl + half * (DM_TS * DM_TS / 4);
-  const int hcx = (ht & 15) * 4;
-  if (tid < 2) { s_hT[tid] = 0; s_hfree[tid] = 0; s_hU[tid] = 0u; }
-  __syncthreads();
-  for (int64_t it2 = blockIdx.x; 2 * it2 < SI; it2 += G) {
-    const int64_t it = 2 * it2 + half;
-    const bool have = it < SI;  // uniform in each half
-    int4 d = have ? list_b[(int64_t)g.act_cap - 1 - it] : make_int4(0, 0, 0, 0);
+  // One sparse item per WAVE (round 3; round 2 had one per 128-thread half,
+  // whose second wave idled through the walk): with at most kSparseMax
+  // pieces a cell is visited at most 15 times, so its counts fit one byte
+  // (hits << 4 | misses: walk_piece_bytes), a tile's counts 4 KiB, and the
+  // four waves' tiles share the LDS of one dense count tile.  A wave walks,
+  // applies and clears its own tile with no workgroup barrier (LDS operations
+  // of one wave complete in order; the wavefront fences keep the compiler
+  // from moving them), so a CU keeps 4 x 7 = 28 sparse tiles in flight.
+  __shared__ int32_t s_wT[kQuarter / 64], s_wfree[kQuarter / 64];
+  __shared__ uint32_t s_wU[kQuarter / 64];
+  __shared__ uint16_t s_list[kQuarter / 64][kSparseList];  // touched 4-cell groups of each wave's tile
+  const int wv = tid >> 6;
+  uint32_t* tq = tl + wv * (DM_TS * DM_TS / 4);
+  const int hcx = (lane & 15) * 4;
+  if (lane == 0) { s_wT[wv] = 0; s_wfree[wv] = 0; s_wU[wv] = 0u; }
+  const int nw = kQuarter / 64;
+  for (int64_t it = (int64_t)blockIdx.x * nw + wv; it < SI; it += (int64_t)G * nw) {
+    int4 d = list_b[(int64_t)g.act_cap - 1 - it];
     d.z = (int64_t)d.y + d.z <= g.seg_cap ? d.z : 0;  // never past the piece array
     const int32_t tile = d.x, c0 = d.y, c = d.z;
     const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
-    const PackedPiece sp = ht < c ? pieces[c0 + ht] : no_piece();
-    const int32_t sfree = have ? tile_free[tile] : 0;
-    int32_t u = walk_piece_bytes(tq, sp, ht < c);
-    const bool inside = tx0 + DM_TS <= g.r.W && ty0 + DM_TS <= g.r.R;  // uniform in the half
+    const PackedPiece sp = lane < c ? pieces[c0 + lane] : no_piece();
+    const int32_t sfree = tile_free[tile];
+    int32_t u = walk_piece_bytes(tq, sp, lane < c);
+    const bool inside = tx0 + DM_TS <= g.r.W && ty0 + DM_TS <= g.r.R;  // uniform in the wave
+    uint32_t wU = 0u;
     if (inside) {
       for (int o = 32; o > 0; o >>= 1) u += __shfl_xor(u, o);
-      if (lane == 0 && u) atomicAdd(&s_hU[half], (uint32_t)u);
+      wU = (uint32_t)u;
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     DM_PH(dm_phase_acc_integrate, 6);
-    // the half's 128 threads cover the tile in two passes of 32 rows (a
-    // thread: one 4-cell group of rows ly0, ly0 + 8, ly0 + 16, ly0 + 24)
-    for (int pass = 0; pass < 2 && have; ++pass) {
-      const int ly0 = (ht >> 4) + 32 * pass;
-      CellRows<4> sc;
-      sc.load_touched(g, tx0, ty0, ly0, 8, hcx, L, state, vec_ok,
-                      [&](int ly) { return tq[ly * 16 + (hcx >> 2)] != 0u; });
-      sc.apply(g, p, tx0, ty0, ly0, 8, hcx, L, state,
-               [&](int ly, uint32_t* h4, uint32_t* m4) {
-                 const uint32_t w = tq[ly * 16 + (hcx >> 2)];
-                 for (int e = 0; e < 4; ++e) {
-                   const uint32_t v = (w >> (8 * e)) & 0xFFu;
-                   h4[e] = v >> 4;
-                   m4[e] = v & 0xFu;
-                 }
-               },
-               &s_hT[half], &s_hfree[half], inside ? nullptr : &s_hU[half]);
+    auto counts = [&](int wi, uint32_t* h4, uint32_t* m4) {
+      const uint32_t w = tq[wi];
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t v = (w >> (8 * e)) & 0xFFu;
+        h4[e] = v >> 4;
+        m4[e] = v & 0xFu;
+      }
+    };
+    // the touched 4-cell groups (non-zero count words, word wi = row * 16 +
+    // group) listed in the wave's LDS list, so each lane loads the L / state
+    // of one or two of them in ONE load round (a ray or two cross a sparse
+    // tile: ~35-70 of its 1024 groups); a tile with more than kSparseList
+    // touched groups takes four 16-row passes instead
+    uint16_t* lst = s_list[wv];
+    int nt = 0;
+    {
+      const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int wi = k * 64 + lane;
+        const bool nz = tq[wi] != 0u;
+        const unsigned long long m = __ballot(nz);
+        const int at = nt + __popcll(m & lt);
+        if (nz && at < kSparseList) lst[at] = (uint16_t)wi;
+        nt += __popcll(m);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (DM_SPARSE_LIST > 0 && nt <= kSparseList) {
+      for (int e0 = 0; e0 < nt; e0 += 128) {
+        const int ea = e0 + lane, eb = e0 + 64 + lane;
+        const int wa = ea < nt ? lst[ea] : 0, wb = eb < nt ? lst[eb] : 0;
+        CellRows<1> ca, cb;
+        ca.load_touched(g, tx0, ty0, wa >> 4, 0, (wa & 15) * 4, L, state, vec_ok, [&](int) { return ea < nt; });
+        cb.load_touched(g, tx0, ty0, wb >> 4, 0, (wb & 15) * 4, L, state, vec_ok, [&](int) { return eb < nt; });
+        if (ea < nt)
+          ca.apply(g, p, tx0, ty0, wa >> 4, 0, (wa & 15) * 4, L, state,
+                   [&](int, uint32_t* h4, uint32_t* m4) { counts(wa, h4, m4); }, &s_wT[wv], &s_wfree[wv],
+                   inside ? nullptr : &s_wU[wv]);
+        if (eb < nt)
+          cb.apply(g, p, tx0, ty0, wb >> 4, 0, (wb & 15) * 4, L, state,
+                   [&](int, uint32_t* h4, uint32_t* m4) { counts(wb, h4, m4); }, &s_wT[wv], &s_wfree[wv],
+                   inside ? nullptr : &s_wU[wv]);
+      }
+    } else {
+      // the wave covers the tile in four passes of 16 rows (a lane: one
+      // 4-cell group of rows ly0, ly0 + 4, ly0 + 8, ly0 + 12)
+      for (int pass = 0; pass < 4; ++pass) {
+        const int ly0 = (lane >> 4) + 16 * pass;
+        CellRows<4> sc;
+        sc.load_touched(g, tx0, ty0, ly0, 4, hcx, L, state, vec_ok,
+                        [&](int ly) { return tq[ly * 16 + (hcx >> 2)] != 0u; });
+        sc.apply(g, p, tx0, ty0, ly0, 4, hcx, L, state,
+                 [&](int ly, uint32_t* h4, uint32_t* m4) { counts(ly * 16 + (hcx >> 2), h4, m4); },
+                 &s_wT[wv], &s_wfree[wv], inside ? nullptr : &s_wU[wv]);
+      }
     }
     DM_PH(dm_phase_acc_integrate, 7);
-    DM_PH_COUNT(dm_phase_acc_integrate, 21, have ? 1 : 0);
+    DM_PH_COUNT(dm_phase_acc_integrate, 21, 1);
     DM_PH_COUNT(dm_phase_acc_integrate, 22, c);
-    __syncthreads();
-    if (ht == 0 && have) {
-      atomicAdd(&s_accT, (unsigned long long)s_hT[half]);
-      atomicAdd(&s_accU, (unsigned long long)s_hU[half]);
-      if (s_hfree[half]) tile_free[tile] = sfree + s_hfree[half];
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      const int32_t T = s_wT[wv], df = s_wfree[wv];
+      const uint32_t U = s_wU[wv] + wU;
+      atomicAdd(&s_accT, (unsigned long long)T);
+      atomicAdd(&s_accU, (unsigned long long)U);
+      if (df) tile_free[tile] = sfree + df;
       tile_count[tile] = 0;  // ready for the next call
+      s_wT[wv] = 0;
+      s_wfree[wv] = 0;
+      s_wU[wv] = 0u;
     }
-    if (ht == 0) { s_hT[half] = 0; s_hfree[half] = 0; s_hU[half] = 0u; }
-    for (int e = ht; e < DM_TS * DM_TS / 4; e += 128) tq[e] = 0u;
-    __syncthreads();
+    for (int e = lane; e < DM_TS * DM_TS / 4; e += 64) tq[e] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
+  __syncthreads();
   if (tid == 0) {
     unsigned long long* sh = ish + (blockIdx.x % kShards) * kShardWords;
     if (s_accT) atomicAdd(&sh[SH_T], s_accT);

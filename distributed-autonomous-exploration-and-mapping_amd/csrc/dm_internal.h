@@ -86,16 +86,18 @@ static_assert(kShards * kShardWords == 512, "k_integrate_reset covers 512 shard 
 enum { SH_U = 0, SH_T = 1, SH_TH = 2, SH_ACT = 3 };  // integrate shard fields
 // frontier shard fields: slots allocated, runs and tiles with frontier
 // cells (the next pass picks its tile kernel from their ratio)
-enum { SH_SLOT = 0, SH_RUNS = 1, SH_FTF = 2 };
+// and tiles too run-rich for a tile-wave (the next pass sizes the big kernel's grid)
+enum { SH_SLOT = 0, SH_RUNS = 1, SH_FTF = 2, SH_BIG = 3 };
 
 // Readback header in front of the sorted cluster records (device out_clu and
 // pinned h_out both point kRbRecords records into their allocation): the
 // frontier counters [CNT_N] and the fullest slot shard [CNT_N], written by
 // k_rank_sort into the mapped host buffer together with the first records.
 // header words: [0, CNT_N) counters, [CNT_N] fullest slot shard, [CNT_N + 1]
-// runs, [CNT_N + 2] tiles with frontier cells (shard sums)
+// runs, [CNT_N + 2] tiles with frontier cells, [CNT_N + 3] run-rich tiles
+// (shard sums)
 constexpr int kRbRecords = 6;  // 6 * 48 B = 288 B >= (CNT_N + 3) * 8 B
-static_assert(kRbRecords * sizeof(dm_cluster) >= (CNT_N + 3) * sizeof(unsigned long long), "readback header");
+static_assert(kRbRecords * sizeof(dm_cluster) >= (CNT_N + 4) * sizeof(unsigned long long), "readback header");
 __host__ __device__ inline unsigned long long* dm_rb_header(dm_cluster* records) {
   return reinterpret_cast<unsigned long long*>(records - kRbRecords);
 }
@@ -292,12 +294,17 @@ struct dm_grid {
   // batch's map update overlaps it.  bits_flag / bits_seq: the bit rows'
   // hand-off (k_seq_signal on `stream`, k_seq_gate on pass_stream).
   hipStream_t pass_stream = nullptr;
+  // big_stream: k_frontier_tile_big over the tiles k_frontier_bits listed as
+  // too run-rich for a tile-wave, beside the wave kernel on the pass stream
+  // (forked after the bit rows, joined before the resolve)
+  hipStream_t big_stream = nullptr;
+  hipEvent_t ev_bigfork = nullptr, ev_big = nullptr;
   unsigned long long* bits_flag = nullptr;  // [kSigWord] / [kGateWord] counts, [kStampWord] pass stamp
   hipEvent_t p_tail = nullptr;        // the last pass_stream pass's end (alias)
   bool p_pending = false;             // pass_stream work `stream` has not been ordered after
   uint64_t p_tail_pass = 0;
   int32_t* ftiles = nullptr;   // tiles with free cells (built by k_frontier_prep)
-  int32_t* big_tiles = nullptr;  // [NT] list positions left to k_frontier_tile_big (too many runs for a tile-wave)
+  int32_t* big_tiles = nullptr;  // [NT] per list position: 1 = too many runs for a tile-wave (k_frontier_bits)
   uint64_t* fbits = nullptr;   // [NT][64] frontier bit rows of the listed tiles (k_frontier_bits)
   int32_t* border = nullptr;   // [tile][4][64] slot ids of a tile's edges (published sides only)
   // tile-edge hand-off words of k_frontier_tile, [4][NT]: horizontal (t, t+1),
@@ -328,11 +335,13 @@ struct dm_grid {
   int has_halo[2] = {0, 0};
   bool frontier_valid = false;
 
-  // large-K cluster sort (row buckets, dm_frontier.hip k_bs_*): used when
+  // large-K cluster sort (LSD radix, dm_frontier.hip k_rx_*): used when
   // the last collected pass of its kind had more than kBucketSortMin clusters
-  int32_t* bs_rows = nullptr;     // [3][kBuckets + 1] per-bucket counts (kept zero), offsets, cursors
-  long long* bs_key = nullptr;    // [bs_cap] labels placed by row
-  int32_t* bs_idx = nullptr;      // [bs_cap] their record indices
+  unsigned long long* bs_key = nullptr;   // [bs_cap] radix-sort keys (label - base), two buffers
+  unsigned long long* bs_key2 = nullptr;
+  int32_t* bs_idx = nullptr;      // [bs_cap] their record indices, two buffers
+  int32_t* bs_idx2 = nullptr;
+  int32_t* bs_hist = nullptr;     // [256][ceil(bs_cap / 2048)] digit x block counts -> offsets
   int64_t bs_cap = 0;
   int64_t sort_hint = 0, msort_hint = 0;  // clusters of the last band / merge readback
   int64_t ftile_hint = 0;                 // listed tiles of the last collected frontier pass
@@ -475,11 +484,10 @@ int dm_launch_rank_sort(hipStream_t stream, long long* clusters, const long long
                         int64_t host_cap, int64_t expect);
 // Listed tiles from which a frontier pass reads fmask instead of state bytes.
 constexpr int64_t kFmaskOnTiles = 8192;
-// Clusters above which the row-bucket sort replaces the O(K^2) rank sort.
+// Clusters above which the radix sort replaces the O(K^2) rank sort.
 constexpr int64_t kBucketSortMin = 4096;
-constexpr int kBuckets = 4096;  // row buckets of the bucket sort (k_bs_scan: 4 per thread)
 int dm_grow_bucket_sort(dm_grid* g, int64_t n);
-// Row-bucket sort of the raw records (labels of rows [row_base, row_base +
+// LSD radix sort of the raw records (labels of rows [row_base, row_base +
 // rows)): same outputs, readback header and flags as dm_launch_rank_sort.
 int dm_launch_bucket_sort(dm_grid* g, hipStream_t stream, long long* clusters, const long long* sums,
                           const long long* labels, const unsigned long long* d_count,

@@ -30,7 +30,7 @@ def _world(seed, W, H, S=6, N=720, nb=3):
 
 
 @pytest.mark.parametrize("P,W,H,seed", [(1, 300, 200, 1), (2, 640, 700, 2), (3, 500, 900, 3),
-                                        (5, 700, 1000, 4)])
+                                        (5, 700, 1200, 4)])
 def test_sharded_handle_equals_single_handle_and_oracle(oracle_lib, P, W, H, seed):
     p, batches, amin, inc = _world(seed, W, H)
     om = oracle_lib.OracleMap(p)

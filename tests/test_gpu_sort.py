@@ -1,9 +1,10 @@
 """GPU: the cluster sort at every cluster count.
 
 The frontier pipeline orders its cluster records by label with one of two
-device sorts (csrc/dm_frontier.hip): the O(K^2) rank sort, or the row-bucket
-sort (k_bs_count / k_bs_scan / k_bs_place / k_bs_rank) once the last
-collected pass of the handle had more than kBucketSortMin (4096) clusters.
+device sorts (csrc/dm_frontier.hip): the O(K^2) rank sort, or the LSD radix
+sort (k_rx_init / k_rx_hist / k_rx_scan / k_rx_scatter / k_rx_emit) once the
+last collected pass of the handle had more than kBucketSortMin (4096)
+clusters.
 Either must give the oracle's list bit for bit whatever the count of the pass
 it actually sorts, including a small pass sorted by the bucket path after a
 large one, the pipelined begin/end passes and the cross-band merge.
@@ -118,3 +119,22 @@ def test_bucket_sort_merge(oracle_lib, P):
     finally:
         for b in bands:
             b.close()
+
+
+@pytest.mark.parametrize("R,W,rows", [(64, 65536, 3), (2048, 16384, 1)])
+def test_radix_sort_clusters_packed_in_few_rows(oracle_lib, R, W, rows):
+    """Clusters packed in a few rows (the round-2 bucket sort's worst case:
+    one label bucket holding most records) and a wide label range; the
+    second pass is sorted by the radix path (hint from the first)."""
+    import dm
+
+    st = np.full((R, W), -1, np.int8)
+    for k in range(rows):
+        st[R // 2 + 2 * k, ::2] = 0  # isolated free cells: W / 2 clusters per row
+    p = cases.make_params(W, R)
+    mask, labels, clusters = _oracle_clusters(oracle_lib, p, st)
+    assert len(clusters) > 4096
+    with dm.OccupancyMapper(p) as m:
+        m.set_state(st)
+        for _ in range(2):
+            assert_frontiers_equal(m.frontiers(want_mask=True, want_labels=True), mask, labels, clusters)
