@@ -488,8 +488,8 @@ def pmc_traffic(kernel, workload):
 FRONTIER_KERNELS = ("frontier_prep", "frontier_bits", "frontier_tile", "frontier_big", "frontier_merge", "frontier_resolve",
                     "frontier_compact", "sort_clusters")
 PMC_FRONTIER_KERNELS = ("k_frontier_prep", "k_frontier_bits", "k_frontier_tile", "k_frontier_tile_big", "k_frontier_merge", "k_frontier_resolve",
-                        "k_frontier_compact", "k_rank_sort", "k_bs_count", "k_bs_scan", "k_bs_place",
-                        "k_bs_rank")
+                        "k_frontier_compact", "k_rank_sort", "k_rx_init", "k_rx_hist", "k_rx_scan",
+                        "k_rx_scatter", "k_rx_emit")
 
 
 def frontier_roofline(avg, cells, F, K, tiles_visited, workload, wall_s=None):

@@ -127,6 +127,7 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   const int64_t segs = nb * per_beam;
   if (segs > g->segs_cap) {
     for (auto& w : g->iw) {
+      if (&w - g->iw >= g->n_iw) break;
       int rc = dev_alloc(&w.pieces, segs, "ray pieces");
       if (rc) { g->segs_cap = 0; return rc; }
     }
@@ -137,8 +138,8 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   if (act < 1) act = 1;
   if (act > g->act_cap) {
     int rc = dev_alloc(&g->act_raw, act * kShards, "first-touch lists");
-    for (auto& w : g->iw)
-      if (!rc) rc = dev_alloc(&w.litems, act, "light work items");
+    for (int i = 0; i < g->n_iw; ++i)
+      if (!rc) rc = dev_alloc(&g->iw[i].litems, act, "light work items");
     if (rc) { g->act_cap = 0; return rc; }
     g->act_cap = act;
   }
@@ -150,6 +151,7 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   const int64_t hitems = segs / chunk + segs / (chunk + 1) + 2;
   if (hitems > g->hitem_cap) {
     for (auto& w : g->iw) {
+      if (&w - g->iw >= g->n_iw) break;
       int rc = dev_alloc(&w.hitems, hitems, "heavy work items");
       if (rc) { g->hitem_cap = 0; return rc; }
     }
@@ -157,6 +159,7 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   }
   if (heavy > g->heavy_cap) {
     for (auto& w : g->iw) {
+      if (&w - g->iw >= g->n_iw) break;
       int rc = dev_alloc(&w.heavy_list, heavy, "heavy tiles");
       if (!rc) rc = dev_alloc(&w.slabs, heavy * 2 * DM_TILE * DM_TILE, "heavy-tile slabs");
       if (!rc) rc = dev_alloc(&w.heavy_done, heavy, "heavy-tile item tickets");
@@ -202,7 +205,8 @@ int dm_grow_bucket_sort(dm_grid* g, int64_t n) {
   if (!rc) rc = dev_alloc(&g->bs_key2, n, "radix-sort keys");
   if (!rc) rc = dev_alloc(&g->bs_idx, n, "radix-sort indices");
   if (!rc) rc = dev_alloc(&g->bs_idx2, n, "radix-sort indices");
-  if (!rc) rc = dev_alloc(&g->bs_hist, 256 * (ceil_div(n, 2048) + 1), "radix-sort histograms");  // k_rx_*: 2048 keys per block
+  // k_rx_*: digit x block counts (up to 2^11 digits, blocks of kRxItems keys)
+  if (!rc) rc = dev_alloc(&g->bs_hist, ((int64_t)1 << g->rx_bits) * (ceil_div(n, dm_rx_items()) + 1), "radix-sort histograms");
   if (rc) { g->bs_cap = 0; return rc; }
   g->bs_cap = n;
   return DM_OK;
@@ -476,7 +480,9 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   };
   if ((rc = dev_alloc(&g->L, cells, "log-odds"))) return fail(rc);
   if ((rc = dev_alloc(&g->state, cells, "state"))) return fail(rc);
+  if (const char* is = getenv("DM_INT_SETS")) g->n_iw = std::min(dm_grid::kIntSetsMax, std::max(2, atoi(is)));
   for (auto& w : g->iw) {
+    if (&w - g->iw >= g->n_iw) break;
     if ((rc = dev_alloc(&w.tile_count, g->NT, "tile counts"))) return fail(rc);
     if ((rc = dev_alloc(&w.tile_cur, g->NT, "tile bin cursors"))) return fail(rc);
     if ((rc = dev_alloc(&w.cnt, CNT_N, "integrate counters"))) return fail(rc);
@@ -510,6 +516,9 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     g->fmask_mode = fm && !strcmp(fm, "on") ? 1 : (fm && !strcmp(fm, "off") ? 2 : 0);
     const char* fk = getenv("DM_FRONTIER_KERNEL");
     g->frontier_kernel = fk && !strcmp(fk, "wave") ? 1 : (fk && !strcmp(fk, "wg") ? 2 : 0);
+    if (const char* sm = getenv("DM_SORT_MIN")) g->sort_min = std::max<int64_t>(0, atoll(sm));
+    if (const char* rb = getenv("DM_RX_BITS")) g->rx_bits = std::min(11, std::max(4, atoi(rb)));
+    g->big_concurrent = !dm_env_off("DM_BIG_STREAM");
   }
   for (auto& f : g->fw) {
     if ((rc = dev_alloc(&f.cnt, CNT_N, "frontier counters"))) return fail(rc);
@@ -597,7 +606,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   // waits on a readback slot's event and then reads mapped host memory:
   // default fences.
   for (hipEvent_t* ev : {&g->ev_fe, &g->ev_bits[0], &g->ev_bits[1], &g->iw[0].ev_free, &g->iw[1].ev_free,
-                         &g->ev_bigfork, &g->ev_big}) {
+                         &g->iw[2].ev_free, &g->ev_bigfork, &g->ev_big}) {
     e = hipEventCreateWithFlags(ev, hipEventDisableTiming | hipEventDisableSystemFence);
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
   }
@@ -622,7 +631,7 @@ int dm_destroy(dm_grid* g) {
   dm_batch_release(&g->batch);
   for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
   for (hipEvent_t ev : {g->ev_fe, g->ev_bits[0], g->ev_bits[1], g->iw[0].ev_free, g->iw[1].ev_free,
-                        g->ev_bigfork, g->ev_big})
+                        g->iw[2].ev_free, g->ev_bigfork, g->ev_big})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& r : g->rb) {
     if (r.ev) (void)hipEventDestroy(r.ev);
@@ -675,8 +684,8 @@ int dm_reset(dm_grid* g) {
   DM_HIP(hipMemsetAsync(g->L, 0, sizeof(float) * (size_t)cells, g->stream));
   DM_HIP(hipMemsetAsync(g->state, 0xFF, (size_t)cells, g->stream));
   DM_HIP(dm_sync_all(g));
-  for (auto& w : g->iw)
-    DM_HIP(hipMemsetAsync(w.tile_count, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
+  for (int i = 0; i < g->n_iw; ++i)
+    DM_HIP(hipMemsetAsync(g->iw[i].tile_count, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
   DM_HIP(hipMemsetAsync(g->tile_free, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
   if ((rc = dm_launch_recount(g))) return rc;  // fmask: every in-grid cell unknown
   for (auto& f : g->fw) DM_HIP(hipMemsetAsync(f.cnt, 0, sizeof(unsigned long long) * CNT_N, g->stream));

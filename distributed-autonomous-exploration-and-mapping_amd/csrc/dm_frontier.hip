@@ -1357,7 +1357,7 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
   }
 }
 
-// ---- LSD radix sort for many clusters (K > kBucketSortMin) ----------------
+// ---- LSD radix sort for many clusters (K > the handle's sort_min, DM_SORT_MIN) ----------------
 // The rank sort is O(K^2): ~0.1 ms at 23k clusters, far more at the 2e5+
 // clusters of a sparse 1 cm map (C5).  Labels are unique row-major cell
 // indices in [base, base + span) (span = rows * W: the band's or the map's
@@ -1383,7 +1383,7 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
 constexpr int kRxThreads = 256;
 constexpr int kRxRounds = 8;                      // keys per thread, all loaded up front
 constexpr int kRxItems = kRxThreads * kRxRounds;  // keys per block
-constexpr int kRxMaxRadix = 256;
+constexpr int kRxMaxRadix = 2048;  // digits of up to 11 bits (DM_RX_BITS)
 constexpr int kRxScanThreads = 1024;
 
 __global__ __launch_bounds__(kRxThreads) void k_rx_init(const long long* __restrict__ clusters,
@@ -1585,6 +1585,8 @@ int grid_for(int64_t n, int threads, int64_t cap) {
 
 static_assert(sizeof(FGeom) == 88, "FGeom has no implicit padding");
 
+int64_t dm_rx_items() { return kRxItems; }
+
 static FGeom make_fgeom(const dm_grid* g, bool want_mask, bool want_labels) {
   FGeom fg;
   fg.W = (int32_t)g->W;
@@ -1648,7 +1650,7 @@ int dm_launch_bucket_sort(dm_grid* g, hipStream_t stream, long long* clusters, c
   const unsigned long long span = (unsigned long long)rows * (unsigned long long)g->W;
   int bits = 1;
   while (bits < 64 && (span - 1) >> bits) ++bits;
-  const int passes = (bits + 7) / 8;
+  const int passes = (bits + g->rx_bits - 1) / g->rx_bits;
   const int db = (bits + passes - 1) / passes;
   // grids follow the expected count (the kernels stride; blocks past the
   // device-side count return)
@@ -1782,20 +1784,26 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
     // the wave kernel: the round-2 launch order ran them after it (C5 at 192
     // beams: 157 us of big tiles behind 194 us of wave tiles).  The tile-edge
     // hand-off unites tiles whatever kernel and order processed them.
-    DM_HIP(dm_batch_flush_all());
-    DM_HIP(hipEventRecord(g->ev_bigfork, ps));
-    DM_HIP(hipStreamWaitEvent(g->big_stream, g->ev_bigfork, 0));
-    dm_timer_begin(g, "frontier_big", &t, g->big_stream);
     // the grid follows the last pass's count (the kernel grid-strides)
     const int big_grid =
         grid_for(std::min<int64_t>(g->NT, dm_quantize_up(g->big_hint + g->big_hint / 4 + 64)), 1, 8192);
-    DM_LAUNCH(k_frontier_tile_big, dim3(big_grid), dim3(kFT), 0, g->big_stream, fg, g->fbits, g->big_tiles,
-              g->ftiles, list_n, g->border, g->rel, g->slot_label, g->slot_parent, g->slot_own,
-              g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh, 0);
-    dm_timer_end(g, &t);
-    DM_HIP(hipGetLastError());
-    DM_HIP(dm_batch_flush_all());
-    DM_HIP(hipEventRecord(g->ev_big, g->big_stream));
+    auto launch_big = [&](hipStream_t bs) -> int {
+      dm_timer_begin(g, "frontier_big", &t, bs);
+      DM_LAUNCH(k_frontier_tile_big, dim3(big_grid), dim3(kFT), 0, bs, fg, g->fbits, g->big_tiles,
+                g->ftiles, list_n, g->border, g->rel, g->slot_label, g->slot_parent, g->slot_own,
+                g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh, 0);
+      dm_timer_end(g, &t);
+      DM_HIP(hipGetLastError());
+      return DM_OK;
+    };
+    if (g->big_concurrent) {
+      DM_HIP(dm_batch_flush_all());
+      DM_HIP(hipEventRecord(g->ev_bigfork, ps));
+      DM_HIP(hipStreamWaitEvent(g->big_stream, g->ev_bigfork, 0));
+      if (int rc = launch_big(g->big_stream)) return rc;
+      DM_HIP(dm_batch_flush_all());
+      DM_HIP(hipEventRecord(g->ev_big, g->big_stream));
+    }
     dm_timer_begin(g, "frontier_tile", &t, ps);
     DM_LAUNCH(k_frontier_tile, dim3(wave_grid), dim3(kFW * 64), 0, ps, fg, g->fbits,
                        g->ftiles, list_n, g->border, g->rel,
@@ -1803,8 +1811,12 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
                        g->edge_slot, g->cnt, g->fsh, g->big_tiles);
     dm_timer_end(g, &t);
     DM_HIP(hipGetLastError());
-    DM_HIP(dm_batch_flush_all());
-    DM_HIP(hipStreamWaitEvent(ps, g->ev_big, 0));
+    if (g->big_concurrent) {
+      DM_HIP(dm_batch_flush_all());
+      DM_HIP(hipStreamWaitEvent(ps, g->ev_big, 0));
+    } else if (int rc = launch_big(ps)) {
+      return rc;
+    }
   } else {
     dm_timer_begin(g, "frontier_tile", &t, ps);
     // one workgroup per listed tile of the last collected pass (+25 %; the
@@ -1843,7 +1855,7 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   dm_timer_begin(g, "sort_clusters", &t, ps);
   // the last collected pass predicts this one's cluster count (either sort
   // is exact for any count; only their speed differs)
-  const int rc = g->sort_hint > kBucketSortMin
+  const int rc = g->sort_hint > g->sort_min
       ? dm_launch_bucket_sort(g, ps, g->clusters, fuse ? g->slot_acc : nullptr, fuse ? g->slot_label : nullptr,
                               g->cnt + CNT_CLUSTERS, g->slot_cap, g->row0, g->R, g->out_clu,
                               g->rank_of, g->cnt + CNT_SORTED, g->cnt, CNT_N, CNT_SORTED, g->fsh,

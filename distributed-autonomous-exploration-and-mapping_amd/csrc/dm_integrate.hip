@@ -1332,9 +1332,9 @@ DM_PH_READER(integrate)
 int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                         const float* d_ranges, const double* d_trig) {
   const int64_t nb = (int64_t)S * N;
-  // calls alternate between the two workspace sets; this one was last used
-  // two calls ago
-  g->iw_cur ^= 1;
+  // calls cycle through the workspace sets; this one was last used n_iw
+  // calls ago
+  g->iw_cur = (g->iw_cur + 1) % g->n_iw;
   dm_grid::IntWs& w = g->iw[g->iw_cur];
   // the kernels below go out as one graph per stream (dm_batch.h)
   DmBatchScope batch(&g->batch, !g->profile);

@@ -245,7 +245,12 @@ struct dm_grid {
     hipEvent_t free_wait = nullptr;
     bool free_owed = false;
   };
-  IntWs iw[2];
+  // calls cycle through n_iw sets (DM_INT_SETS=2|3, read at dm_create):
+  // with 3, call k+1's front-end waits for call k-2's accumulation instead of
+  // call k-1's, so it can run while call k-1's accumulation is dispatched
+  static constexpr int kIntSetsMax = 3;
+  IntWs iw[kIntSetsMax];
+  int n_iw = 2;
   int iw_cur = 0;                // set of the last integrate call
   // heavy tiles applied by their last k_tile_accum item (default) instead of
   // a separate k_heavy_apply launch (DM_HEAVY_SEPARATE=1, A/B measurement)
@@ -336,17 +341,25 @@ struct dm_grid {
   bool frontier_valid = false;
 
   // large-K cluster sort (LSD radix, dm_frontier.hip k_rx_*): used when
-  // the last collected pass of its kind had more than kBucketSortMin clusters
+  // the last collected pass of its kind had more than sort_min clusters
   unsigned long long* bs_key = nullptr;   // [bs_cap] radix-sort keys (label - base), two buffers
   unsigned long long* bs_key2 = nullptr;
   int32_t* bs_idx = nullptr;      // [bs_cap] their record indices, two buffers
   int32_t* bs_idx2 = nullptr;
-  int32_t* bs_hist = nullptr;     // [256][ceil(bs_cap / 2048)] digit x block counts -> offsets
+  int32_t* bs_hist = nullptr;     // [2^rx_bits][ceil(bs_cap / kRxItems)] digit x block counts -> offsets
   int64_t bs_cap = 0;
   int64_t sort_hint = 0, msort_hint = 0;  // clusters of the last band / merge readback
   int64_t ftile_hint = 0;                 // listed tiles of the last collected frontier pass
   int64_t runs_hint = 0, ftf_hint = 0;    // its runs and tiles with frontier cells
   int64_t big_hint = 0;                   // its tiles left to k_frontier_tile_big by k_frontier_tile
+  // A/B knobs of the pass (read at dm_create): the cluster count above which
+  // the radix sort replaces the rank sort (DM_SORT_MIN), the radix digit
+  // width cap (DM_RX_BITS, 4..11), and whether the run-rich tiles' kernel
+  // runs beside the wave kernel on big_stream (DM_BIG_STREAM=0: after it,
+  // on the pass stream)
+  int64_t sort_min = 4096;
+  int rx_bits = 8;
+  bool big_concurrent = true;
   // tile kernel choice: 0 from those statistics, 1 always the wave-per-tile
   // kernel, 2 always the 256-thread kernel (DM_FRONTIER_KERNEL=auto|wave|wg,
   // read at dm_create, for A/B measurements; all three are exact)
@@ -407,7 +420,12 @@ inline void dm_select_slot(dm_grid* g, int slot) {
 // accumulation is enqueued on g->stream before this point): `recorded`, an
 // event just recorded on g->stream, or each set's own ev_free recorded now.
 inline hipError_t dm_mark_ws_free(dm_grid* g, hipEvent_t recorded = nullptr) {
-  for (auto& w : g->iw) {
+  // `recorded` (a pass-parity or readback-slot event) is re-recorded two
+  // passes later: with 3 sets a front-end would then wait for a later
+  // accumulation than its set's own, so each set records its own event
+  if (g->n_iw > 2) recorded = nullptr;
+  for (int i = 0; i < g->n_iw; ++i) {
+    dm_grid::IntWs& w = g->iw[i];
     if (!w.free_owed) continue;
     w.free_owed = false;
     w.free_wait = recorded ? recorded : w.ev_free;
@@ -484,9 +502,8 @@ int dm_launch_rank_sort(hipStream_t stream, long long* clusters, const long long
                         int64_t host_cap, int64_t expect);
 // Listed tiles from which a frontier pass reads fmask instead of state bytes.
 constexpr int64_t kFmaskOnTiles = 8192;
-// Clusters above which the radix sort replaces the O(K^2) rank sort.
-constexpr int64_t kBucketSortMin = 4096;
 int dm_grow_bucket_sort(dm_grid* g, int64_t n);
+int64_t dm_rx_items();  // keys per radix-sort block (dm_frontier.hip)
 // LSD radix sort of the raw records (labels of rows [row_base, row_base +
 // rows)): same outputs, readback header and flags as dm_launch_rank_sort.
 int dm_launch_bucket_sort(dm_grid* g, hipStream_t stream, long long* clusters, const long long* sums,

@@ -290,7 +290,7 @@ int dm_launch_merge(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t 
                      g->m_acc, g->m_clu, g->m_cnt);
   DM_HIP(hipGetLastError());
   // merged labels are global row-major indices over the whole map
-  const int rc = g->msort_hint > kBucketSortMin
+  const int rc = g->msort_hint > g->sort_min
       ? dm_launch_bucket_sort(g, g->stream, g->m_clu, nullptr, nullptr, g->m_cnt + M_K, n, 0, g->H, g->m_out, nullptr, g->m_cnt + M_SORTED,
                               g->m_cnt, 4, M_SORTED, nullptr, g->h_out_dev, g->h_out_cap)
       : dm_launch_rank_sort(g->stream, g->m_clu, nullptr, nullptr, g->m_cnt + M_K, n, g->p.origin_x, g->p.origin_y,
