@@ -120,9 +120,23 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
     int rc = dev_alloc(&g->beams, nbc, "beams");
     if (!rc) rc = dev_alloc(&g->blk_hist, bc * 1024, "per-block tile histograms");
     if (!rc) rc = dev_alloc(&g->blk_n, bc, "per-block histogram sizes");
+    if (!rc) rc = dev_alloc(&g->blk_np, bc, "per-block staged pieces");
     if (rc) { g->beams_cap = g->blk_cap = 0; return rc; }
     g->beams_cap = nbc;
     g->blk_cap = bc;
+  }
+  // staged pieces: a region of 256 threads x the per-beam bound per workgroup
+  // (a thread enumerates one beam or one k-range of it)
+  if (g->fe_staged) {
+    const int64_t sb = std::max<int64_t>(256 * per_beam, g->stage_blk);
+    const int64_t sc = sb * g->blk_cap;
+    if (sc > g->stage_cap) {
+      int rc = dev_alloc(&g->stage, sc, "staged ray pieces");
+      if (!rc) rc = dev_alloc(&g->stage_sr, sc, "staged piece places");
+      if (rc) { g->stage_cap = g->stage_blk = 0; return rc; }
+      g->stage_cap = sc;
+    }
+    g->stage_blk = sb;
   }
   const int64_t segs = nb * per_beam;
   if (segs > g->segs_cap) {
@@ -519,6 +533,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     if (const char* sm = getenv("DM_SORT_MIN")) g->sort_min = std::max<int64_t>(0, atoll(sm));
     if (const char* rb = getenv("DM_RX_BITS")) g->rx_bits = std::min(11, std::max(4, atoi(rb)));
     g->big_concurrent = !dm_env_off("DM_BIG_STREAM");
+    g->fe_staged = !dm_env_off("DM_FE_STAGED");
   }
   for (auto& f : g->fw) {
     if ((rc = dev_alloc(&f.cnt, CNT_N, "frontier counters"))) return fail(rc);
@@ -655,6 +670,7 @@ int dm_destroy(dm_grid* g) {
   }
   dev_free(g->L); dev_free(g->state); dev_free(g->fmask);
   dev_free(g->tile_free); dev_free(g->beams); dev_free(g->blk_hist); dev_free(g->blk_n);
+  dev_free(g->blk_np); dev_free(g->stage); dev_free(g->stage_sr);
   dev_free(g->trig);
   dev_free(g->pose4); dev_free(g->ranges); 
   dev_free(g->bs_key); dev_free(g->bs_key2); dev_free(g->bs_idx); dev_free(g->bs_idx2); dev_free(g->bs_hist);

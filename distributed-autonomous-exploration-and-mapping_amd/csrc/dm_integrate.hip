@@ -43,6 +43,7 @@ struct Geom {
   int32_t chunks, chunk_len;  // each beam enumerated as `chunks` k-ranges (dm_integrate_chunks)
   int32_t sparse_pieces;  // light tiles with at most this many pieces are sparse items
   int32_t pad;
+  int64_t stage_blk;  // staged pieces per k_beam_prep workgroup (0: not staged, k_scatter places them)
 };
 
 // Thread v of k_beam_prep / k_scatter: beam v % nb, k-range v / nb (chunk-
@@ -141,19 +142,41 @@ __device__ inline void first_touch(const Geom& g, int32_t tile, int32_t old, int
   else atomicOr(&cnt[CNT_IOVERFLOW], 1ull);
 }
 
+// A piece as k_tile_accum consumes it: tile-local LDS addresses (pitch
+// kLdsPitch), packed to 16 bytes (dm_ray.h).
+__device__ inline PackedPiece make_piece(const Geom& g, const Beam& bm, int32_t tile, int32_t k0, int32_t k1) {
+  const int32_t tx0 = (tile % g.r.TX) * DM_TS;
+  const int32_t ty0 = (tile / g.r.TX) * DM_TS;
+  return dm_pack_piece(dm_tile_piece(bm, k0, k1, g.r.row0, tx0, ty0, kLdsPitch));
+}
+
+// stage_sr code of a piece counted straight into tile_count (its tile found
+// no slot in the workgroup's LDS table): k_gather bumps the tile's cursor
+constexpr uint32_t kStageGlobal = 0x80000000u;
+
+// Staged mode (g.stage_blk > 0, the default): every piece is also packed and
+// stored in this workgroup's region of `stage`, in enumeration order, with its
+// place in the workgroup's histogram (hash slot | rank among the slot's pieces
+// << 16); k_gather moves it into its tile's bin after k_plan, so the beams are
+// enumerated once per call instead of twice (k_beam_prep, then k_scatter).
+// Emission index: one LDS bump per wave per emitting step.
 __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const double* __restrict__ pose4,
                                                    const float* __restrict__ ranges,
                                                    const double* __restrict__ trig,
                                                    Beam* __restrict__ beams, int32_t* tile_count,
                                                    int32_t* act_raw, unsigned long long* ish,
                                                    int2* __restrict__ blk_hist, int32_t* __restrict__ blk_n,
-                                                   unsigned long long* cnt) {
+                                                   PackedPiece* __restrict__ stage, uint32_t* __restrict__ stage_sr,
+                                                   int32_t* __restrict__ blk_np, unsigned long long* cnt) {
   __shared__ int32_t hkey[kHash];
   __shared__ int32_t hcnt[kHash];
-  __shared__ int32_t s_nh;
-  const int tid = threadIdx.x;
+  __shared__ int32_t s_nh, s_np;
+  const int tid = threadIdx.x, lane = lane_id();
   for (int e = tid; e < kHash; e += 256) { hkey[e] = -1; hcnt[e] = 0; }
+  if (tid == 0) { s_nh = 0; s_np = 0; }
   __syncthreads();
+  const bool staged = g.stage_blk > 0;
+  const int64_t sbase = (int64_t)blockIdx.x * g.stage_blk;
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + tid;
   if (v < g.nb * g.chunks) {
     const BeamChunk bc = beam_chunk(g, v);
@@ -161,34 +184,66 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
     const Beam bm = dm_make_beam(a, pose4, ranges, trig, s, i);
     if (bc.k_lo == 0) beams[bc.b] = bm;
     if ((bm.flags & 1) && bc.k_lo <= bm.n) {
-      dm_for_each_piece(bm, g.r, [&](int32_t tile, int32_t, int32_t) {
+      dm_for_each_piece(bm, g.r, [&](int32_t tile, int32_t k0, int32_t k1) {
         const LaneRun run = lane_run(tile);
+        if (!staged) {
+          if (run.head) {
+            const int h = hash_insert(hkey, tile);
+            if (h >= 0) {
+              atomicAdd(&hcnt[h], run.len);
+            } else {
+              const int32_t old = atomicAdd(&tile_count[tile], run.len);
+              first_touch(g, tile, old, act_raw, ish, cnt);
+            }
+          }
+          return;
+        }
+        uint32_t sr = 0u;
         if (run.head) {
           const int h = hash_insert(hkey, tile);
           if (h >= 0) {
-            atomicAdd(&hcnt[h], run.len);
+            sr = (uint32_t)h | ((uint32_t)atomicAdd(&hcnt[h], run.len) << 16);
           } else {
             const int32_t old = atomicAdd(&tile_count[tile], run.len);
             first_touch(g, tile, old, act_raw, ish, cnt);
+            sr = kStageGlobal | (uint32_t)tile;
           }
+        }
+        sr = __shfl(sr, run.head_lane);
+        if (!(sr & kStageGlobal)) sr += (uint32_t)run.rank << 16;  // the slot's rank (< 2^15: <= 512 pieces)
+        // this wave's emitting lanes take consecutive staging entries
+        const unsigned long long act = __ballot(1);
+        const int lead = __ffsll(act) - 1;
+        int32_t e0 = 0;
+        if (lane == lead) e0 = atomicAdd(&s_np, __popcll(act));
+        const int64_t e = (int64_t)__shfl(e0, lead) + __popcll(act & ((1ull << lane) - 1ull));
+        if (e < g.stage_blk) {
+          stage[sbase + e] = make_piece(g, bm, tile, k0, k1);
+          stage_sr[sbase + e] = sr;
         }
       }, bc.k_lo, bc.k_hi);
     }
   }
-  if (tid == 0) s_nh = 0;
   __syncthreads();
-  // flush the histogram, and keep it (compacted) for k_scatter: its single
-  // placement pass then needs no counting pass of its own
+  // flush the histogram, and keep it (compacted, with each entry's hash slot)
+  // for k_gather / k_scatter: their single placement pass then needs no
+  // counting pass of its own
   int2* my_hist = blk_hist + (int64_t)blockIdx.x * kHash;
   for (int e = tid; e < kHash; e += 256) {
     const int32_t tile = hkey[e];
     if (tile < 0) continue;
     const int32_t old = atomicAdd(&tile_count[tile], hcnt[e]);
     first_touch(g, tile, old, act_raw, ish, cnt);
-    my_hist[atomicAdd(&s_nh, 1)] = make_int2(tile, hcnt[e]);
+    my_hist[atomicAdd(&s_nh, 1)] = make_int2(tile, hcnt[e] | (e << 16));
   }
   __syncthreads();
-  if (tid == 0) blk_n[blockIdx.x] = s_nh;
+  if (tid == 0) {
+    blk_n[blockIdx.x] = s_nh;
+    if (staged) {
+      blk_np[blockIdx.x] = s_np;
+      if ((int64_t)s_np > g.stage_blk) atomicOr(&cnt[CNT_IOVERFLOW], 2ull);  // cannot happen (grow_integrate's bound)
+    }
+  }
 }
 
 // Work plan for the apply phase (one block).  A tile's pieces are cut into
@@ -335,16 +390,50 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan(Geom g, const int32_t* __
   }
 }
 
-// A piece as k_tile_accum consumes it: tile-local LDS addresses (pitch
-// kLdsPitch), packed to 16 bytes (dm_ray.h).
 __device__ inline void put_piece(const Geom& g, PackedPiece* pieces, int64_t idx, const Beam& bm,
                                  int32_t tile, int32_t k0, int32_t k1, unsigned long long* cnt) {
   if (idx >= 0 && idx < g.seg_cap) {
-    const int32_t tx0 = (tile % g.r.TX) * DM_TS;
-    const int32_t ty0 = (tile / g.r.TX) * DM_TS;
-    pieces[idx] = dm_pack_piece(dm_tile_piece(bm, k0, k1, g.r.row0, tx0, ty0, kLdsPitch));
+    pieces[idx] = make_piece(g, bm, tile, k0, k1);
   } else {
     atomicOr(&cnt[CNT_IOVERFLOW], 2ull);
+  }
+}
+
+// Staged pieces -> per-tile bins (replaces k_scatter's second enumeration):
+// one workgroup per k_beam_prep workgroup; one cursor bump per histogram
+// entry reserves the workgroup's range of each tile's bin (hbase, by hash
+// slot), then every staged piece goes to hbase[slot] + its rank.  Pieces of a
+// tile that found no LDS slot bump the tile's cursor one by one (rare: the
+// table holds 1024 tiles per 256 beams).  The first round's loads go out
+// before the cursor bumps.
+__global__ __launch_bounds__(256) void k_gather(Geom g, int32_t* tile_cur, const int2* __restrict__ blk_hist,
+                                                const int32_t* __restrict__ blk_n,
+                                                const int32_t* __restrict__ blk_np,
+                                                const PackedPiece* __restrict__ stage,
+                                                const uint32_t* __restrict__ stage_sr,
+                                                PackedPiece* __restrict__ pieces, unsigned long long* cnt) {
+  __shared__ int32_t hbase[kHash];
+  const int tid = threadIdx.x;
+  const int32_t nh = blk_n[blockIdx.x];
+  const int32_t np = (int32_t)min((int64_t)blk_np[blockIdx.x], g.stage_blk);
+  const int64_t sbase = (int64_t)blockIdx.x * g.stage_blk;
+  PackedPiece pc = tid < np ? stage[sbase + tid] : PackedPiece{0u, 0u, 0u, 1u};
+  uint32_t sr = tid < np ? stage_sr[sbase + tid] : 0u;
+  const int2* my_hist = blk_hist + (int64_t)blockIdx.x * kHash;
+  for (int e = tid; e < nh; e += 256) {
+    const int2 te = my_hist[e];
+    hbase[te.y >> 16] = atomicAdd(&tile_cur[te.x], te.y & 0xFFFF);
+  }
+  __syncthreads();
+  for (int32_t e = tid; e < np; e += 256) {
+    if (e != tid) {
+      pc = stage[sbase + e];
+      sr = stage_sr[sbase + e];
+    }
+    const int64_t dst = (sr & kStageGlobal) ? (int64_t)atomicAdd(&tile_cur[sr & ~kStageGlobal], 1)
+                                            : (int64_t)hbase[sr & 0xFFFFu] + (int64_t)(sr >> 16);
+    if (dst >= 0 && dst < g.seg_cap) pieces[dst] = pc;
+    else atomicOr(&cnt[CNT_IOVERFLOW], 2ull);
   }
 }
 
@@ -375,7 +464,7 @@ __global__ __launch_bounds__(256) void k_scatter(RayArgs a, Geom g, const Beam* 
   for (int e = tid; e < nh; e += 256) {
     const int2 te = my_hist[e];
     const int h = hash_insert(hkey, te.x);  // the same entries fit: same table size
-    if (h >= 0) hbase[h] = atomicAdd(&tile_cur[te.x], te.y);
+    if (h >= 0) hbase[h] = atomicAdd(&tile_cur[te.x], te.y & 0xFFFF);
   }
   __syncthreads();
   const bool valid = in && (bm.flags & 1) && bc.k_lo <= bm.n;
@@ -1283,7 +1372,7 @@ __global__ __launch_bounds__(256) void k_map_image(int64_t R, int64_t W, const i
   }
 }
 
-static_assert(sizeof(Geom) == 72 && sizeof(RayArgs) == 40 && sizeof(ApplyArgs) == 24,
+static_assert(sizeof(Geom) == 80 && sizeof(RayArgs) == 40 && sizeof(ApplyArgs) == 24,
               "kernel argument structs have no implicit padding (dm_batch.h cache keys)");
 
 Geom make_geom(const dm_grid* g) {
@@ -1302,6 +1391,7 @@ Geom make_geom(const dm_grid* g) {
   ge.chunk_len = 0;
   ge.sparse_pieces = std::min(g->sparse_pieces, kSparseMax);  // byte-packed counts (walk_piece_bytes)
   ge.pad = 0;
+  ge.stage_blk = 0;
   return ge;
 }
 
@@ -1373,8 +1463,10 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   const int nblk = (int)((nb * ge.chunks + 255) / 256);
   KernelTimer t;
   dm_timer_begin(g, "beam_prep", &t, fs);
+  ge.stage_blk = g->fe_staged ? g->stage_blk : 0;
   DM_LAUNCH(k_beam_prep, dim3(nblk), dim3(256), 0, fs, a, ge, d_pose4, d_ranges,
-                     d_trig, g->beams, w.tile_count, g->act_raw, w.sh, g->blk_hist, g->blk_n, w.cnt);
+                     d_trig, g->beams, w.tile_count, g->act_raw, w.sh, g->blk_hist, g->blk_n, g->stage,
+                     g->stage_sr, g->blk_np, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "plan", &t, fs);
@@ -1383,9 +1475,14 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                      w.heavy_list, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
+  // (the bench's kernel table keeps the name "scatter" for this stage either way)
   dm_timer_begin(g, "scatter", &t, fs);
-  DM_LAUNCH(k_scatter, dim3(nblk), dim3(256), 0, fs, a, ge, g->beams,
-                     w.tile_cur, g->blk_hist, g->blk_n, w.pieces, w.cnt);
+  if (ge.stage_blk > 0)
+    DM_LAUNCH(k_gather, dim3(nblk), dim3(256), 0, fs, ge, w.tile_cur, g->blk_hist, g->blk_n, g->blk_np,
+              g->stage, g->stage_sr, w.pieces, w.cnt);
+  else
+    DM_LAUNCH(k_scatter, dim3(nblk), dim3(256), 0, fs, a, ge, g->beams,
+                       w.tile_cur, g->blk_hist, g->blk_n, w.pieces, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (g->overlap && !g->fe_gate) {

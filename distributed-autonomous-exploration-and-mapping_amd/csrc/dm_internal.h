@@ -217,8 +217,22 @@ struct dm_grid {
   // integrate workspace
   Beam* beams = nullptr; int64_t beams_cap = 0;
   int64_t blk_cap = 0;            // workgroups blk_hist / blk_n hold
-  int2* blk_hist = nullptr;       // [beam blocks][1024] k_beam_prep's (tile, pieces) histogram
+  int2* blk_hist = nullptr;       // [beam blocks][1024] k_beam_prep's (tile, pieces | hash slot << 16) histogram
   int32_t* blk_n = nullptr;       // [beam blocks] its entries
+  // Staged front-end (default; DM_FE_STAGED=0: k_scatter's second
+  // enumeration instead): k_beam_prep stores every piece it enumerates,
+  // packed, in its workgroup's region of `stage` with its place in the
+  // workgroup's tile histogram (stage_sr: hash slot | rank << 16, or bit 31 |
+  // tile for a tile the LDS table could not hold); k_gather moves them into
+  // the tile bins once k_plan has placed the bins.  Shared by the workspace
+  // sets: k_gather of a call runs before the next call's k_beam_prep (both
+  // on the front-end stream).
+  bool fe_staged = true;
+  PackedPiece* stage = nullptr;   // [beam blocks][stage_blk]
+  uint32_t* stage_sr = nullptr;   // [beam blocks][stage_blk]
+  int32_t* blk_np = nullptr;      // [beam blocks] pieces staged
+  int64_t stage_blk = 0;          // staged pieces per workgroup region (256 threads x pieces per beam bound)
+  int64_t stage_cap = 0;          // pieces `stage` holds
   int64_t segs_cap = 0;           // pieces per workspace
   int32_t* act_raw = nullptr;    // [kShards][act_cap] first-touch lists per shard
   int64_t act_cap = 0;
