@@ -221,6 +221,14 @@ int dm_grow_bucket_sort(dm_grid* g, int64_t n) {
   if (!rc) rc = dev_alloc(&g->bs_idx2, n, "radix-sort indices");
   // k_rx_*: digit x block counts (up to 2^11 digits, blocks of kRxItems keys)
   if (!rc) rc = dev_alloc(&g->bs_hist, ((int64_t)1 << g->rx_bits) * (ceil_div(n, dm_rx_items()) + 1), "radix-sort histograms");
+  if (!rc && g->rs_rows < g->H) {  // row-bucket sort: rows of the whole map (merges sort over H rows)
+    rc = dev_alloc(&g->rs_cnt, g->H, "row-sort counters");
+    if (!rc) rc = dev_alloc(&g->rs_off, g->H + 1, "row-sort offsets");
+    if (!rc) {
+      DM_HIP(hipMemset(g->rs_cnt, 0, sizeof(int32_t) * (size_t)g->H));
+      g->rs_rows = g->H;
+    }
+  }
   if (rc) { g->bs_cap = 0; return rc; }
   g->bs_cap = n;
   return DM_OK;
@@ -532,8 +540,9 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     g->frontier_kernel = fk && !strcmp(fk, "wave") ? 1 : (fk && !strcmp(fk, "wg") ? 2 : 0);
     if (const char* sm = getenv("DM_SORT_MIN")) g->sort_min = std::max<int64_t>(0, atoll(sm));
     if (const char* rb = getenv("DM_RX_BITS")) g->rx_bits = std::min(11, std::max(4, atoi(rb)));
+    if (const char* ls = getenv("DM_LARGE_SORT")) g->row_sort = strcmp(ls, "radix") != 0;
     g->big_concurrent = !dm_env_off("DM_BIG_STREAM");
-    g->fe_staged = !dm_env_off("DM_FE_STAGED");
+    g->fe_staged = dm_env_on("DM_FE_STAGED");  // staged front-end: opt-in (A/B: slower pipelined)
   }
   for (auto& f : g->fw) {
     if ((rc = dev_alloc(&f.cnt, CNT_N, "frontier counters"))) return fail(rc);
@@ -674,6 +683,7 @@ int dm_destroy(dm_grid* g) {
   dev_free(g->trig);
   dev_free(g->pose4); dev_free(g->ranges); 
   dev_free(g->bs_key); dev_free(g->bs_key2); dev_free(g->bs_idx); dev_free(g->bs_idx2); dev_free(g->bs_hist);
+  dev_free(g->rs_cnt); dev_free(g->rs_off);
   dev_free(g->border); dev_free(g->rel); dev_free(g->slot_label); dev_free(g->slot_root);
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
   dev_free(g->edge_label); dev_free(g->mask); dev_free(g->labels);

@@ -1562,6 +1562,133 @@ __global__ __launch_bounds__(kRxThreads) void k_rx_emit(double ox, double oy, do
     put_sorted(ox, oy, res, clusters, sums, labels, vals[p], p, out, rank_of, host_out, host_cap);
 }
 
+// ---- row-bucket sort for many clusters (the default for K > sort_min) --------------------------
+// A label is the row-major index y * W + x of a component's first cell, so
+// label order is (row, column) order: one counting pass by row puts every
+// record in its row's range, and a record's place inside that range is the
+// number of records of the same row with a smaller column.  Four kernels
+// whatever the key width (the radix sort above needs 1 + 3 * passes + 1):
+//   k_rs_count  per record: key = label - base, row = key / W, slot = its
+//               arrival in the row (atomic on the row's counter)
+//   k_rs_scan   one workgroup: exclusive scan of the row counts -> row
+//               offsets (rows + 1 of them), and the counters back to zero
+//               for the next sort (they are zero when allocated)
+//   k_rs_place  record -> offset[row] + slot (unordered inside the row)
+//   k_rs_rank   position p: rank among its row's keys (a scan of the row's
+//               range, O(b) for a row of b records), then the same record
+//               write + readback header as k_rank_sort.
+// A frontier's components are spread over many rows (C5's 219k clusters of
+// 64 robots: a few per row), so b is small; a pathological row of b records
+// costs O(b^2) compares but stays exact.
+__global__ __launch_bounds__(256) void k_rs_count(const long long* __restrict__ clusters,
+                                                  const long long* __restrict__ labels,
+                                                  const unsigned long long* __restrict__ count, int64_t cap,
+                                                  long long base, int64_t W, int32_t* __restrict__ row_cnt,
+                                                  unsigned long long* __restrict__ keys, int32_t* __restrict__ slot) {
+  const int64_t K = (int64_t)*count;
+  if (K > cap) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < K; i += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long key = (unsigned long long)(record_key(clusters, labels, i) - base);
+    const int64_t row = (int64_t)(key / (unsigned long long)W);
+    keys[i] = key;
+    slot[i] = atomicAdd(&row_cnt[row], 1);
+  }
+}
+
+constexpr int kRsScanThreads = 1024;
+__global__ __launch_bounds__(kRsScanThreads) void k_rs_scan(const unsigned long long* __restrict__ count,
+                                                            int64_t cap, int64_t rows, int32_t* __restrict__ row_cnt,
+                                                            int32_t* __restrict__ row_off) {
+  __shared__ int32_t sv[kRxScanLds];
+  __shared__ int32_t wsum[kRsScanThreads / 64];
+  const int64_t K = (int64_t)*count;
+  if (K > cap) return;
+  const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+  int32_t carry = 0;
+  for (int64_t c0 = 0; c0 < rows; c0 += kRxScanLds) {
+    const int m = (int)min<int64_t>(kRxScanLds, rows - c0);
+    for (int j = tid; j < m; j += kRsScanThreads) {
+      sv[j] = row_cnt[c0 + j];
+      row_cnt[c0 + j] = 0;
+    }
+    __syncthreads();
+    const int per = (m + kRsScanThreads - 1) / kRsScanThreads;
+    const int lo = min(m, tid * per), hi = min(m, lo + per);
+    int32_t seg = 0;
+    for (int j = lo; j < hi; ++j) seg += sv[j];
+    int32_t incl = seg;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t t = __shfl_up(incl, d);
+      if (lane >= d) incl += t;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int32_t run = carry + incl - seg, total = 0;
+#pragma unroll
+    for (int q = 0; q < kRsScanThreads / 64; ++q) {
+      const int32_t ws = wsum[q];
+      run += q < w ? ws : 0;
+      total += ws;
+    }
+    for (int j = lo; j < hi; ++j) {
+      const int32_t x = sv[j];
+      sv[j] = run;
+      run += x;
+    }
+    carry += total;
+    __syncthreads();
+    for (int j = tid; j < m; j += kRsScanThreads) row_off[c0 + j] = sv[j];
+    __syncthreads();
+  }
+  if (tid == 0) row_off[rows] = carry;
+}
+
+__global__ __launch_bounds__(256) void k_rs_place(const unsigned long long* __restrict__ count, int64_t cap,
+                                                  int64_t W, const unsigned long long* __restrict__ keys,
+                                                  const int32_t* __restrict__ slot,
+                                                  const int32_t* __restrict__ row_off,
+                                                  unsigned long long* __restrict__ keys_out,
+                                                  int32_t* __restrict__ idx_out) {
+  const int64_t K = (int64_t)*count;
+  if (K > cap) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < K; i += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long key = keys[i];
+    const int64_t p = (int64_t)row_off[(int64_t)(key / (unsigned long long)W)] + slot[i];
+    keys_out[p] = key;
+    idx_out[p] = (int32_t)i;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rs_rank(double ox, double oy, double res, long long* clusters,
+                                                 const long long* sums, const long long* labels,
+                                                 const unsigned long long* __restrict__ count, int64_t cap,
+                                                 int64_t W, const unsigned long long* __restrict__ keys,
+                                                 const int32_t* __restrict__ idx,
+                                                 const int32_t* __restrict__ row_off,
+                                                 dm_cluster* __restrict__ out, int32_t* __restrict__ rank_of,
+                                                 unsigned long long* sorted, const unsigned long long* __restrict__ cnt,
+                                                 int ncnt, int sorted_idx, const unsigned long long* __restrict__ fsh,
+                                                 dm_cluster* __restrict__ host_out, int64_t host_cap) {
+  const int64_t K = (int64_t)*count;
+  if (blockIdx.x == 0) write_rb_header(K, cap, sorted, cnt, ncnt, sorted_idx, fsh, host_out);
+  if (K > cap) {
+    fix_raw_records(clusters, sums, labels, K);
+    return;
+  }
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < K; p += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long key = keys[p];
+    const int64_t row = (int64_t)(key / (unsigned long long)W);
+    const int32_t lo = row_off[row], hi = row_off[row + 1];
+    int32_t r = 0;
+    int32_t q = lo;
+    for (; q + 4 <= hi; q += 4)
+      r += (keys[q] < key) + (keys[q + 1] < key) + (keys[q + 2] < key) + (keys[q + 3] < key);
+    for (; q < hi; ++q) r += keys[q] < key;
+    put_sorted(ox, oy, res, clusters, sums, labels, idx[p], (int64_t)lo + r, out, rank_of, host_out, host_cap);
+  }
+}
+
 // Cell slot -> final label (the root of a set is its min-label slot).
 __global__ __launch_bounds__(256) void k_slot_labels(int64_t n, int64_t slot_cap, const int32_t* __restrict__ cslot,
                                                      const int32_t* __restrict__ slot_root,
@@ -1647,6 +1774,25 @@ int dm_launch_bucket_sort(dm_grid* g, hipStream_t stream, long long* clusters, c
                         (long long)max_records);
   // key = label - base over [0, span)
   const long long base = row_base * g->W;
+  if (g->row_sort && rows <= g->rs_rows) {
+    // grids follow the expected count (the kernels stride; blocks past the
+    // device-side count return)
+    const int64_t expect = std::min<int64_t>(max_records, std::max<int64_t>(2 * g->sort_hint, 4096));
+    const int eg = grid_for(expect, 256, 4096);
+    DM_LAUNCH(k_rs_count, dim3(eg), dim3(256), 0, stream, clusters, labels, d_count, max_records, base, g->W,
+              g->rs_cnt, g->bs_key, g->bs_idx2);
+    DM_HIP(hipGetLastError());
+    DM_LAUNCH(k_rs_scan, dim3(1), dim3(kRsScanThreads), 0, stream, d_count, max_records, rows, g->rs_cnt, g->rs_off);
+    DM_HIP(hipGetLastError());
+    DM_LAUNCH(k_rs_place, dim3(eg), dim3(256), 0, stream, d_count, max_records, g->W, g->bs_key, g->bs_idx2,
+              g->rs_off, g->bs_key2, g->bs_idx);
+    DM_HIP(hipGetLastError());
+    DM_LAUNCH(k_rs_rank, dim3(eg), dim3(256), 0, stream, g->p.origin_x, g->p.origin_y, g->p.resolution, clusters,
+              sums, labels, d_count, max_records, g->W, g->bs_key2, g->bs_idx, g->rs_off, out, rank_of, d_sorted, cnt,
+              ncnt, sorted_idx, fsh, host_out, host_cap);
+    DM_HIP(hipGetLastError());
+    return DM_OK;
+  }
   const unsigned long long span = (unsigned long long)rows * (unsigned long long)g->W;
   int bits = 1;
   while (bits < 64 && (span - 1) >> bits) ++bits;

@@ -154,12 +154,21 @@ __device__ inline PackedPiece make_piece(const Geom& g, const Beam& bm, int32_t 
 // no slot in the workgroup's LDS table): k_gather bumps the tile's cursor
 constexpr uint32_t kStageGlobal = 0x80000000u;
 
-// Staged mode (g.stage_blk > 0, the default): every piece is also packed and
-// stored in this workgroup's region of `stage`, in enumeration order, with its
-// place in the workgroup's histogram (hash slot | rank among the slot's pieces
-// << 16); k_gather moves it into its tile's bin after k_plan, so the beams are
-// enumerated once per call instead of twice (k_beam_prep, then k_scatter).
-// Emission index: one LDS bump per wave per emitting step.
+__device__ inline PackedPiece no_stage_piece() {
+  PackedPiece q;
+  q.x = 0u; q.y = 0u; q.z = 0u; q.w = 1u;
+  return q;
+}
+
+// Staged mode (kStaged, the default): every piece is also packed and stored
+// in this workgroup's region of `stage`, in enumeration order, with its
+// workgroup histogram slot (or kStageGlobal | tile); k_gather moves it into
+// its tile's bin after k_plan, so the beams are enumerated once per call
+// instead of twice (k_beam_prep, then k_scatter).  A piece's place inside
+// its bin is arbitrary (counts are integers: order-free), so k_gather ranks
+// the pieces of a slot itself.  Emission index: one LDS bump per wave per
+// emitting step, issued before the histogram's so the two latencies overlap.
+template <bool kStaged>
 __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const double* __restrict__ pose4,
                                                    const float* __restrict__ ranges,
                                                    const double* __restrict__ trig,
@@ -171,12 +180,10 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
   __shared__ int32_t hkey[kHash];
   __shared__ int32_t hcnt[kHash];
   __shared__ int32_t s_nh, s_np;
-  const int tid = threadIdx.x, lane = lane_id();
+  const int tid = threadIdx.x;
   for (int e = tid; e < kHash; e += 256) { hkey[e] = -1; hcnt[e] = 0; }
   if (tid == 0) { s_nh = 0; s_np = 0; }
   __syncthreads();
-  const bool staged = g.stage_blk > 0;
-  const int64_t sbase = (int64_t)blockIdx.x * g.stage_blk;
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + tid;
   if (v < g.nb * g.chunks) {
     const BeamChunk bc = beam_chunk(g, v);
@@ -185,41 +192,35 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
     if (bc.k_lo == 0) beams[bc.b] = bm;
     if ((bm.flags & 1) && bc.k_lo <= bm.n) {
       dm_for_each_piece(bm, g.r, [&](int32_t tile, int32_t k0, int32_t k1) {
-        const LaneRun run = lane_run(tile);
-        if (!staged) {
-          if (run.head) {
-            const int h = hash_insert(hkey, tile);
-            if (h >= 0) {
-              atomicAdd(&hcnt[h], run.len);
-            } else {
-              const int32_t old = atomicAdd(&tile_count[tile], run.len);
-              first_touch(g, tile, old, act_raw, ish, cnt);
-            }
-          }
-          return;
+        int32_t e0 = 0;
+        unsigned long long act = 0ull;
+        int lead = 0;
+        if (kStaged) {  // this wave's emitting lanes take consecutive staging entries
+          act = __ballot(1);
+          lead = __ffsll(act) - 1;
+          if (lane_id() == lead) e0 = atomicAdd(&s_np, __popcll(act));
         }
+        const LaneRun run = lane_run(tile);
         uint32_t sr = 0u;
         if (run.head) {
           const int h = hash_insert(hkey, tile);
           if (h >= 0) {
-            sr = (uint32_t)h | ((uint32_t)atomicAdd(&hcnt[h], run.len) << 16);
+            atomicAdd(&hcnt[h], run.len);
+            sr = (uint32_t)h;
           } else {
             const int32_t old = atomicAdd(&tile_count[tile], run.len);
             first_touch(g, tile, old, act_raw, ish, cnt);
             sr = kStageGlobal | (uint32_t)tile;
           }
         }
-        sr = __shfl(sr, run.head_lane);
-        if (!(sr & kStageGlobal)) sr += (uint32_t)run.rank << 16;  // the slot's rank (< 2^15: <= 512 pieces)
-        // this wave's emitting lanes take consecutive staging entries
-        const unsigned long long act = __ballot(1);
-        const int lead = __ffsll(act) - 1;
-        int32_t e0 = 0;
-        if (lane == lead) e0 = atomicAdd(&s_np, __popcll(act));
-        const int64_t e = (int64_t)__shfl(e0, lead) + __popcll(act & ((1ull << lane) - 1ull));
-        if (e < g.stage_blk) {
-          stage[sbase + e] = make_piece(g, bm, tile, k0, k1);
-          stage_sr[sbase + e] = sr;
+        if (kStaged) {
+          sr = __shfl(sr, run.head_lane);
+          const int64_t e = (int64_t)__shfl(e0, lead) + __popcll(act & ((1ull << lane_id()) - 1ull));
+          if (e < g.stage_blk) {
+            const int64_t at = (int64_t)blockIdx.x * g.stage_blk + e;
+            stage[at] = make_piece(g, bm, tile, k0, k1);
+            stage_sr[at] = sr;
+          }
         }
       }, bc.k_lo, bc.k_hi);
     }
@@ -239,7 +240,7 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
   __syncthreads();
   if (tid == 0) {
     blk_n[blockIdx.x] = s_nh;
-    if (staged) {
+    if (kStaged) {
       blk_np[blockIdx.x] = s_np;
       if ((int64_t)s_np > g.stage_blk) atomicOr(&cnt[CNT_IOVERFLOW], 2ull);  // cannot happen (grow_integrate's bound)
     }
@@ -401,9 +402,10 @@ __device__ inline void put_piece(const Geom& g, PackedPiece* pieces, int64_t idx
 
 // Staged pieces -> per-tile bins (replaces k_scatter's second enumeration):
 // one workgroup per k_beam_prep workgroup; one cursor bump per histogram
-// entry reserves the workgroup's range of each tile's bin (hbase, by hash
-// slot), then every staged piece goes to hbase[slot] + its rank.  Pieces of a
-// tile that found no LDS slot bump the tile's cursor one by one (rare: the
+// entry reserves the workgroup's range of each tile's bin (hcur, by hash
+// slot), then every staged piece takes the next place of its slot's range
+// (an LDS cursor: the order inside a bin is free).  Pieces of a tile that
+// found no LDS slot bump the tile's global cursor one by one (rare: the
 // table holds 1024 tiles per 256 beams).  The first round's loads go out
 // before the cursor bumps.
 __global__ __launch_bounds__(256) void k_gather(Geom g, int32_t* tile_cur, const int2* __restrict__ blk_hist,
@@ -412,17 +414,21 @@ __global__ __launch_bounds__(256) void k_gather(Geom g, int32_t* tile_cur, const
                                                 const PackedPiece* __restrict__ stage,
                                                 const uint32_t* __restrict__ stage_sr,
                                                 PackedPiece* __restrict__ pieces, unsigned long long* cnt) {
-  __shared__ int32_t hbase[kHash];
+  __shared__ int32_t hcur[kHash];
   const int tid = threadIdx.x;
   const int32_t nh = blk_n[blockIdx.x];
   const int32_t np = (int32_t)min((int64_t)blk_np[blockIdx.x], g.stage_blk);
   const int64_t sbase = (int64_t)blockIdx.x * g.stage_blk;
-  PackedPiece pc = tid < np ? stage[sbase + tid] : PackedPiece{0u, 0u, 0u, 1u};
-  uint32_t sr = tid < np ? stage_sr[sbase + tid] : 0u;
+  PackedPiece pc = no_stage_piece();
+  uint32_t sr = 0u;
+  if (tid < np) {
+    pc = stage[sbase + tid];
+    sr = stage_sr[sbase + tid];
+  }
   const int2* my_hist = blk_hist + (int64_t)blockIdx.x * kHash;
   for (int e = tid; e < nh; e += 256) {
     const int2 te = my_hist[e];
-    hbase[te.y >> 16] = atomicAdd(&tile_cur[te.x], te.y & 0xFFFF);
+    hcur[te.y >> 16] = atomicAdd(&tile_cur[te.x], te.y & 0xFFFF);
   }
   __syncthreads();
   for (int32_t e = tid; e < np; e += 256) {
@@ -431,7 +437,7 @@ __global__ __launch_bounds__(256) void k_gather(Geom g, int32_t* tile_cur, const
       sr = stage_sr[sbase + e];
     }
     const int64_t dst = (sr & kStageGlobal) ? (int64_t)atomicAdd(&tile_cur[sr & ~kStageGlobal], 1)
-                                            : (int64_t)hbase[sr & 0xFFFFu] + (int64_t)(sr >> 16);
+                                            : (int64_t)atomicAdd(&hcur[sr], 1);
     if (dst >= 0 && dst < g.seg_cap) pieces[dst] = pc;
     else atomicOr(&cnt[CNT_IOVERFLOW], 2ull);
   }
@@ -1464,9 +1470,14 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   KernelTimer t;
   dm_timer_begin(g, "beam_prep", &t, fs);
   ge.stage_blk = g->fe_staged ? g->stage_blk : 0;
-  DM_LAUNCH(k_beam_prep, dim3(nblk), dim3(256), 0, fs, a, ge, d_pose4, d_ranges,
-                     d_trig, g->beams, w.tile_count, g->act_raw, w.sh, g->blk_hist, g->blk_n, g->stage,
-                     g->stage_sr, g->blk_np, w.cnt);
+  if (ge.stage_blk > 0)
+    DM_LAUNCH(k_beam_prep<true>, dim3(nblk), dim3(256), 0, fs, a, ge, d_pose4, d_ranges,
+              d_trig, g->beams, w.tile_count, g->act_raw, w.sh, g->blk_hist, g->blk_n, g->stage,
+              g->stage_sr, g->blk_np, w.cnt);
+  else
+    DM_LAUNCH(k_beam_prep<false>, dim3(nblk), dim3(256), 0, fs, a, ge, d_pose4, d_ranges,
+              d_trig, g->beams, w.tile_count, g->act_raw, w.sh, g->blk_hist, g->blk_n, g->stage,
+              g->stage_sr, g->blk_np, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "plan", &t, fs);

@@ -219,7 +219,7 @@ struct dm_grid {
   int64_t blk_cap = 0;            // workgroups blk_hist / blk_n hold
   int2* blk_hist = nullptr;       // [beam blocks][1024] k_beam_prep's (tile, pieces | hash slot << 16) histogram
   int32_t* blk_n = nullptr;       // [beam blocks] its entries
-  // Staged front-end (default; DM_FE_STAGED=0: k_scatter's second
+  // Staged front-end (opt-in, DM_FE_STAGED=1; default: k_scatter's second
   // enumeration instead): k_beam_prep stores every piece it enumerates,
   // packed, in its workgroup's region of `stage` with its place in the
   // workgroup's tile histogram (stage_sr: hash slot | rank << 16, or bit 31 |
@@ -227,7 +227,7 @@ struct dm_grid {
   // the tile bins once k_plan has placed the bins.  Shared by the workspace
   // sets: k_gather of a call runs before the next call's k_beam_prep (both
   // on the front-end stream).
-  bool fe_staged = true;
+  bool fe_staged = false;
   PackedPiece* stage = nullptr;   // [beam blocks][stage_blk]
   uint32_t* stage_sr = nullptr;   // [beam blocks][stage_blk]
   int32_t* blk_np = nullptr;      // [beam blocks] pieces staged
@@ -362,6 +362,12 @@ struct dm_grid {
   int32_t* bs_idx2 = nullptr;
   int32_t* bs_hist = nullptr;     // [2^rx_bits][ceil(bs_cap / kRxItems)] digit x block counts -> offsets
   int64_t bs_cap = 0;
+  // row-bucket sort (k_rs_*, the default large-K sort; DM_LARGE_SORT=radix:
+  // the LSD radix k_rx_*): per-row counters (zero between sorts) and offsets
+  int32_t* rs_cnt = nullptr;      // [rs_rows]
+  int32_t* rs_off = nullptr;      // [rs_rows + 1]
+  int64_t rs_rows = 0;
+  bool row_sort = true;
   int64_t sort_hint = 0, msort_hint = 0;  // clusters of the last band / merge readback
   int64_t ftile_hint = 0;                 // listed tiles of the last collected frontier pass
   int64_t runs_hint = 0, ftf_hint = 0;    // its runs and tiles with frontier cells

@@ -1,10 +1,11 @@
 """GPU: the cluster sort at every cluster count.
 
-The frontier pipeline orders its cluster records by label with one of two
-device sorts (csrc/dm_frontier.hip): the O(K^2) rank sort, or the LSD radix
-sort (k_rx_init / k_rx_hist / k_rx_scan / k_rx_scatter / k_rx_emit) once the
-last collected pass of the handle had more than kBucketSortMin (4096)
-clusters.
+The frontier pipeline orders its cluster records by label with one of three
+device sorts (csrc/dm_frontier.hip): the O(K^2) rank sort, or, once the last
+collected pass of the handle had more than sort_min (4096) clusters, the
+row-bucket sort (k_rs_count / k_rs_scan / k_rs_place / k_rs_rank, the
+default) or the LSD radix sort (k_rx_*, DM_LARGE_SORT=radix).  Every large-K
+test runs with both.
 Either must give the oracle's list bit for bit whatever the count of the pass
 it actually sorts, including a small pass sorted by the bucket path after a
 large one, the pipelined begin/end passes and the cross-band merge.
@@ -32,11 +33,16 @@ def _oracle_clusters(oracle_lib, p, st):
     return om.frontiers()
 
 
+LARGE_SORTS = ["row", "radix"]
+
+
 # K: 26k (> kBucketSortMin, < the rank sort's 65536 cap), 105k (> both)
+@pytest.mark.parametrize("large_sort", LARGE_SORTS)
 @pytest.mark.parametrize("R,W,seed", [(512, 512, 1), (1024, 1024, 2)])
-def test_bucket_sort_band(oracle_lib, R, W, seed):
+def test_bucket_sort_band(oracle_lib, monkeypatch, R, W, seed, large_sort):
     import dm
 
+    monkeypatch.setenv("DM_LARGE_SORT", large_sort)
     big = sparse_state(seed, R, W)
     small = cases.blob_state(seed, R, W, n_blobs=40)      # a few dozen clusters
     mid = cases.random_state(seed + 7, R, W)              # a few thousand
@@ -62,9 +68,11 @@ def test_bucket_sort_band(oracle_lib, R, W, seed):
             np.testing.assert_array_equal(fr.clusters, exp_big[2])
 
 
-def test_bucket_sort_min_size_filter(oracle_lib):
+@pytest.mark.parametrize("large_sort", LARGE_SORTS)
+def test_bucket_sort_min_size_filter(oracle_lib, monkeypatch, large_sort):
     import dm
 
+    monkeypatch.setenv("DM_LARGE_SORT", large_sort)
     st = cases.random_state(5, 768, 640, p_free=0.45, p_occ=0.05)
     p = cases.make_params(640, 768, min_frontier_size=3)
     exp = _oracle_clusters(oracle_lib, p, st)
@@ -75,14 +83,16 @@ def test_bucket_sort_min_size_filter(oracle_lib):
         assert_frontiers_equal(m.frontiers(want_mask=True, want_labels=True), *exp)
 
 
+@pytest.mark.parametrize("large_sort", LARGE_SORTS)
 @pytest.mark.parametrize("P", [2, 4])
-def test_bucket_sort_merge(oracle_lib, P):
+def test_bucket_sort_merge(oracle_lib, monkeypatch, P, large_sort):
     """Cross-band merge of ~105k clusters: rank sort cap exceeded first (host
     sort), then the bucket sort over global rows."""
     import dm
     import torch
     from dm.sharded import band_params
 
+    monkeypatch.setenv("DM_LARGE_SORT", large_sort)
     R, W = 1024, 1024
     st = sparse_state(2, R, W)
     p = cases.make_params(W, R)
@@ -121,13 +131,16 @@ def test_bucket_sort_merge(oracle_lib, P):
             b.close()
 
 
+@pytest.mark.parametrize("large_sort", LARGE_SORTS)
 @pytest.mark.parametrize("R,W,rows", [(64, 65536, 3), (2048, 16384, 1)])
-def test_radix_sort_clusters_packed_in_few_rows(oracle_lib, R, W, rows):
+def test_radix_sort_clusters_packed_in_few_rows(oracle_lib, monkeypatch, R, W, rows, large_sort):
     """Clusters packed in a few rows (the round-2 bucket sort's worst case:
-    one label bucket holding most records) and a wide label range; the
-    second pass is sorted by the radix path (hint from the first)."""
+    one label bucket holding most records; for the row sort, rows of 8-32 k
+    records: its O(b^2) worst case, slow but exact) and a wide label range;
+    the second pass is sorted by the large-K path (hint from the first)."""
     import dm
 
+    monkeypatch.setenv("DM_LARGE_SORT", large_sort)
     st = np.full((R, W), -1, np.int8)
     for k in range(rows):
         st[R // 2 + 2 * k, ::2] = 0  # isolated free cells: W / 2 clusters per row
