@@ -620,10 +620,24 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     g->own_stream = true;
     e = hipStreamCreateWithPriority(&g->fe_stream, hipStreamNonBlocking, p_fe);
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(front-end)"));
-    e = hipStreamCreateWithPriority(&g->pass_stream, hipStreamNonBlocking, p_pass);
-    if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(pass)"));
-    e = hipStreamCreateWithPriority(&g->big_stream, hipStreamNonBlocking, p_pass);
-    if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(big)"));
+    // DM_PASS_CUS=n (A/B): the frontier labelling streams
+    // (pass, big) confined to CUs [0, n) while the map and front-end streams
+    // keep the whole chip, so a pass's labelling takes at most n CUs from the
+    // next batch's integrate
+    const int pass_cus = getenv("DM_PASS_CUS") ? atoi(getenv("DM_PASS_CUS")) : 0;
+    if (pass_cus > 0 && pass_cus < g->n_cu) {
+      std::vector<uint32_t> pm((size_t)(g->n_cu + 31) / 32, 0u);
+      for (int c = 0; c < pass_cus; ++c) pm[(size_t)c / 32] |= 1u << (c % 32);
+      e = hipExtStreamCreateWithCUMask(&g->pass_stream, (uint32_t)pm.size(), pm.data());
+      if (e != hipSuccess) return fail(dm_hip_check(e, "hipExtStreamCreateWithCUMask(pass)"));
+      e = hipExtStreamCreateWithCUMask(&g->big_stream, (uint32_t)pm.size(), pm.data());
+      if (e != hipSuccess) return fail(dm_hip_check(e, "hipExtStreamCreateWithCUMask(big)"));
+    } else {
+      e = hipStreamCreateWithPriority(&g->pass_stream, hipStreamNonBlocking, p_pass);
+      if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(pass)"));
+      e = hipStreamCreateWithPriority(&g->big_stream, hipStreamNonBlocking, p_pass);
+      if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(big)"));
+    }
   }
   // ev_fe / ev_free only order the two streams on the device: no system-
   // scope fence (no host-visible cache writeback at every step).  The host

@@ -373,21 +373,6 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
     DM_PH(dm_phase_acc_frontier, 6);
     const long long base = sbase;
     const long long sh0 = (long long)(blockIdx.x % kShards) * g.slot_per;
-    for (int r = tid; r < nruns; r += kFT) {
-      if (r_par[r] != r) continue;
-      const int c = root_rank(s_root, s_rootpre, r);
-      if (base + c >= g.slot_per) { atomicOr(&cnt[CNT_OVERFLOW], kOvSlots); continue; }
-      const long long slot = sh0 + base + c;
-      const long long gy = (long long)g.row0 + ty0 + r_y[r];
-      const long long gx = (long long)tx0 + r_s[r];
-      const uint32_t zx = szx[c];
-      const long long sz = zx >> 18;
-      slot_label[slot] = gy * g.W + gx;  // (slot_parent[slot] == slot since k_frontier_prep)
-      const long long sx = sz * tx0 + (zx & 0x3FFFFu);
-      const long long sy = sz * ((long long)g.row0 + ty0) + ssy[c];
-      slot_own[3 * slot + 0] = sz; slot_own[3 * slot + 1] = sx; slot_own[3 * slot + 2] = sy;
-      slot_acc[3 * slot + 0] = sz; slot_acc[3 * slot + 1] = sx; slot_acc[3 * slot + 2] = sy;
-    }
     // ---- 5. unions across the tile's edges -------------------------------------
     // Wave w owns edge w ([0] first row, [1] last row, [2] first col, [3]
     // last col; lane = position along it) and the slot of its lane's cell.
@@ -487,6 +472,24 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
           }
         }
       }
+    }
+    // the slots' labels and sums (read only by k_frontier_resolve, after this
+    // kernel): stored after the hand-off, so the edge wave's vmcnt(0) before
+    // its arrival drains the border stores alone
+    for (int r = tid; r < nruns; r += kFT) {
+      if (r_par[r] != r) continue;
+      const int c = root_rank(s_root, s_rootpre, r);
+      if (base + c >= g.slot_per) { atomicOr(&cnt[CNT_OVERFLOW], kOvSlots); continue; }
+      const long long slot = sh0 + base + c;
+      const long long gy = (long long)g.row0 + ty0 + r_y[r];
+      const long long gx = (long long)tx0 + r_s[r];
+      const uint32_t zx = szx[c];
+      const long long sz = zx >> 18;
+      slot_label[slot] = gy * g.W + gx;  // (slot_parent[slot] == slot since k_frontier_prep)
+      const long long sx = sz * tx0 + (zx & 0x3FFFFu);
+      const long long sy = sz * ((long long)g.row0 + ty0) + ssy[c];
+      slot_own[3 * slot + 0] = sz; slot_own[3 * slot + 1] = sx; slot_own[3 * slot + 2] = sy;
+      slot_acc[3 * slot + 0] = sz; slot_acc[3 * slot + 1] = sx; slot_acc[3 * slot + 2] = sy;
     }
     // band edge rows (cross-band merging) and optional dense outputs
     const bool dense = g.want_mask || g.want_labels;
@@ -924,33 +927,6 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
       const long long v = base + rootpre[root >> 6] + __popcll(rootw[root >> 6] & ((1ull << (root & 63)) - 1ull));
       return v < g.slot_per ? (int32_t)(sh0 + v) : -1;
     };
-    {
-      uint64_t s_ = st;
-      int r = rbase;
-      while (s_) {
-        const int s0 = __ffsll((unsigned long long)s_) - 1;
-        if (par[r] == r) {
-          const int32_t slot = slot_of_run(r);
-          if (slot < 0) {
-            atomicOr(&cnt[CNT_OVERFLOW], kOvSlots);
-          } else {
-            const unsigned long long a = acc[r];
-            const long long sz = (long long)(a >> 40);
-            const long long sx = sz * tx0 + (long long)((a >> 20) & 0xFFFFFull);
-            const long long sy = sz * ((long long)g.row0 + ty0) + (long long)(a & 0xFFFFFull);
-            slot_label[slot] = ((long long)g.row0 + ty0 + lane) * g.W + tx0 + s0;
-            slot_own[3 * (int64_t)slot + 0] = sz;
-            slot_own[3 * (int64_t)slot + 1] = sx;
-            slot_own[3 * (int64_t)slot + 2] = sy;
-            slot_acc[3 * (int64_t)slot + 0] = sz;
-            slot_acc[3 * (int64_t)slot + 1] = sx;
-            slot_acc[3 * (int64_t)slot + 2] = sy;
-          }
-        }
-        ++r;
-        s_ &= s_ - 1;
-      }
-    }
     DM_PH(dm_phase_acc_ftile, 5);
     // ---- 8. edges: publish, arrive, unite -------------------
     // sides [0] first row, [1] last row, [2] first col, [3] last col; lane =
@@ -1018,6 +994,36 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
         if (b >= 0) dm_uf_unite_idx(slot_parent, me, b, uflag, kOvUnionFind);
       }
       DM_PH(dm_phase_acc_ftile, 8);
+    }
+    // the slots' labels and sums (read only by k_frontier_resolve, after this
+    // kernel): stored after the hand-off, so the vmcnt(0) before the arrivals
+    // drains the border stores alone
+    {
+      uint64_t s_ = st;
+      int r = rbase;
+      while (s_) {
+        const int s0 = __ffsll((unsigned long long)s_) - 1;
+        if (par[r] == r) {
+          const int32_t slot = slot_of_run(r);
+          if (slot < 0) {
+            atomicOr(&cnt[CNT_OVERFLOW], kOvSlots);
+          } else {
+            const unsigned long long a = acc[r];
+            const long long sz = (long long)(a >> 40);
+            const long long sx = sz * tx0 + (long long)((a >> 20) & 0xFFFFFull);
+            const long long sy = sz * ((long long)g.row0 + ty0) + (long long)(a & 0xFFFFFull);
+            slot_label[slot] = ((long long)g.row0 + ty0 + lane) * g.W + tx0 + s0;
+            slot_own[3 * (int64_t)slot + 0] = sz;
+            slot_own[3 * (int64_t)slot + 1] = sx;
+            slot_own[3 * (int64_t)slot + 2] = sy;
+            slot_acc[3 * (int64_t)slot + 0] = sz;
+            slot_acc[3 * (int64_t)slot + 1] = sx;
+            slot_acc[3 * (int64_t)slot + 2] = sy;
+          }
+        }
+        ++r;
+        s_ &= s_ - 1;
+      }
     }
     // ---- 9. band edge rows (cross-band merging) and optional dense outputs ---
     const int32_t gy = ty0 + lane;

@@ -849,6 +849,9 @@ __device__ inline void heavy_quarter(const Geom& g, const ApplyArgs& p, int64_t 
 #ifndef DM_ACCUM_OCC
 #define DM_ACCUM_OCC 7
 #endif
+#ifndef DM_EARLY_PIECES
+#define DM_EARLY_PIECES 1
+#endif
 #ifndef DM_TICKET_RELEASE
 #define DM_TICKET_RELEASE 0
 #endif
@@ -859,21 +862,30 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
     const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok,
     const int32_t* __restrict__ heavy_list, int32_t* heavy_done, const unsigned long long* __restrict__ halt) {
-  // a timed-out front-end hand-off (kHaltWord): this call's workspace was
-  // never written, so nothing is applied (the host reports DM_ERR_PIPELINE)
-  if (*halt) return;
   __shared__ uint32_t tl[kTileWords + 64];  // + one spare word per lane (walk_piece_plain)
   __shared__ int32_t s_T, s_free, s_last;
   __shared__ uint32_t s_U;
   const int tid = threadIdx.x, lane = lane_id();
+  // The halt word and the item counts in one round of loads (a workgroup
+  // runs about one item at C3, so its first item's dependent loads -- counts,
+  // descriptor, pieces -- are on every item's path; the halt check used to
+  // be a round of its own in front of them).
+  const unsigned long long hv = *halt;
+  const unsigned long long ca = cnt[cnt_a];
+  const unsigned long long cb = cnt[cnt_b];  // (the one launch passes all three counters)
+  const unsigned long long cc = cnt[cnt_c];
   // (clamped to the list capacities: k_plan flags and drops what does not fit)
-  const int64_t HI = min((int64_t)cnt[cnt_a], g.hitem_cap);
-  const int64_t LI = cnt_b >= 0 ? min((int64_t)cnt[cnt_b], (int64_t)g.act_cap) : 0;
+  const int64_t HI = min((int64_t)ca, g.hitem_cap);
+  const int64_t LI = min((int64_t)cb, (int64_t)g.act_cap);
   const int64_t n_items = HI + LI;
   // sparse items (litems from the top, cnt_c of them): a second loop
-  const int64_t SI = cnt_c >= 0 ? min((int64_t)cnt[cnt_c], (int64_t)g.act_cap) : 0;
+  const int64_t SI = min((int64_t)cc, (int64_t)g.act_cap);
   const int64_t G = gridDim.x;
-  if ((int64_t)blockIdx.x >= n_items && 2 * (int64_t)blockIdx.x >= SI) return;
+  // a timed-out front-end hand-off (kHaltWord): this call's workspace was
+  // never written, so nothing is applied (the host reports DM_ERR_PIPELINE).
+  // One exit test on all four loads, so they go out together.
+  const unsigned long long idle = ((int64_t)blockIdx.x >= n_items && 2 * (int64_t)blockIdx.x >= SI) ? 1ull : 0ull;
+  if ((hv | idle) != 0ull) return;
   auto item_of = [&](int64_t it) {
     int4 d = it < n_items ? (it < HI ? list_a[it] : list_b[it - HI]) : make_int4(0, 0, 0, -1);
     // an item never reads past the piece array (k_plan keeps p0 + c <= seg_cap)
@@ -888,14 +900,20 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
   PackedPiece mine;
   CellRows<4> cells;
   int32_t tfree;
-  auto issue_pieces = [&](const int4& d) {
+  auto load_pieces = [&](const int4& d) -> PackedPiece {
     const int32_t c0 = __builtin_amdgcn_readfirstlane(d.y);
     const int32_t c = __builtin_amdgcn_readfirstlane(d.z);
     // lanes past the item's pieces re-read its last one (past the list's end:
     // piece 0); unconditional, so the loop carries no phi of the old pieces
-    mine = pieces[c0 + min(tid, max(c - 1, 0))];
+    return pieces[c0 + min(tid, max(c - 1, 0))];
   };
-  issue_pieces(info);
+  mine = load_pieces(info);
+  // DM_EARLY_PIECES: the next item's pieces are issued right after this
+  // item's walk, BEFORE its apply stores.  Loads and stores share the wave's
+  // in-order vmcnt counter, so pieces issued after the stores (the other
+  // form) make the next walk's wait for them also a wait for the previous
+  // item's stores to drain.
+  PackedPiece mine_n = mine;
   for (int e = tid; e < kTileWords; e += kQuarter) tl[e] = 0u;
   if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; s_accT = 0ull; s_accU = 0ull; }
   __syncthreads();
@@ -912,6 +930,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
       // heavy (a sensor's tile): the pieces all start at the sensor's cell;
       // walk_piece's staggered start keeps a wave's lanes on different cells
       walk_piece(tl, mine, tid < c, lane);
+      if (DM_EARLY_PIECES) mine_n = load_pieces(next);
       __syncthreads();
       DM_PH(dm_phase_acc_integrate, 1);
       DM_PH_COUNT(dm_phase_acc_integrate, 17, 1);
@@ -999,6 +1018,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
         for (int o = 32; o > 0; o >>= 1) u += __shfl_xor(u, o);
         if (lane == 0) atomicAdd(&s_U, (uint32_t)u);
       }
+      if (DM_EARLY_PIECES) mine_n = load_pieces(next);
       __syncthreads();
       DM_PH(dm_phase_acc_integrate, 3);
       DM_PH_COUNT(dm_phase_acc_integrate, 16, 1);
@@ -1021,10 +1041,11 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
       if (s_free) tile_free[tile] = tfree + s_free;
       tile_count[tile] = 0;  // ready for the next call
     }
-    // the next item: its pieces go out now, ahead of its walk
+    // the next item: its pieces go out now (or went out after the walk),
+    // ahead of its walk
     info = next;
     next = item_of(it + 2 * G);
-    issue_pieces(info);
+    mine = DM_EARLY_PIECES ? mine_n : load_pieces(info);
     for (int e = tid; e < kTileWords; e += kQuarter) tl[e] = 0u;
     if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; }
     __syncthreads();
