@@ -152,12 +152,22 @@ def _exchange_like_sharded_mapper(handles, rec_cap):
     frontiers() (which grows its slots and sets its sort hint) and the
     capacity grows; the next device exchange must then succeed."""
     got, got_last, max_k = _device_exchange(handles, rec_cap)
-    if got is None:
+    reasons = []
+    # dm/sharded.py falls back (host merge, capacities grown) on every
+    # incomplete pass, so more than one fallback is allowed here too: a slot
+    # shard region can overflow again on the next pass (which tiles share a
+    # region depends on the order the tile kernels take them)
+    for _ in range(3):
+        if got is not None:
+            break
+        reasons.append(getattr(handles[0], "last_incomplete", None))
         for h in handles:
             h.frontiers()
         while rec_cap < max_k:
             rec_cap *= 2
         got, got_last, max_k = _device_exchange(handles, rec_cap)
+    if reasons:
+        print("device exchange fallbacks:", reasons)
     return got, got_last, max_k
 
 
