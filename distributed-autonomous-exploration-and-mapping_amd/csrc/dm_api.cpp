@@ -224,6 +224,7 @@ int dm_grow_bucket_sort(dm_grid* g, int64_t n) {
   if (!rc && g->rs_rows < g->H) {  // row-bucket sort: rows of the whole map (merges sort over H rows)
     rc = dev_alloc(&g->rs_cnt, g->H, "row-sort counters");
     if (!rc) rc = dev_alloc(&g->rs_off, g->H + 1, "row-sort offsets");
+    if (!rc) rc = dev_alloc(&g->rs_status, g->H / 8192 + 2, "row-sort workgroup totals");
     if (!rc) {
       DM_HIP(hipMemset(g->rs_cnt, 0, sizeof(int32_t) * (size_t)g->H));
       g->rs_rows = g->H;
@@ -697,7 +698,7 @@ int dm_destroy(dm_grid* g) {
   dev_free(g->trig);
   dev_free(g->pose4); dev_free(g->ranges); 
   dev_free(g->bs_key); dev_free(g->bs_key2); dev_free(g->bs_idx); dev_free(g->bs_idx2); dev_free(g->bs_hist);
-  dev_free(g->rs_cnt); dev_free(g->rs_off);
+  dev_free(g->rs_cnt); dev_free(g->rs_off); dev_free(g->rs_status);
   dev_free(g->border); dev_free(g->rel); dev_free(g->slot_label); dev_free(g->slot_root);
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
   dev_free(g->edge_label); dev_free(g->mask); dev_free(g->labels);

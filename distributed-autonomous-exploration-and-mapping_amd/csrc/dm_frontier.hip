@@ -373,6 +373,21 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
     DM_PH(dm_phase_acc_frontier, 6);
     const long long base = sbase;
     const long long sh0 = (long long)(blockIdx.x % kShards) * g.slot_per;
+    for (int r = tid; r < nruns; r += kFT) {
+      if (r_par[r] != r) continue;
+      const int c = root_rank(s_root, s_rootpre, r);
+      if (base + c >= g.slot_per) { atomicOr(&cnt[CNT_OVERFLOW], kOvSlots); continue; }
+      const long long slot = sh0 + base + c;
+      const long long gy = (long long)g.row0 + ty0 + r_y[r];
+      const long long gx = (long long)tx0 + r_s[r];
+      const uint32_t zx = szx[c];
+      const long long sz = zx >> 18;
+      slot_label[slot] = gy * g.W + gx;  // (slot_parent[slot] == slot since k_frontier_prep)
+      const long long sx = sz * tx0 + (zx & 0x3FFFFu);
+      const long long sy = sz * ((long long)g.row0 + ty0) + ssy[c];
+      slot_own[3 * slot + 0] = sz; slot_own[3 * slot + 1] = sx; slot_own[3 * slot + 2] = sy;
+      slot_acc[3 * slot + 0] = sz; slot_acc[3 * slot + 1] = sx; slot_acc[3 * slot + 2] = sy;
+    }
     // ---- 5. unions across the tile's edges -------------------------------------
     // Wave w owns edge w ([0] first row, [1] last row, [2] first col, [3]
     // last col; lane = position along it) and the slot of its lane's cell.
@@ -472,24 +487,6 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
           }
         }
       }
-    }
-    // the slots' labels and sums (read only by k_frontier_resolve, after this
-    // kernel): stored after the hand-off, so the edge wave's vmcnt(0) before
-    // its arrival drains the border stores alone
-    for (int r = tid; r < nruns; r += kFT) {
-      if (r_par[r] != r) continue;
-      const int c = root_rank(s_root, s_rootpre, r);
-      if (base + c >= g.slot_per) { atomicOr(&cnt[CNT_OVERFLOW], kOvSlots); continue; }
-      const long long slot = sh0 + base + c;
-      const long long gy = (long long)g.row0 + ty0 + r_y[r];
-      const long long gx = (long long)tx0 + r_s[r];
-      const uint32_t zx = szx[c];
-      const long long sz = zx >> 18;
-      slot_label[slot] = gy * g.W + gx;  // (slot_parent[slot] == slot since k_frontier_prep)
-      const long long sx = sz * tx0 + (zx & 0x3FFFFu);
-      const long long sy = sz * ((long long)g.row0 + ty0) + ssy[c];
-      slot_own[3 * slot + 0] = sz; slot_own[3 * slot + 1] = sx; slot_own[3 * slot + 2] = sy;
-      slot_acc[3 * slot + 0] = sz; slot_acc[3 * slot + 1] = sx; slot_acc[3 * slot + 2] = sy;
     }
     // band edge rows (cross-band merging) and optional dense outputs
     const bool dense = g.want_mask || g.want_labels;
@@ -927,6 +924,33 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
       const long long v = base + rootpre[root >> 6] + __popcll(rootw[root >> 6] & ((1ull << (root & 63)) - 1ull));
       return v < g.slot_per ? (int32_t)(sh0 + v) : -1;
     };
+    {
+      uint64_t s_ = st;
+      int r = rbase;
+      while (s_) {
+        const int s0 = __ffsll((unsigned long long)s_) - 1;
+        if (par[r] == r) {
+          const int32_t slot = slot_of_run(r);
+          if (slot < 0) {
+            atomicOr(&cnt[CNT_OVERFLOW], kOvSlots);
+          } else {
+            const unsigned long long a = acc[r];
+            const long long sz = (long long)(a >> 40);
+            const long long sx = sz * tx0 + (long long)((a >> 20) & 0xFFFFFull);
+            const long long sy = sz * ((long long)g.row0 + ty0) + (long long)(a & 0xFFFFFull);
+            slot_label[slot] = ((long long)g.row0 + ty0 + lane) * g.W + tx0 + s0;
+            slot_own[3 * (int64_t)slot + 0] = sz;
+            slot_own[3 * (int64_t)slot + 1] = sx;
+            slot_own[3 * (int64_t)slot + 2] = sy;
+            slot_acc[3 * (int64_t)slot + 0] = sz;
+            slot_acc[3 * (int64_t)slot + 1] = sx;
+            slot_acc[3 * (int64_t)slot + 2] = sy;
+          }
+        }
+        ++r;
+        s_ &= s_ - 1;
+      }
+    }
     DM_PH(dm_phase_acc_ftile, 5);
     // ---- 8. edges: publish, arrive, unite -------------------
     // sides [0] first row, [1] last row, [2] first col, [3] last col; lane =
@@ -994,36 +1018,6 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
         if (b >= 0) dm_uf_unite_idx(slot_parent, me, b, uflag, kOvUnionFind);
       }
       DM_PH(dm_phase_acc_ftile, 8);
-    }
-    // the slots' labels and sums (read only by k_frontier_resolve, after this
-    // kernel): stored after the hand-off, so the vmcnt(0) before the arrivals
-    // drains the border stores alone
-    {
-      uint64_t s_ = st;
-      int r = rbase;
-      while (s_) {
-        const int s0 = __ffsll((unsigned long long)s_) - 1;
-        if (par[r] == r) {
-          const int32_t slot = slot_of_run(r);
-          if (slot < 0) {
-            atomicOr(&cnt[CNT_OVERFLOW], kOvSlots);
-          } else {
-            const unsigned long long a = acc[r];
-            const long long sz = (long long)(a >> 40);
-            const long long sx = sz * tx0 + (long long)((a >> 20) & 0xFFFFFull);
-            const long long sy = sz * ((long long)g.row0 + ty0) + (long long)(a & 0xFFFFFull);
-            slot_label[slot] = ((long long)g.row0 + ty0 + lane) * g.W + tx0 + s0;
-            slot_own[3 * (int64_t)slot + 0] = sz;
-            slot_own[3 * (int64_t)slot + 1] = sx;
-            slot_own[3 * (int64_t)slot + 2] = sy;
-            slot_acc[3 * (int64_t)slot + 0] = sz;
-            slot_acc[3 * (int64_t)slot + 1] = sx;
-            slot_acc[3 * (int64_t)slot + 2] = sy;
-          }
-        }
-        ++r;
-        s_ &= s_ - 1;
-      }
     }
     // ---- 9. band edge rows (cross-band merging) and optional dense outputs ---
     const int32_t gy = ty0 + lane;
@@ -1286,18 +1280,27 @@ __device__ inline void put_sorted(double ox, double oy, double res, const long l
 // Cluster list sorted by label, with centroids (SPEC a10).  Labels are
 // unique (one per component), so a record's position is the number of
 // records with a smaller label.  One workgroup per 64 records (lane = record),
-// its 16 waves split the keys: the labels are staged through LDS in
-// 4096-key chunks (every thread's loads in flight at once) and each wave
-// counts over its sixteenth of the chunk with wave-uniform LDS broadcasts;
-// the 16 partial counts are summed in LDS.  O(K^2) compares spread over
+// its waves split the keys: the labels are staged through LDS in chunks
+// (every thread's loads in flight at once) and each wave counts over its
+// share of the chunk with wave-uniform LDS broadcasts; the waves' partial
+// counts are summed in LDS.  O(K^2) compares spread over
 // ceil(K/64) workgroups: no serial single-workgroup network, a few
 // microseconds at C3's ~1.6k clusters.  Records become dm_cluster with
 // cx_m = ox + ((double)sum_x / (double)size + 0.5) * res (IEEE division in
 // double on host and device).  rank_of (may be NULL) receives each input
 // record's sorted position.  More than kRankSortCap records: *sorted = 0
 // and the host sorts the raw records.
-constexpr int kSortChunk = 4096;
-constexpr int kSortThreads = 1024;
+// 256 threads (round 3; 1024 before): a workgroup that needs 16 wave slots
+// and 36 KiB of LDS on one CU waits for a CU to drain while the next batch's
+// k_tile_accum fills the chip beside the pass (DM_SORT_THREADS / _CHUNK: A/B)
+#ifndef DM_SORT_THREADS
+#define DM_SORT_THREADS 256
+#endif
+#ifndef DM_SORT_CHUNK
+#define DM_SORT_CHUNK 2048
+#endif
+constexpr int kSortChunk = DM_SORT_CHUNK;
+constexpr int kSortThreads = DM_SORT_THREADS;
 constexpr int kSortWaves = kSortThreads / 64;
 constexpr int64_t kRankSortCap = 1 << 16;
 
@@ -1386,11 +1389,85 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
 // record) took 0.31 ms at C5's 219k clusters: robots cluster their
 // frontiers in a few buckets.  Every kernel reads the device-side count;
 // K > cap leaves the result unsorted (flag 0), as the rank sort does.
+// Exclusive scan of n int32 counts by ONE 1024-thread workgroup, in
+// registers: each round a thread takes 32 consecutive counts (eight 16-byte
+// loads), sums them, and the workgroup scans the 1024 sums with wave scans and
+// a 16-entry LDS table; rounds carry.  (The earlier form staged 32768 counts
+// in 128 KiB of LDS: such a workgroup waits for a CU with its LDS free, which
+// on a busy chip -- the next batch's kernels beside the pass -- took 95-250 us
+// for C5's 65536 rows.)  in == out is allowed; zero_in also zeroes the input.
+constexpr int kScanThreads = 1024;
+constexpr int kScanPer = 32;
+__device__ inline void block_exclusive_scan(int32_t* in, int32_t* out, int64_t n, bool zero_in,
+                                            int32_t* total_out) {
+  __shared__ int32_t wsum[kScanThreads / 64];
+  const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+  int32_t carry = 0;
+  for (int64_t c0 = 0; c0 < n; c0 += (int64_t)kScanThreads * kScanPer) {
+    const int64_t b = c0 + (int64_t)tid * kScanPer;
+    int32_t v[kScanPer];
+    if (b + kScanPer <= n) {
+#pragma unroll
+      for (int q = 0; q < kScanPer / 4; ++q) {
+        const int4 t = reinterpret_cast<const int4*>(in + b)[q];
+        v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+      }
+      if (zero_in) {
+#pragma unroll
+        for (int q = 0; q < kScanPer / 4; ++q) reinterpret_cast<int4*>(in + b)[q] = make_int4(0, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kScanPer; ++i) {
+        v[i] = b + i < n ? in[b + i] : 0;
+        if (zero_in && b + i < n) in[b + i] = 0;
+      }
+    }
+    int32_t seg = 0;
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) seg += v[i];
+    int32_t incl = seg;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t t = __shfl_up(incl, d);
+      if (lane >= d) incl += t;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int32_t run = carry + incl - seg, total = 0;
+#pragma unroll
+    for (int q = 0; q < kScanThreads / 64; ++q) {
+      const int32_t ws = wsum[q];
+      run += q < w ? ws : 0;
+      total += ws;
+    }
+    if (b + kScanPer <= n) {
+#pragma unroll
+      for (int q = 0; q < kScanPer / 4; ++q) {
+        int4 t;
+        t.x = run; run += v[4 * q];
+        t.y = run; run += v[4 * q + 1];
+        t.z = run; run += v[4 * q + 2];
+        t.w = run; run += v[4 * q + 3];
+        reinterpret_cast<int4*>(out + b)[q] = t;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kScanPer; ++i) {
+        if (b + i < n) out[b + i] = run;
+        run += v[i];
+      }
+    }
+    carry += total;
+    __syncthreads();  // wsum is rewritten next round
+  }
+  if (total_out && tid == 0) *total_out = carry;
+}
+
 constexpr int kRxThreads = 256;
 constexpr int kRxRounds = 8;                      // keys per thread, all loaded up front
 constexpr int kRxItems = kRxThreads * kRxRounds;  // keys per block
 constexpr int kRxMaxRadix = 2048;  // digits of up to 11 bits (DM_RX_BITS)
-constexpr int kRxScanThreads = 1024;
 
 __global__ __launch_bounds__(kRxThreads) void k_rx_init(const long long* __restrict__ clusters,
                                                         const long long* __restrict__ labels,
@@ -1431,57 +1508,14 @@ __global__ __launch_bounds__(kRxThreads) void k_rx_hist(const unsigned long long
   }
 }
 
-// Exclusive scan of hist[0, R * nblk) in place, one workgroup: the entries
-// are staged in LDS with coalesced loads (up to kRxScanLds of them: 128 KiB,
-// a single workgroup may declare 160 KiB on gfx950), each thread scans a
-// contiguous segment there, the segment sums are scanned across the
-// workgroup, and the result goes back with coalesced stores.  More entries
-// (more than 2^18 keys at 8-bit digits) take the same steps in chunks of
-// kRxScanLds with a carry.
-constexpr int kRxScanLds = 32768;
-__global__ __launch_bounds__(kRxScanThreads) void k_rx_scan(const unsigned long long* __restrict__ count,
-                                                            int64_t cap, int db, int32_t* __restrict__ hist) {
-  __shared__ int32_t sv[kRxScanLds];
-  __shared__ int32_t wsum[kRxScanThreads / 64];
+// Exclusive scan of hist[0, R * nblk) in place, one workgroup
+// (block_exclusive_scan: registers, no large LDS footprint).
+__global__ __launch_bounds__(kScanThreads) void k_rx_scan(const unsigned long long* __restrict__ count,
+                                                         int64_t cap, int db, int32_t* __restrict__ hist) {
   const int64_t K = (int64_t)*count;
   if (K > cap) return;
   const int64_t nblk = (K + kRxItems - 1) / kRxItems;
-  const int64_t n = ((int64_t)1 << db) * nblk;
-  const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
-  int32_t carry = 0;
-  for (int64_t c0 = 0; c0 < n; c0 += kRxScanLds) {
-    const int m = (int)min<int64_t>(kRxScanLds, n - c0);
-    for (int j = tid; j < m; j += kRxScanThreads) sv[j] = hist[c0 + j];
-    __syncthreads();
-    const int per = (m + kRxScanThreads - 1) / kRxScanThreads;
-    const int lo = min(m, tid * per), hi = min(m, lo + per);
-    int32_t seg = 0;
-    for (int j = lo; j < hi; ++j) seg += sv[j];
-    int32_t incl = seg;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int32_t t = __shfl_up(incl, d);
-      if (lane >= d) incl += t;
-    }
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    int32_t run = carry + incl - seg, total = 0;
-#pragma unroll
-    for (int q = 0; q < kRxScanThreads / 64; ++q) {
-      const int32_t ws = wsum[q];
-      run += q < w ? ws : 0;
-      total += ws;
-    }
-    for (int j = lo; j < hi; ++j) {
-      const int32_t x = sv[j];
-      sv[j] = run;
-      run += x;
-    }
-    carry += total;
-    __syncthreads();
-    for (int j = tid; j < m; j += kRxScanThreads) hist[c0 + j] = sv[j];
-    __syncthreads();
-  }
+  block_exclusive_scan(hist, hist, ((int64_t)1 << db) * nblk, false, nullptr);
 }
 
 __global__ __launch_bounds__(kRxThreads) void k_rx_scatter(const unsigned long long* __restrict__ count, int64_t cap,
@@ -1576,9 +1610,10 @@ __global__ __launch_bounds__(kRxThreads) void k_rx_emit(double ox, double oy, do
 // whatever the key width (the radix sort above needs 1 + 3 * passes + 1):
 //   k_rs_count  per record: key = label - base, row = key / W, slot = its
 //               arrival in the row (atomic on the row's counter)
-//   k_rs_scan   one workgroup: exclusive scan of the row counts -> row
-//               offsets (rows + 1 of them), and the counters back to zero
-//               for the next sort (they are zero when allocated)
+//   k_rs_scan   exclusive scan of the row counts -> row offsets (rows + 1
+//               of them) by 8192-row workgroups that publish their totals,
+//               and the counters back to zero for the next sort (they are
+//               zero when allocated)
 //   k_rs_place  record -> offset[row] + slot (unordered inside the row)
 //   k_rs_rank   position p: rank among its row's keys (a scan of the row's
 //               range, O(b) for a row of b records), then the same record
@@ -1590,9 +1625,12 @@ __global__ __launch_bounds__(256) void k_rs_count(const long long* __restrict__ 
                                                   const long long* __restrict__ labels,
                                                   const unsigned long long* __restrict__ count, int64_t cap,
                                                   long long base, int64_t W, int32_t* __restrict__ row_cnt,
-                                                  unsigned long long* __restrict__ keys, int32_t* __restrict__ slot) {
+                                                  unsigned long long* __restrict__ keys, int32_t* __restrict__ slot,
+                                                  unsigned long long* status, int n_status) {
   const int64_t K = (int64_t)*count;
   if (K > cap) return;
+  if (blockIdx.x == 0)  // k_rs_scan's published-total words, for this sort
+    for (int e = threadIdx.x; e < n_status; e += blockDim.x) status[e] = 0ull;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < K; i += (int64_t)gridDim.x * blockDim.x) {
     const unsigned long long key = (unsigned long long)(record_key(clusters, labels, i) - base);
     const int64_t row = (int64_t)(key / (unsigned long long)W);
@@ -1601,53 +1639,95 @@ __global__ __launch_bounds__(256) void k_rs_count(const long long* __restrict__ 
   }
 }
 
-constexpr int kRsScanThreads = 1024;
-__global__ __launch_bounds__(kRsScanThreads) void k_rs_scan(const unsigned long long* __restrict__ count,
-                                                            int64_t cap, int64_t rows, int32_t* __restrict__ row_cnt,
-                                                            int32_t* __restrict__ row_off) {
-  __shared__ int32_t sv[kRxScanLds];
-  __shared__ int32_t wsum[kRsScanThreads / 64];
+// Row offsets by many small workgroups (a 1024-thread workgroup waits for a
+// whole CU to drain while the next batch's k_tile_accum fills the chip: the
+// single-workgroup scan measured 27-250 us at C5): workgroup b scans rows
+// [b * kRsChunk, +kRsChunk) in registers (256 threads x 32 rows), publishes
+// its total in status[b] (bit 63 = published; k_rs_count zeroed the words),
+// then adds the totals of ALL earlier workgroups (each published right after
+// its own reduce, so no serial chain: a workgroup only waits for earlier
+// ones, which were dispatched first).
+constexpr int kRsPer = 32;
+constexpr int64_t kRsChunk = 256 * kRsPer;
+__global__ __launch_bounds__(256) void k_rs_scan(const unsigned long long* __restrict__ count, int64_t cap,
+                                                 int64_t rows, int32_t* __restrict__ row_cnt,
+                                                 int32_t* __restrict__ row_off, unsigned long long* status) {
   const int64_t K = (int64_t)*count;
   if (K > cap) return;
+  __shared__ int32_t wsum[4];
+  __shared__ unsigned long long s_pre;
   const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
-  int32_t carry = 0;
-  for (int64_t c0 = 0; c0 < rows; c0 += kRxScanLds) {
-    const int m = (int)min<int64_t>(kRxScanLds, rows - c0);
-    for (int j = tid; j < m; j += kRsScanThreads) {
-      sv[j] = row_cnt[c0 + j];
-      row_cnt[c0 + j] = 0;
-    }
-    __syncthreads();
-    const int per = (m + kRsScanThreads - 1) / kRsScanThreads;
-    const int lo = min(m, tid * per), hi = min(m, lo + per);
-    int32_t seg = 0;
-    for (int j = lo; j < hi; ++j) seg += sv[j];
-    int32_t incl = seg;
+  const int64_t blk = blockIdx.x;
+  const int64_t b = blk * kRsChunk + (int64_t)tid * kRsPer;
+  int32_t v[kRsPer];
+  if (b + kRsPer <= rows) {
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int32_t t = __shfl_up(incl, d);
-      if (lane >= d) incl += t;
+    for (int q = 0; q < kRsPer / 4; ++q) {
+      const int4 t = reinterpret_cast<const int4*>(row_cnt + b)[q];
+      v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
     }
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    int32_t run = carry + incl - seg, total = 0;
 #pragma unroll
-    for (int q = 0; q < kRsScanThreads / 64; ++q) {
-      const int32_t ws = wsum[q];
-      run += q < w ? ws : 0;
-      total += ws;
+    for (int q = 0; q < kRsPer / 4; ++q) reinterpret_cast<int4*>(row_cnt + b)[q] = make_int4(0, 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < kRsPer; ++i) {
+      v[i] = b + i < rows ? row_cnt[b + i] : 0;
+      if (b + i < rows) row_cnt[b + i] = 0;
     }
-    for (int j = lo; j < hi; ++j) {
-      const int32_t x = sv[j];
-      sv[j] = run;
-      run += x;
-    }
-    carry += total;
-    __syncthreads();
-    for (int j = tid; j < m; j += kRsScanThreads) row_off[c0 + j] = sv[j];
-    __syncthreads();
   }
-  if (tid == 0) row_off[rows] = carry;
+  int32_t seg = 0;
+#pragma unroll
+  for (int i = 0; i < kRsPer; ++i) seg += v[i];
+  int32_t incl = seg;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int32_t t = __shfl_up(incl, d);
+    if (lane >= d) incl += t;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  const int32_t total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  int32_t run = incl - seg;
+  for (int q = 0; q < w; ++q) run += wsum[q];
+  if (tid == 0)
+    __hip_atomic_store(&status[blk], (1ull << 63) | (unsigned long long)(uint32_t)total, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  // the earlier workgroups' totals (bounded polls: they were dispatched
+  // before this one, so they publish)
+  long long pre = 0;
+  for (int64_t e = tid; e < blk; e += 256) {
+    unsigned long long sv = 0ull;
+    for (int it = 0; it < (1 << 22); ++it) {
+      sv = __hip_atomic_load(&status[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (sv >> 63) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    pre += (long long)(sv & 0xFFFFFFFFull);
+  }
+  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+  if (tid == 0) s_pre = 0;
+  __syncthreads();
+  if (lane == 0 && pre) atomicAdd(&s_pre, (unsigned long long)pre);
+  __syncthreads();
+  run += (int32_t)s_pre;
+  if (b + kRsPer <= rows) {
+#pragma unroll
+    for (int q = 0; q < kRsPer / 4; ++q) {
+      int4 t;
+      t.x = run; run += v[4 * q];
+      t.y = run; run += v[4 * q + 1];
+      t.z = run; run += v[4 * q + 2];
+      t.w = run; run += v[4 * q + 3];
+      reinterpret_cast<int4*>(row_off + b)[q] = t;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < kRsPer; ++i) {
+      if (b + i < rows) row_off[b + i] = run;
+      run += v[i];
+    }
+  }
+  if (blk == (int64_t)gridDim.x - 1 && tid == 0) row_off[rows] = (int32_t)s_pre + total;
 }
 
 __global__ __launch_bounds__(256) void k_rs_place(const unsigned long long* __restrict__ count, int64_t cap,
@@ -1785,10 +1865,12 @@ int dm_launch_bucket_sort(dm_grid* g, hipStream_t stream, long long* clusters, c
     // device-side count return)
     const int64_t expect = std::min<int64_t>(max_records, std::max<int64_t>(2 * g->sort_hint, 4096));
     const int eg = grid_for(expect, 256, 4096);
+    const int nsb = (int)((rows + kRsChunk - 1) / kRsChunk);
     DM_LAUNCH(k_rs_count, dim3(eg), dim3(256), 0, stream, clusters, labels, d_count, max_records, base, g->W,
-              g->rs_cnt, g->bs_key, g->bs_idx2);
+              g->rs_cnt, g->bs_key, g->bs_idx2, g->rs_status, nsb);
     DM_HIP(hipGetLastError());
-    DM_LAUNCH(k_rs_scan, dim3(1), dim3(kRsScanThreads), 0, stream, d_count, max_records, rows, g->rs_cnt, g->rs_off);
+    DM_LAUNCH(k_rs_scan, dim3(nsb), dim3(256), 0, stream, d_count, max_records, rows, g->rs_cnt, g->rs_off,
+              g->rs_status);
     DM_HIP(hipGetLastError());
     DM_LAUNCH(k_rs_place, dim3(eg), dim3(256), 0, stream, d_count, max_records, g->W, g->bs_key, g->bs_idx2,
               g->rs_off, g->bs_key2, g->bs_idx);
@@ -1820,7 +1902,7 @@ int dm_launch_bucket_sort(dm_grid* g, hipStream_t stream, long long* clusters, c
     const int dbp = std::min(db, bits - shift);
     DM_LAUNCH(k_rx_hist, dim3(bg), dim3(kRxThreads), 0, stream, d_count, max_records, ka, shift, dbp, g->bs_hist);
     DM_HIP(hipGetLastError());
-    DM_LAUNCH(k_rx_scan, dim3(1), dim3(kRxScanThreads), 0, stream, d_count, max_records, dbp, g->bs_hist);
+    DM_LAUNCH(k_rx_scan, dim3(1), dim3(kScanThreads), 0, stream, d_count, max_records, dbp, g->bs_hist);
     DM_HIP(hipGetLastError());
     DM_LAUNCH(k_rx_scatter, dim3(bg), dim3(kRxThreads), 0, stream, d_count, max_records, ka, va, shift, dbp,
               g->bs_hist, kb, vb);

@@ -366,6 +366,7 @@ struct dm_grid {
   // the LSD radix k_rx_*): per-row counters (zero between sorts) and offsets
   int32_t* rs_cnt = nullptr;      // [rs_rows]
   int32_t* rs_off = nullptr;      // [rs_rows + 1]
+  unsigned long long* rs_status = nullptr;  // [rs_rows / 8192 + 1] k_rs_scan's published workgroup totals
   int64_t rs_rows = 0;
   bool row_sort = true;
   int64_t sort_hint = 0, msort_hint = 0;  // clusters of the last band / merge readback
