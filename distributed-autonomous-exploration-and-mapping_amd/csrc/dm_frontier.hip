@@ -1290,16 +1290,19 @@ __device__ inline void put_sorted(double ox, double oy, double res, const long l
 // double on host and device).  rank_of (may be NULL) receives each input
 // record's sorted position.  More than kRankSortCap records: *sorted = 0
 // and the host sorts the raw records.
-// 256 threads (round 3; 1024 before): a workgroup that needs 16 wave slots
-// and 36 KiB of LDS on one CU waits for a CU to drain while the next batch's
-// k_tile_accum fills the chip beside the pass (DM_SORT_THREADS / _CHUNK: A/B)
+// DM_SORT_THREADS / _CHUNK (A/B): 256 threads with 2048-key chunks measured
+// 17.6 vs 11.1 us at C3 (profiles/r03_sort_width_fk_fmask_ab.log): the
+// waves' share of the compares, not the placement of a 16-wave workgroup
 #ifndef DM_SORT_THREADS
-#define DM_SORT_THREADS 256
+#define DM_SORT_THREADS 1024
 #endif
 #ifndef DM_SORT_CHUNK
-#define DM_SORT_CHUNK 2048
+#define DM_SORT_CHUNK 4096
 #endif
 constexpr int kSortChunk = DM_SORT_CHUNK;
+// clusters (predicted from the last collected pass) from which a band pass's
+// records reach the host by a DMA copy instead of the sort kernel's stores
+constexpr int64_t kDmaReadbackMin = 32768;
 constexpr int kSortThreads = DM_SORT_THREADS;
 constexpr int kSortWaves = kSortThreads / 64;
 constexpr int64_t kRankSortCap = 1 << 16;
@@ -2088,18 +2091,33 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   }
   dm_timer_begin(g, "sort_clusters", &t, ps);
   // the last collected pass predicts this one's cluster count (either sort
-  // is exact for any count; only their speed differs)
+  // is exact for any count; only their speed differs).  Many records (C5's
+  // 2e5+): the sort kernel writes only the readback header into mapped host
+  // memory and the records go over PCIe by a DMA copy after it
+  // (DM_DMA_READBACK=0: the kernel writes them, A/B): 10 MB of remote
+  // stores kept the sort kernel's waves -- and the CUs the next batch needs
+  // -- waiting on the link for ~0.2 ms
+  const bool dma = g->dma_readback && g->sort_hint > g->sort_min && g->sort_hint >= kDmaReadbackMin;
+  const int64_t kcap = dma ? 0 : g->h_out_cap;
   const int rc = g->sort_hint > g->sort_min
       ? dm_launch_bucket_sort(g, ps, g->clusters, fuse ? g->slot_acc : nullptr, fuse ? g->slot_label : nullptr,
                               g->cnt + CNT_CLUSTERS, g->slot_cap, g->row0, g->R, g->out_clu,
                               g->rank_of, g->cnt + CNT_SORTED, g->cnt, CNT_N, CNT_SORTED, g->fsh,
-                              g->h_out_dev, g->h_out_cap)
+                              g->h_out_dev, kcap)
       : dm_launch_rank_sort(ps, g->clusters, fuse ? g->slot_acc : nullptr, fuse ? g->slot_label : nullptr,
                             g->cnt + CNT_CLUSTERS, g->slot_cap, g->p.origin_x,
                             g->p.origin_y, g->p.resolution, g->out_clu, g->rank_of, g->cnt + CNT_SORTED,
-                            g->cnt, CNT_N, CNT_SORTED, g->fsh, g->h_out_dev, g->h_out_cap, g->sort_hint);
+                            g->cnt, CNT_N, CNT_SORTED, g->fsh, g->h_out_dev, kcap, g->sort_hint);
   dm_timer_end(g, &t);
   if (rc) return rc;
+  g->rb[g->cur_slot].dma_copied = -1;
+  if (dma) {
+    // the predicted count and a margin (the host copies any remainder)
+    const int64_t ncopy = std::min<int64_t>(g->h_out_cap, g->sort_hint + g->sort_hint / 4 + 64);
+    DM_HIP(dm_batch_flush_all());
+    DM_HIP(hipMemcpyAsync(g->h_out, g->out_clu, sizeof(dm_cluster) * (size_t)ncopy, hipMemcpyDeviceToHost, ps));
+    g->rb[g->cur_slot].dma_copied = ncopy;
+  }
   DM_HIP(batch.finish());
   return DM_OK;
 }
@@ -2112,7 +2130,8 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
 int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied) {
   const unsigned long long* hdr = dm_rb_header(g->h_out);
   memcpy(g->h_cnt, hdr, sizeof(unsigned long long) * CNT_N);
-  *copied = std::min<int64_t>(g->h_out_cap, g->slot_cap);
+  const int64_t dc = g->rb[g->cur_slot].dma_copied;
+  *copied = std::min<int64_t>(dc >= 0 ? dc : g->h_out_cap, std::min<int64_t>(g->h_out_cap, g->slot_cap));
   const unsigned long long most = hdr[CNT_N];
   if (g->h_cnt[CNT_OVERFLOW] & kOvPipeline)
     return dm_set_error(DM_ERR_PIPELINE, "the overlapped pipeline's front-end hand-off timed out: a map "

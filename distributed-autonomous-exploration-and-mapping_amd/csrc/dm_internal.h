@@ -174,6 +174,7 @@ struct dm_grid {
     uint64_t pass = 0;                // fr_pass / m_pass of the pass
     int64_t merge_n = 0;              // nranks * rec_cap of a merge
     uint64_t wepoch = 0, mepoch = 0;  // passes / merges that wrote out_clu / m_out so far
+    int64_t dma_copied = -1;          // >= 0: the pass's records reached h_out by a DMA copy of this many
   };
 #ifndef DM_RB_SLOTS
 #define DM_RB_SLOTS 2
@@ -369,6 +370,9 @@ struct dm_grid {
   unsigned long long* rs_status = nullptr;  // [rs_rows / 8192 + 1] k_rs_scan's published workgroup totals
   int64_t rs_rows = 0;
   bool row_sort = true;
+  // band passes with many clusters copy their records to the host with a DMA
+  // copy instead of the sort kernel's mapped stores (DM_DMA_READBACK=0: A/B)
+  bool dma_readback = true;
   int64_t sort_hint = 0, msort_hint = 0;  // clusters of the last band / merge readback
   int64_t ftile_hint = 0;                 // listed tiles of the last collected frontier pass
   int64_t runs_hint = 0, ftf_hint = 0;    // its runs and tiles with frontier cells
