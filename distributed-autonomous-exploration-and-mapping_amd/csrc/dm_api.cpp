@@ -542,7 +542,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     if (const char* sm = getenv("DM_SORT_MIN")) g->sort_min = std::max<int64_t>(0, atoll(sm));
     if (const char* rb = getenv("DM_RX_BITS")) g->rx_bits = std::min(11, std::max(4, atoi(rb)));
     if (const char* ls = getenv("DM_LARGE_SORT")) g->row_sort = strcmp(ls, "radix") != 0;
-    g->dma_readback = !dm_env_off("DM_DMA_READBACK");
+    g->dma_readback = dm_env_on("DM_DMA_READBACK");
     g->big_concurrent = !dm_env_off("DM_BIG_STREAM");
     g->fe_staged = dm_env_on("DM_FE_STAGED");  // staged front-end: opt-in (A/B: slower pipelined)
   }

@@ -370,9 +370,13 @@ struct dm_grid {
   unsigned long long* rs_status = nullptr;  // [rs_rows / 8192 + 1] k_rs_scan's published workgroup totals
   int64_t rs_rows = 0;
   bool row_sort = true;
-  // band passes with many clusters copy their records to the host with a DMA
-  // copy instead of the sort kernel's mapped stores (DM_DMA_READBACK=0: A/B)
-  bool dma_readback = true;
+  // DM_DMA_READBACK=1 (A/B): band passes with many clusters copy their
+  // records to the host with a DMA copy after the sort instead of the sort
+  // kernel's mapped stores.  Off by default: at C5-4096 the sort kernels
+  // drop 230 -> 41 us, but the copy then runs after them instead of
+  // overlapping them and the pass ends later (step 1.48 -> 1.59 ms,
+  // profiles/r03_dma_readback_ab.log)
+  bool dma_readback = false;
   int64_t sort_hint = 0, msort_hint = 0;  // clusters of the last band / merge readback
   int64_t ftile_hint = 0;                 // listed tiles of the last collected frontier pass
   int64_t runs_hint = 0, ftf_hint = 0;    // its runs and tiles with frontier cells
