@@ -3,9 +3,7 @@ goes.  Times K steps of
   full   integrate + frontier pass, pipelined as bench.py (overlap on, depth 2)
   int    integrate only, overlap on (front-end on its own stream)
   int1   integrate only, overlap off (one stream)
-  fe     the integrate front-end alone: DM_FE_ONLY-style, by integrating an
-         empty-range batch is not possible, so instead: full with a pass
-         every 4th step (pass4)
+  pass4  integrate every step, a frontier pass every 4th step
 Prints us per step for each mode.  Diagnostic only (never the bench line).
 Usage: python tools/cycle_probe.py [steps]"""
 import os
