@@ -881,10 +881,17 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
   // sparse items (litems from the top, cnt_c of them): a second loop
   const int64_t SI = min((int64_t)cc, (int64_t)g.act_cap);
   const int64_t G = gridDim.x;
+  // Sparse items go to the workgroups after the dense ones (rank 0 = the
+  // workgroup right after the last dense item, wrapping around the grid), so
+  // they run beside the dense items instead of behind the first (longest)
+  // ones: a small call (one 360-beam scan) is one round of items, and its
+  // sparse tiles used to queue behind its heavy and medium tiles.
+  const int64_t sp_rank = ((int64_t)blockIdx.x - n_items % G + G) % G;
+  const unsigned long long idle =
+      ((int64_t)blockIdx.x >= n_items && sp_rank * (kQuarter / 64) >= SI) ? 1ull : 0ull;
   // a timed-out front-end hand-off (kHaltWord): this call's workspace was
   // never written, so nothing is applied (the host reports DM_ERR_PIPELINE).
   // One exit test on all four loads, so they go out together.
-  const unsigned long long idle = ((int64_t)blockIdx.x >= n_items && 2 * (int64_t)blockIdx.x >= SI) ? 1ull : 0ull;
   if ((hv | idle) != 0ull) return;
   auto item_of = [&](int64_t it) {
     int4 d = it < n_items ? (it < HI ? list_a[it] : list_b[it - HI]) : make_int4(0, 0, 0, -1);
@@ -1070,7 +1077,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
   const int hcx = (lane & 15) * 4;
   if (lane == 0) { s_wT[wv] = 0; s_wfree[wv] = 0; s_wU[wv] = 0u; }
   const int nw = kQuarter / 64;
-  for (int64_t it = (int64_t)blockIdx.x * nw + wv; it < SI; it += (int64_t)G * nw) {
+  for (int64_t it = sp_rank * nw + wv; it < SI; it += (int64_t)G * nw) {
     int4 d = list_b[(int64_t)g.act_cap - 1 - it];
     d.z = (int64_t)d.y + d.z <= g.seg_cap ? d.z : 0;  // never past the piece array
     const int32_t tile = d.x, c0 = d.y, c = d.z;
