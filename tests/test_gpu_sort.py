@@ -36,13 +36,20 @@ def _oracle_clusters(oracle_lib, p, st):
 LARGE_SORTS = ["row", "radix"]
 
 
+def _set_large_sort(monkeypatch, large_sort):
+    """DM_LARGE_SORT for the handle created next; "row-dma" is the row sort
+    with the opt-in DMA readback of large record lists (DM_DMA_READBACK=1)."""
+    monkeypatch.setenv("DM_LARGE_SORT", "radix" if large_sort == "radix" else "row")
+    monkeypatch.setenv("DM_DMA_READBACK", "1" if large_sort == "row-dma" else "0")
+
+
 # K: 26k (> kBucketSortMin, < the rank sort's 65536 cap), 105k (> both)
-@pytest.mark.parametrize("large_sort", LARGE_SORTS)
+@pytest.mark.parametrize("large_sort", LARGE_SORTS + ["row-dma"])
 @pytest.mark.parametrize("R,W,seed", [(512, 512, 1), (1024, 1024, 2)])
 def test_bucket_sort_band(oracle_lib, monkeypatch, R, W, seed, large_sort):
     import dm
 
-    monkeypatch.setenv("DM_LARGE_SORT", large_sort)
+    _set_large_sort(monkeypatch, large_sort)
     big = sparse_state(seed, R, W)
     small = cases.blob_state(seed, R, W, n_blobs=40)      # a few dozen clusters
     mid = cases.random_state(seed + 7, R, W)              # a few thousand
@@ -72,7 +79,7 @@ def test_bucket_sort_band(oracle_lib, monkeypatch, R, W, seed, large_sort):
 def test_bucket_sort_min_size_filter(oracle_lib, monkeypatch, large_sort):
     import dm
 
-    monkeypatch.setenv("DM_LARGE_SORT", large_sort)
+    _set_large_sort(monkeypatch, large_sort)
     st = cases.random_state(5, 768, 640, p_free=0.45, p_occ=0.05)
     p = cases.make_params(640, 768, min_frontier_size=3)
     exp = _oracle_clusters(oracle_lib, p, st)
@@ -92,7 +99,7 @@ def test_bucket_sort_merge(oracle_lib, monkeypatch, P, large_sort):
     import torch
     from dm.sharded import band_params
 
-    monkeypatch.setenv("DM_LARGE_SORT", large_sort)
+    _set_large_sort(monkeypatch, large_sort)
     R, W = 1024, 1024
     st = sparse_state(2, R, W)
     p = cases.make_params(W, R)
@@ -140,7 +147,7 @@ def test_radix_sort_clusters_packed_in_few_rows(oracle_lib, monkeypatch, R, W, r
     the second pass is sorted by the large-K path (hint from the first)."""
     import dm
 
-    monkeypatch.setenv("DM_LARGE_SORT", large_sort)
+    _set_large_sort(monkeypatch, large_sort)
     st = np.full((R, W), -1, np.int8)
     for k in range(rows):
         st[R // 2 + 2 * k, ::2] = 0  # isolated free cells: W / 2 clusters per row
