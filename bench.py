@@ -76,11 +76,60 @@ def parse():
                     help="skip the explored-map frontier measurement (frontier_ms_explored)")
     ap.add_argument("--no-host-inputs", action="store_true",
                     help="skip the PCIe-inclusive measurement (value_host_inputs)")
+    ap.add_argument("--step-trace", default=None,
+                    help="C3 / C4: write every timed step's host start-to-start time (us) to this JSON file")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: start N rank
+    processes of this same script (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment, exactly what
+    torch.distributed.run would give them) and wait for them.  This process
+    never touches the GPU (no torch import), so the children are fresh
+    processes, not an exec of a GPU-initialised one.  Rank 0 prints the JSON
+    line on the inherited stdout; the first rank that fails ends the others
+    (their own PIDs) and its exit code is returned."""
+    import subprocess
+
+    n = args.gpus
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   DM_BENCH_LAUNCHER="bench.py --gpus N (self-spawned ranks)")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:  # a failed rank: end the others (exact PIDs)
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc if rc >= 0 else 128 - rc
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(spawn_ranks(args))
     if args.config not in ("C3", "C4"):
         return run_config(args)
     c4 = args.config == "C4"
@@ -92,8 +141,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world_size != args.gpus:
-        if world_size == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}: launch N ranks with "
+                         "torch.distributed.run or let bench.py spawn them (no WORLD_SIZE)")
     if args.device_override is not None:
         local_rank = args.device_override
     torch.cuda.set_device(local_rank)
@@ -254,6 +303,15 @@ def main():
 
     barrier()
     torch.cuda.synchronize()
+    # no cyclic-GC pass inside the timed steps (the objects of warm-up and
+    # setup are frozen first): a collection is a host stall of 0.1+ ms that
+    # the pipelined step cannot hide (as timeit does; reference counting still
+    # frees everything the steps create)
+    import gc
+
+    gc.collect()
+    gc.freeze()
+    gc.disable()
     t0 = time.perf_counter()
     marks = []
     fr = run_steps(args.warmup, args.steps, marks=marks)
@@ -261,19 +319,33 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
-    batching = {k: band.last_stats()[k] for k in ("graph_launches", "direct_launches", "graph_hits",
-                                                  "graph_misses")}
+    gc.enable()
+    gc.unfreeze()
+    if args.step_trace:
+        with open(args.step_trace, "w") as f:
+            json.dump({"rank": rank, "step_us": (np.diff(np.asarray(marks)) * 1e6).tolist()}, f)
     cdev = dev if args.backend == "nccl" else torch.device("cpu")
-    if world_size > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     U_rank = sum(counts[(args.warmup + k) % len(counts)][0] for k in range(args.steps))
     U_all = U_rank
+    ranks_info = None
     if world_size > 1:
-        t = torch.tensor([U_rank], dtype=torch.int64, device=cdev)
+        # per-rank record of the timed region: [elapsed s, updates, exchange
+        # fallbacks, step p50 us, step max us], summed into rank order
+        cad = _cadence(marks) or {"p50": 0.0, "max": 0.0}
+        t = torch.zeros((world_size, 5), dtype=torch.float64, device=cdev)
+        t[rank] = torch.tensor([elapsed, float(U_rank), float(getattr(mapper, "fallbacks", 0)),
+                                cad["p50"], cad["max"]], dtype=torch.float64)
         dist.all_reduce(t)
-        U_all = int(t.item())
+        per = t.cpu().numpy()
+        elapsed = float(per[:, 0].max())
+        U_all = int(round(per[:, 1].sum()))
+        ranks_info = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                      "launcher": os.environ.get("DM_BENCH_LAUNCHER", "torch.distributed.run"),
+                      "ms_per_step": [float(x) / args.steps * 1e3 for x in per[:, 0]],
+                      "updates": [int(round(x)) for x in per[:, 1]],
+                      "exchange_fallbacks": [int(x) for x in per[:, 2]],
+                      "step_wall_us_p50": [float(x) for x in per[:, 3]],
+                      "step_wall_us_max": [float(x) for x in per[:, 4]]}
 
     # integrate-only and frontier-only timings (untimed w.r.t. `value`)
     reps = max(3, min(args.steps, 20))
@@ -306,13 +378,10 @@ def main():
     avg = {name: tot / max(1, n) for name, (n, tot) in kstats.items()}
     dominant = max(kstats, key=lambda n: kstats[n][1]) if kstats else None
     # roofline of the dominant integrate kernel, k_tile_accum: it performs
-    # every update (8 B each) and applies the touched cells (25 B each) —
-    # all of them, heavy tiles included, unless a separate k_heavy_apply ran
-    # (DM_HEAVY_SEPARATE=1)
-    TH_mean = float(np.mean([st["touched_heavy"] for st in stats])) if "heavy_apply" in kstats else 0.0
+    # every update (8 B each) and applies every touched cell (25 B each),
+    # heavy tiles included
     t_accum_ms = avg.get("tile_accum", float("nan"))
-    bytes_accum = (TILE_APPLY_BYTES_PER_UPDATE * U_mean
-                   + TILE_APPLY_BYTES_PER_TOUCHED * (T_mean - TH_mean))
+    bytes_accum = TILE_APPLY_BYTES_PER_UPDATE * U_mean + TILE_APPLY_BYTES_PER_TOUCHED * T_mean
     achieved = bytes_accum / (t_accum_ms * 1e-3) / 1e9 if t_accum_ms > 0 else None
     workload = "C4" if c4 else "C3"
     traffic, traffic_src = pmc_traffic("k_tile_accum", workload)
@@ -427,7 +496,7 @@ def main():
                                  if traffic and t_accum_ms > 0 else None),
                 "avg_launch_ms": t_accum_ms,
                 "algorithmic_bytes_per_launch": bytes_accum,
-                "bytes_model": ("8*U + 25*(T - T_heavy) per call" if TH_mean else "8*U + 25*T per call") + " (SURVEY.md §8(d) per-unit figures)",
+                "bytes_model": "8*U + 25*T per call (SURVEY.md §8(d) per-unit figures)",
                 "atomics": atom,
                 "frontier": fr_roof,
             },
@@ -439,7 +508,11 @@ def main():
             "scans_per_rank_batch": float(np.mean([p.shape[0] for p, _ in pool])),
             "exchange": ("device: RCCL all-gather of halo rows + export records, dm_merge_bands"
                          if world_size > 1 else None),
-            "exchange_fallbacks": getattr(mapper, "fallbacks", 0),
+            "exchange_fallbacks": (sum(ranks_info["exchange_fallbacks"]) if ranks_info
+                                   else getattr(mapper, "fallbacks", 0)),
+            # N > 1: the world size the process group reports, the launcher,
+            # and every rank's own timed region (value uses the slowest)
+            "ranks": ranks_info,
             "pipelined": (f"step k+1's integrate front-end overlaps step k's frontier pass "
                           f"(dm_set_overlap + dm_frontiers_begin/_end), {args.depth} passes in flight")
             if pipelined else None,
@@ -448,8 +521,6 @@ def main():
             # host-side start-to-start time of each timed step (rank 0): a
             # host stall shows here as a long tail, kernel time in `roofline`
             "step_wall_us": _cadence(marks),
-            # libdm's launch batching (dm_batch.h) over the whole run so far
-            "launch_batching": batching,
         }
         print(json.dumps(result), flush=True)
     mapper.close()
@@ -485,11 +556,21 @@ def pmc_traffic(kernel, workload):
     return w.get("kernels", {}).get(kernel, {}).get("traffic_bytes"), src
 
 
-FRONTIER_KERNELS = ("frontier_prep", "frontier_bits", "frontier_tile", "frontier_big", "frontier_merge", "frontier_resolve",
+# the pass's kernels in stream order; frontier_big runs on its own stream
+# beside frontier_tile, so the pass's device time counts the
+# longer of the two
+FRONTIER_KERNELS = ("frontier_prep", "frontier_bits", "frontier_tile", "frontier_big", "frontier_resolve",
                     "frontier_compact", "sort_clusters")
-PMC_FRONTIER_KERNELS = ("k_frontier_prep", "k_frontier_bits", "k_frontier_tile", "k_frontier_tile_big", "k_frontier_merge", "k_frontier_resolve",
-                        "k_frontier_compact", "k_rank_sort", "k_rx_init", "k_rx_hist", "k_rx_scan",
-                        "k_rx_scatter", "k_rx_emit")
+PMC_FRONTIER_KERNELS = ("k_frontier_prep", "k_frontier_bits", "k_frontier_tile", "k_frontier_tile_big",
+                        "k_frontier_resolve", "k_frontier_compact", "k_rank_sort", "k_rs_count", "k_rs_scan",
+                        "k_rs_place", "k_rs_rank")
+
+
+def frontier_device_ms(avg):
+    """Device time of a pass from per-kernel averages: the kernels in stream
+    order, with frontier_tile and frontier_big (concurrent) as the longer."""
+    serial = sum(avg.get(k, 0.0) for k in FRONTIER_KERNELS if k not in ("frontier_tile", "frontier_big"))
+    return serial + max(avg.get("frontier_tile", 0.0), avg.get("frontier_big", 0.0))
 
 
 def frontier_roofline(avg, cells, F, K, tiles_visited, workload, wall_s=None):
@@ -502,7 +583,7 @@ def frontier_roofline(avg, cells, F, K, tiles_visited, workload, wall_s=None):
     + a 4096-byte mask each: `visited_bytes`), `frac_full_map` the whole-map
     model (it charges bytes a sparse pass never touches), and
     `frac_traffic` the PMC-measured bytes."""
-    t_ms = sum(avg.get(k, 0.0) for k in FRONTIER_KERNELS)
+    t_ms = frontier_device_ms(avg)
     B = 2.0 * cells + 16.0 * F + 48.0 * K
     ach_full = B / (t_ms * 1e-3) / 1e9 if t_ms > 0 else None
     out = {"bound": "hbm", "bytes_model": "(4096 + 260 + 4096)*tiles_visited + 16*F + 48*K per pass "
@@ -669,7 +750,7 @@ def _cadence(marks):
             "max": float(d.max()), "n": int(d.size)}
 
 
-def _profiled_roofline(band, run, U_mean, T_mean, TH_mean):
+def _profiled_roofline(band, run, U_mean, T_mean):
     """Per-kernel average launch time (HIP events on the library's stream)
     over `run()`, and the k_tile_accum roofline (SURVEY.md §8(d) bytes)."""
     band.profile(True)
@@ -679,16 +760,13 @@ def _profiled_roofline(band, run, U_mean, T_mean, TH_mean):
     band.profile(False)
     avg = {name: tot / max(1, n) for name, (n, tot) in kstats.items()}
     t_ms = avg.get("tile_accum", float("nan"))
-    if "heavy_apply" not in kstats:  # heavy tiles applied inside k_tile_accum
-        TH_mean = 0.0
-    bytes_accum = (TILE_APPLY_BYTES_PER_UPDATE * U_mean
-                   + TILE_APPLY_BYTES_PER_TOUCHED * (T_mean - TH_mean))
+    bytes_accum = TILE_APPLY_BYTES_PER_UPDATE * U_mean + TILE_APPLY_BYTES_PER_TOUCHED * T_mean
     achieved = bytes_accum / (t_ms * 1e-3) / 1e9 if t_ms > 0 else None
     return avg, {
         "kernel": "tile_accum", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
         "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
         "traffic": None, "avg_launch_ms": t_ms, "algorithmic_bytes_per_launch": bytes_accum,
-        "bytes_model": ("8*U + 25*(T - T_heavy) per call" if TH_mean else "8*U + 25*T per call") + " (SURVEY.md §8(d) per-unit figures)",
+        "bytes_model": "8*U + 25*T per call (SURVEY.md §8(d) per-unit figures)",
     }
 
 
@@ -774,13 +852,12 @@ def _run_replay(args, np, torch, synth, m, params, amin, dev):
         m.integrate_device(p0 + 32 * k, 1, r0 + 4 * N * k, N, amin, inc)
 
     # per-scan U / T (properties of the scan, not of the map), untimed
-    U = T = TH = 0
+    U = T = 0
     for k in range(n):
         integrate(k)
         st = m.last_stats()
         U += st["updates"]
         T += st["touched"]
-        TH += st["touched_heavy"]
     m.reset()
     _pipelined(m, integrate, range(min(args.warmup * 20, n)))
     m.reset()
@@ -802,7 +879,7 @@ def _run_replay(args, np, torch, synth, m, params, amin, dev):
         m.frontiers()
         tf.append(time.perf_counter() - a)
     avg, roof = _profiled_roofline(m, lambda: [(integrate(k), m.frontiers()) for k in range(reps)],
-                                   U / n, T / n, TH / n)
+                                   U / n, T / n)
     cpu = None
     if args.cpu_seconds > 0:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -897,7 +974,7 @@ def _run_c5(args, np, torch, synth, m, params, amin, dev, world):
         fst = m.last_stats()  # the last pass's listed tiles, tile-local components, clusters
         mean = lambda key: float(np.mean([st[key] for st in stats]))  # noqa: E731
         avg, roof = _profiled_roofline(m, lambda: [(integrate(k), m.frontiers()) for k in range(5)],
-                                       mean("updates"), mean("touched"), mean("touched_heavy"))
+                                       mean("updates"), mean("touched"))
         rows.append({"beams_per_scan": N, "value": U / elapsed,
                      "ms_per_step": elapsed / args.steps * 1e3,
                      "integrate_ms": float(np.median(ti)) * 1e3,

@@ -47,10 +47,6 @@ bool dm_env_on(const char* name) {  // opt-in A/B switches: NAME=1
   return v && v[0] == '1';
 }
 
-bool dm_env_off(const char* name) {  // opt-out A/B switches: NAME=0
-  const char* v = getenv(name);
-  return v && v[0] == '0';
-}
 
 struct HostCluster {
   long long label, size, sum_x, sum_y;
@@ -120,28 +116,13 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
     int rc = dev_alloc(&g->beams, nbc, "beams");
     if (!rc) rc = dev_alloc(&g->blk_hist, bc * 1024, "per-block tile histograms");
     if (!rc) rc = dev_alloc(&g->blk_n, bc, "per-block histogram sizes");
-    if (!rc) rc = dev_alloc(&g->blk_np, bc, "per-block staged pieces");
     if (rc) { g->beams_cap = g->blk_cap = 0; return rc; }
     g->beams_cap = nbc;
     g->blk_cap = bc;
   }
-  // staged pieces: a region of 256 threads x the per-beam bound per workgroup
-  // (a thread enumerates one beam or one k-range of it)
-  if (g->fe_staged) {
-    const int64_t sb = std::max<int64_t>(256 * per_beam, g->stage_blk);
-    const int64_t sc = sb * g->blk_cap;
-    if (sc > g->stage_cap) {
-      int rc = dev_alloc(&g->stage, sc, "staged ray pieces");
-      if (!rc) rc = dev_alloc(&g->stage_sr, sc, "staged piece places");
-      if (rc) { g->stage_cap = g->stage_blk = 0; return rc; }
-      g->stage_cap = sc;
-    }
-    g->stage_blk = sb;
-  }
   const int64_t segs = nb * per_beam;
   if (segs > g->segs_cap) {
     for (auto& w : g->iw) {
-      if (&w - g->iw >= g->n_iw) break;
       int rc = dev_alloc(&w.pieces, segs, "ray pieces");
       if (rc) { g->segs_cap = 0; return rc; }
     }
@@ -152,8 +133,8 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   if (act < 1) act = 1;
   if (act > g->act_cap) {
     int rc = dev_alloc(&g->act_raw, act * kShards, "first-touch lists");
-    for (int i = 0; i < g->n_iw; ++i)
-      if (!rc) rc = dev_alloc(&g->iw[i].litems, act, "light work items");
+    for (auto& w : g->iw)
+      if (!rc) rc = dev_alloc(&w.litems, act, "light work items");
     if (rc) { g->act_cap = 0; return rc; }
     g->act_cap = act;
   }
@@ -165,7 +146,6 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   const int64_t hitems = segs / chunk + segs / (chunk + 1) + 2;
   if (hitems > g->hitem_cap) {
     for (auto& w : g->iw) {
-      if (&w - g->iw >= g->n_iw) break;
       int rc = dev_alloc(&w.hitems, hitems, "heavy work items");
       if (rc) { g->hitem_cap = 0; return rc; }
     }
@@ -173,7 +153,6 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   }
   if (heavy > g->heavy_cap) {
     for (auto& w : g->iw) {
-      if (&w - g->iw >= g->n_iw) break;
       int rc = dev_alloc(&w.heavy_list, heavy, "heavy tiles");
       if (!rc) rc = dev_alloc(&w.slabs, heavy * 2 * DM_TILE * DM_TILE, "heavy-tile slabs");
       if (!rc) rc = dev_alloc(&w.heavy_done, heavy, "heavy-tile item tickets");
@@ -215,13 +194,11 @@ int ensure_trig(dm_grid* g, int32_t N, float amin, float inc) {
 // sort may be asked to order (band slot_cap, merge m_cap).
 int dm_grow_bucket_sort(dm_grid* g, int64_t n) {
   if (n <= g->bs_cap) return DM_OK;
-  int rc = dev_alloc(&g->bs_key, n, "radix-sort keys");
-  if (!rc) rc = dev_alloc(&g->bs_key2, n, "radix-sort keys");
-  if (!rc) rc = dev_alloc(&g->bs_idx, n, "radix-sort indices");
-  if (!rc) rc = dev_alloc(&g->bs_idx2, n, "radix-sort indices");
-  // k_rx_*: digit x block counts (up to 2^11 digits, blocks of kRxItems keys)
-  if (!rc) rc = dev_alloc(&g->bs_hist, ((int64_t)1 << g->rx_bits) * (ceil_div(n, dm_rx_items()) + 1), "radix-sort histograms");
-  if (!rc && g->rs_rows < g->H) {  // row-bucket sort: rows of the whole map (merges sort over H rows)
+  int rc = dev_alloc(&g->bs_key, n, "row-sort keys");
+  if (!rc) rc = dev_alloc(&g->bs_key2, n, "row-sort keys");
+  if (!rc) rc = dev_alloc(&g->bs_idx, n, "row-sort indices");
+  if (!rc) rc = dev_alloc(&g->bs_idx2, n, "row-sort indices");
+  if (!rc && g->rs_rows < g->H) {  // rows of the whole map (merges sort over H rows)
     rc = dev_alloc(&g->rs_cnt, g->H, "row-sort counters");
     if (!rc) rc = dev_alloc(&g->rs_off, g->H + 1, "row-sort offsets");
     if (!rc) rc = dev_alloc(&g->rs_status, g->H / 8192 + 2, "row-sort workgroup totals");
@@ -269,35 +246,47 @@ int grow_host_out(dm_grid* g, int slot, int64_t need) {
   dm_grid::RbSlot& r = g->rb[slot];
   if (need <= r.h_out_cap) return DM_OK;
   int64_t cap = std::max<int64_t>(need, 2 * r.h_out_cap);
-  if (r.h_out) (void)hipHostFree(r.h_out - kRbRecords);
+  if (r.h_out) (void)hipHostFree(r.h_out - kRbHostRecords);
   r.h_out = nullptr;
   r.h_out_cap = 0;
   // mapped + coherent: k_rank_sort writes the readback header and the first
-  // records straight into it over PCIe (no D2H copy command per call)
-  dm_cluster* base = nullptr;
-  DM_HIP(hipHostMalloc((void**)&base, sizeof(dm_cluster) * (size_t)(cap + kRbRecords),
+  // records (32 bytes each) straight into it over PCIe (no D2H copy command
+  // per call)
+  dm_raw_record* base = nullptr;
+  DM_HIP(hipHostMalloc((void**)&base, sizeof(dm_raw_record) * (size_t)(cap + kRbHostRecords),
                        hipHostMallocMapped | hipHostMallocCoherent));
-  dm_cluster* dbase = nullptr;
+  dm_raw_record* dbase = nullptr;
   const hipError_t e = hipHostGetDevicePointer((void**)&dbase, base, 0);
   if (e != hipSuccess) {
     (void)hipHostFree(base);
     return dm_hip_check(e, "hipHostGetDevicePointer(cluster readback)");
   }
-  r.h_out = base + kRbRecords;
-  r.h_out_dev = dbase + kRbRecords;
+  r.h_out = base + kRbHostRecords;
+  r.h_out_dev = dbase + kRbHostRecords;
   r.h_out_cap = cap;
   return DM_OK;
 }
 
 // Copy nw sorted cluster records to `out`: the first `have` are already in
-// g->h_out (arrived with the counters); the rest come from d_sorted.  When
-// the device could not sort (too many records), sort the n raw records of
-// d_raw ([n][4] int64) here and compute the centroids with the same formula.
+// g->h_out (32-byte records that arrived with the counters: the centroids
+// are added here, dm_centroid); the rest come from d_sorted.  When the device
+// could not sort (too many records), sort the n raw records of d_raw ([n][4]
+// int64) here and compute the centroids with the same formula.
 int copy_clusters(dm_grid* g, bool sorted, int64_t n, int64_t nw, int64_t have,
                   const dm_cluster* d_sorted, const long long* d_raw, dm_cluster* out) {
   if (sorted) {
     have = std::min<int64_t>(have, nw);
-    if (have > 0) memcpy(out, g->h_out, sizeof(dm_cluster) * (size_t)have);
+    const double ox = g->p.origin_x, oy = g->p.origin_y, res = g->p.resolution;
+    for (int64_t i = 0; i < have; ++i) {
+      const dm_raw_record& q = g->h_out[i];
+      dm_cluster& c = out[i];
+      c.label = q.label;
+      c.size = q.size;
+      c.sum_x = q.sum_x;
+      c.sum_y = q.sum_y;
+      c.cx_m = dm_centroid(ox, q.sum_x, q.size, res);
+      c.cy_m = dm_centroid(oy, q.sum_y, q.size, res);
+    }
     if (nw > have)
       DM_HIP(hipMemcpy(out + have, d_sorted + have, sizeof(dm_cluster) * (size_t)(nw - have),
                        hipMemcpyDeviceToHost));
@@ -312,10 +301,8 @@ int copy_clusters(dm_grid* g, bool sorted, int64_t n, int64_t nw, int64_t have,
     c.size = hc[i].size;
     c.sum_x = hc[i].sum_x;
     c.sum_y = hc[i].sum_y;
-    const double mx = (double)c.sum_x / (double)c.size;
-    const double my = (double)c.sum_y / (double)c.size;
-    c.cx_m = g->p.origin_x + (mx + 0.5) * g->p.resolution;
-    c.cy_m = g->p.origin_y + (my + 0.5) * g->p.resolution;
+    c.cx_m = dm_centroid(g->p.origin_x, c.sum_x, c.size, g->p.resolution);
+    c.cy_m = dm_centroid(g->p.origin_y, c.sum_y, c.size, g->p.resolution);
   }
   return DM_OK;
 }
@@ -503,9 +490,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   };
   if ((rc = dev_alloc(&g->L, cells, "log-odds"))) return fail(rc);
   if ((rc = dev_alloc(&g->state, cells, "state"))) return fail(rc);
-  if (const char* is = getenv("DM_INT_SETS")) g->n_iw = std::min(dm_grid::kIntSetsMax, std::max(2, atoi(is)));
   for (auto& w : g->iw) {
-    if (&w - g->iw >= g->n_iw) break;
     if ((rc = dev_alloc(&w.tile_count, g->NT, "tile counts"))) return fail(rc);
     if ((rc = dev_alloc(&w.tile_cur, g->NT, "tile bin cursors"))) return fail(rc);
     if ((rc = dev_alloc(&w.cnt, CNT_N, "integrate counters"))) return fail(rc);
@@ -515,38 +500,23 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   }
   if ((rc = dev_alloc(&g->tile_free, g->NT, "tile free counts"))) return fail(rc);
   if ((rc = dev_alloc(&g->fmask, g->NT * DM_TILE * 16, "tile free / unknown bit rows"))) return fail(rc);
-  {
-    const char* sep = getenv("DM_HEAVY_SEPARATE");
-    g->fuse_heavy = !(sep && sep[0] == '1');
-    // cross-stream hand-offs (C3 A/B): the front-end ->
-    // map update by a device-side seq gate (DM_FE_GATE=0: an event wait;
-    // gate 215-218 vs event 211-213 x 10^9, profiles/r02_fe_gate_ab.log), the
-    // bit rows -> pass stream by an event wait (DM_PASS_GATE=1: a seq gate,
-    // 179-183 x 10^9 when it still freed the integrate workspaces by the
-    // readback event).  Either way the workspaces are freed by an event on
-    // the grid stream after the bit rows (a timed-out pass gate cannot free
-    // them before the accumulation that reads them)
-    g->fe_gate = !dm_env_off("DM_FE_GATE");
-    g->pass_gate = dm_env_on("DM_PASS_GATE");
-    if (const char* ag = getenv("DM_ACCUM_GRID")) g->accum_grid = std::max(1, atoi(ag));
-    if (const char* ct = getenv("DM_CHUNK_THREADS")) g->chunk_threads_per_cu = std::max(1, atoi(ct));
-    if (const char* sp = getenv("DM_SPARSE_PIECES")) g->sparse_pieces = std::max(0, atoi(sp));
-    // launch batching into graphs (dm_batch.h) only with DM_GRAPHS=1: measured
-    // neutral to slightly slower at C3
-    g->batch.enabled = dm_env_on("DM_GRAPHS");
-    g->fault_gate = dm_env_on("DM_FAULT_GATE");
-    const char* fm = getenv("DM_FMASK");
-    g->fmask_mode = fm && !strcmp(fm, "on") ? 1 : (fm && !strcmp(fm, "off") ? 2 : 0);
-    const char* fk = getenv("DM_FRONTIER_KERNEL");
-    g->frontier_kernel = fk && !strcmp(fk, "wave") ? 1 : (fk && !strcmp(fk, "wg") ? 2 : 0);
-    if (const char* sm = getenv("DM_SORT_MIN")) g->sort_min = std::max<int64_t>(0, atoll(sm));
-    if (const char* rb = getenv("DM_RX_BITS")) g->rx_bits = std::min(11, std::max(4, atoi(rb)));
-    if (const char* ls = getenv("DM_LARGE_SORT")) g->row_sort = strcmp(ls, "radix") != 0;
-    g->dma_readback = dm_env_on("DM_DMA_READBACK");
-    g->big_concurrent = !dm_env_off("DM_BIG_STREAM");
-    g->fe_staged = dm_env_on("DM_FE_STAGED");  // staged front-end: opt-in (A/B: slower pipelined)
-  }
+  // The five run-time switches (read once, here): DM_SPARSE_PIECES (0: no
+  // sparse work items), DM_FMASK=on|off (fmask maintenance forced either way),
+  // DM_FRONTIER_KERNEL=wave|wg (one frontier tile kernel for every pass),
+  // DM_SORT_MIN (cluster count above which the row sort runs) and
+  // DM_FAULT_GATE=1 (fault injection: the front-end hand-off never arrives).
+  // Each selects between paths the default also runs, so tests can drive
+  // every path on small maps; none changes a result.
+  if (const char* sp = getenv("DM_SPARSE_PIECES")) g->sparse_pieces = std::max(0, atoi(sp));
+  const char* fm = getenv("DM_FMASK");
+  g->fmask_mode = fm && !strcmp(fm, "on") ? 1 : (fm && !strcmp(fm, "off") ? 2 : 0);
+  const char* fk = getenv("DM_FRONTIER_KERNEL");
+  g->frontier_kernel = fk && !strcmp(fk, "wave") ? 1 : (fk && !strcmp(fk, "wg") ? 2 : 0);
+  if (const char* sm = getenv("DM_SORT_MIN")) g->sort_min = std::max<int64_t>(0, atoll(sm));
+  g->fault_gate = dm_env_on("DM_FAULT_GATE");
   for (auto& f : g->fw) {
+    e = hipEventCreateWithFlags(&f.ev_split, hipEventDisableTiming | hipEventDisableSystemFence);
+    if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
     if ((rc = dev_alloc(&f.cnt, CNT_N, "frontier counters"))) return fail(rc);
     DM_HIP(hipMemset(f.cnt, 0, sizeof(unsigned long long) * CNT_N));
     if ((rc = dev_alloc(&f.fsh, kShards * kShardWords, "frontier shard counters"))) return fail(rc);
@@ -567,7 +537,11 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   DM_HIP(hipMemset(g->rel, 0, sizeof(unsigned long long) * 4 * (size_t)g->NT));
   if ((rc = dev_alloc(&g->edge_label, 2 * g->W, "edge labels"))) return fail(rc);
   if ((rc = dev_alloc(&g->halo, 2 * g->W, "halo rows"))) return fail(rc);
-  if ((rc = grow_slots(g, 1 << 16))) return fail(rc);
+  // slot arrays sized for the map up front (a pass that overflows them has
+  // no result and must be rerun): two tile-local components per tile, ~276 B
+  // each (C3: 36 MB; a 65536^2 map: 0.6 GB of its 288 GB).  C5's sparse rays
+  // need ~8 per listed tile, i.e. at most 0.4 per tile of the map.
+  if ((rc = grow_slots(g, std::max<int64_t>(1 << 16, 2 * g->NT)))) return fail(rc);
   dm_select_fw(g, g->fparity);
   for (int sl = 0; sl <= dm_grid::kRbSlots; ++sl)
     if ((rc = grow_host_out(g, sl, 1 << 14))) return fail(rc);
@@ -582,71 +556,28 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipHostMalloc(merge counters)"));
   e = hipDeviceGetAttribute(&g->n_cu, hipDeviceAttributeMultiprocessorCount, device);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipDeviceGetAttribute(multiprocessor count)"));
-  // Stream priorities (DM_STREAM_PRIO=0 turns them off, for A/B): the map
-  // chain (accumulation, frontier pass) high, the integrate front-end low,
-  // so a front-end enqueued early fills what the map chain leaves idle
-  // instead of competing with the accumulation for its CUs.
-  // DM_STREAM_PRIO=XYZ (A/B): priorities of the map stream, the front-end
-  // stream and the pass stream, 'h' or 'l' each (default "hlh").
+  // Stream priorities: the map chain (accumulation, frontier prep and bit
+  // rows) and the pass's labelling streams high, the integrate front-end low,
+  // so a front-end enqueued early fills what the map chain leaves idle instead
+  // of competing with the accumulation for its CUs (round-2/3 A/B of every
+  // combination and of CU-masked streams: DESIGN.md §3.3).
   int prio_lo = 0, prio_hi = 0;
-  int p_grid = 0, p_fe = 0, p_pass = 0;
-  {
-    const char* sp = getenv("DM_STREAM_PRIO");
-    if (!(sp && sp[0] == '0')) (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    const char* pr = sp && strlen(sp) == 3 ? sp : "hlh";
-    p_grid = pr[0] == 'h' ? prio_hi : prio_lo;
-    p_fe = pr[1] == 'h' ? prio_hi : prio_lo;
-    p_pass = pr[2] == 'h' ? prio_hi : prio_lo;
-  }
-  // DM_FE_CUS=n (A/B): the integrate front-end's stream runs
-  // on CUs [0, n) of the CU mask and the map / pass streams on the rest, so
-  // batch k+1's front-end runs beside accumulation k instead of after its
-  // last dispatch (KFD spreads a contiguous range of mask bits evenly over
-  // the shader engines).  CU-masked streams carry no priority.
-  const int fe_cus = getenv("DM_FE_CUS") ? atoi(getenv("DM_FE_CUS")) : 0;
-  if (fe_cus > 0 && fe_cus < g->n_cu) {
-    std::vector<uint32_t> fe_mask((size_t)(g->n_cu + 31) / 32, 0u), map_mask(fe_mask.size(), 0u);
-    for (int c = 0; c < g->n_cu; ++c) (c < fe_cus ? fe_mask : map_mask)[(size_t)c / 32] |= 1u << (c % 32);
-    e = hipExtStreamCreateWithCUMask(&g->stream, (uint32_t)map_mask.size(), map_mask.data());
-    if (e != hipSuccess) return fail(dm_hip_check(e, "hipExtStreamCreateWithCUMask"));
-    g->own_stream = true;
-    e = hipExtStreamCreateWithCUMask(&g->fe_stream, (uint32_t)fe_mask.size(), fe_mask.data());
-    if (e != hipSuccess) return fail(dm_hip_check(e, "hipExtStreamCreateWithCUMask(front-end)"));
-    e = hipExtStreamCreateWithCUMask(&g->pass_stream, (uint32_t)map_mask.size(), map_mask.data());
-    if (e != hipSuccess) return fail(dm_hip_check(e, "hipExtStreamCreateWithCUMask(pass)"));
-    e = hipExtStreamCreateWithCUMask(&g->big_stream, (uint32_t)map_mask.size(), map_mask.data());
-    if (e != hipSuccess) return fail(dm_hip_check(e, "hipExtStreamCreateWithCUMask(big)"));
-  } else {
-    e = hipStreamCreateWithPriority(&g->stream, hipStreamNonBlocking, p_grid);
-    if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate"));
-    g->own_stream = true;
-    e = hipStreamCreateWithPriority(&g->fe_stream, hipStreamNonBlocking, p_fe);
-    if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(front-end)"));
-    // DM_PASS_CUS=n (A/B): the frontier labelling streams
-    // (pass, big) confined to CUs [0, n) while the map and front-end streams
-    // keep the whole chip, so a pass's labelling takes at most n CUs from the
-    // next batch's integrate
-    const int pass_cus = getenv("DM_PASS_CUS") ? atoi(getenv("DM_PASS_CUS")) : 0;
-    if (pass_cus > 0 && pass_cus < g->n_cu) {
-      std::vector<uint32_t> pm((size_t)(g->n_cu + 31) / 32, 0u);
-      for (int c = 0; c < pass_cus; ++c) pm[(size_t)c / 32] |= 1u << (c % 32);
-      e = hipExtStreamCreateWithCUMask(&g->pass_stream, (uint32_t)pm.size(), pm.data());
-      if (e != hipSuccess) return fail(dm_hip_check(e, "hipExtStreamCreateWithCUMask(pass)"));
-      e = hipExtStreamCreateWithCUMask(&g->big_stream, (uint32_t)pm.size(), pm.data());
-      if (e != hipSuccess) return fail(dm_hip_check(e, "hipExtStreamCreateWithCUMask(big)"));
-    } else {
-      e = hipStreamCreateWithPriority(&g->pass_stream, hipStreamNonBlocking, p_pass);
-      if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(pass)"));
-      e = hipStreamCreateWithPriority(&g->big_stream, hipStreamNonBlocking, p_pass);
-      if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(big)"));
-    }
-  }
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  e = hipStreamCreateWithPriority(&g->stream, hipStreamNonBlocking, prio_hi);
+  if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate"));
+  g->own_stream = true;
+  e = hipStreamCreateWithPriority(&g->fe_stream, hipStreamNonBlocking, prio_lo);
+  if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(front-end)"));
+  e = hipStreamCreateWithPriority(&g->pass_stream, hipStreamNonBlocking, prio_hi);
+  if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(pass)"));
+  e = hipStreamCreateWithPriority(&g->big_stream, hipStreamNonBlocking, prio_hi);
+  if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(big)"));
   // ev_fe / ev_free only order the two streams on the device: no system-
   // scope fence (no host-visible cache writeback at every step).  The host
   // waits on a readback slot's event and then reads mapped host memory:
   // default fences.
   for (hipEvent_t* ev : {&g->ev_fe, &g->ev_bits[0], &g->ev_bits[1], &g->iw[0].ev_free, &g->iw[1].ev_free,
-                         &g->iw[2].ev_free, &g->ev_bigfork, &g->ev_big}) {
+                         &g->ev_bigfork, &g->ev_big}) {
     e = hipEventCreateWithFlags(ev, hipEventDisableTiming | hipEventDisableSystemFence);
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
   }
@@ -668,21 +599,21 @@ int dm_destroy(dm_grid* g) {
   if (!g) return DM_OK;
   (void)hipSetDevice(g->device);
   (void)dm_sync_all(g);
-  dm_batch_release(&g->batch);
   for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
   for (hipEvent_t ev : {g->ev_fe, g->ev_bits[0], g->ev_bits[1], g->iw[0].ev_free, g->iw[1].ev_free,
-                        g->iw[2].ev_free, g->ev_bigfork, g->ev_big})
+                        g->ev_bigfork, g->ev_big})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& r : g->rb) {
     if (r.ev) (void)hipEventDestroy(r.ev);
     if (r.out_clu) (void)hipFree(r.out_clu - kRbRecords);
-    if (r.h_out) (void)hipHostFree(r.h_out - kRbRecords);
+    if (r.h_out) (void)hipHostFree(r.h_out - kRbHostRecords);
     dev_free(r.m_out);
   }
   if (g->fe_stream) (void)hipStreamDestroy(g->fe_stream);
   if (g->pass_stream) (void)hipStreamDestroy(g->pass_stream);
   if (g->big_stream) (void)hipStreamDestroy(g->big_stream);
   for (auto& f : g->fw) {
+    if (f.ev_split) (void)hipEventDestroy(f.ev_split);
     dev_free(f.cnt); dev_free(f.fsh); dev_free(f.ftiles); dev_free(f.big_tiles); dev_free(f.fbits);
     dev_free(f.edge_slot); dev_free(f.slot_parent);
   }
@@ -695,10 +626,9 @@ int dm_destroy(dm_grid* g) {
   }
   dev_free(g->L); dev_free(g->state); dev_free(g->fmask);
   dev_free(g->tile_free); dev_free(g->beams); dev_free(g->blk_hist); dev_free(g->blk_n);
-  dev_free(g->blk_np); dev_free(g->stage); dev_free(g->stage_sr);
   dev_free(g->trig);
   dev_free(g->pose4); dev_free(g->ranges); 
-  dev_free(g->bs_key); dev_free(g->bs_key2); dev_free(g->bs_idx); dev_free(g->bs_idx2); dev_free(g->bs_hist);
+  dev_free(g->bs_key); dev_free(g->bs_key2); dev_free(g->bs_idx); dev_free(g->bs_idx2);
   dev_free(g->rs_cnt); dev_free(g->rs_off); dev_free(g->rs_status);
   dev_free(g->border); dev_free(g->rel); dev_free(g->slot_label); dev_free(g->slot_root);
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
@@ -726,8 +656,7 @@ int dm_reset(dm_grid* g) {
   DM_HIP(hipMemsetAsync(g->L, 0, sizeof(float) * (size_t)cells, g->stream));
   DM_HIP(hipMemsetAsync(g->state, 0xFF, (size_t)cells, g->stream));
   DM_HIP(dm_sync_all(g));
-  for (int i = 0; i < g->n_iw; ++i)
-    DM_HIP(hipMemsetAsync(g->iw[i].tile_count, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
+  for (auto& w : g->iw) DM_HIP(hipMemsetAsync(w.tile_count, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
   DM_HIP(hipMemsetAsync(g->tile_free, 0, sizeof(int32_t) * (size_t)g->NT, g->stream));
   if ((rc = dm_launch_recount(g))) return rc;  // fmask: every in-grid cell unknown
   for (auto& f : g->fw) DM_HIP(hipMemsetAsync(f.cnt, 0, sizeof(unsigned long long) * CNT_N, g->stream));
@@ -866,15 +795,13 @@ int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out) {
   const unsigned long long* fs = g->h_sh + kShards * kShardWords;
   const unsigned long long* ic = g->h_cnt + CNT_N;  // the last integrate call's counters
   const uint64_t items = ic[CNT_ITEMS] + ic[CNT_LITEMS] + ic[CNT_SITEMS];  // heavy + light + sparse items
-  const uint64_t v[14] = {dm_shard_sum(g->h_sh, SH_U),  dm_shard_sum(g->h_sh, SH_T),
-                          dm_shard_sum(g->h_sh, SH_TH), ic[CNT_SEGS],
-                          ic[CNT_ACTIVE],               items,
-                          ic[CNT_HEAVY],                g->h_cnt[CNT_FL0],
-                          dm_shard_sum(fs, SH_SLOT),    g->h_cnt[CNT_CLUSTERS],
-                          g->batch.graph_launches,      g->batch.direct_launches,
-                          g->batch.hits,                g->batch.misses};
-  for (int32_t i = 0; i < cap && i < 14; ++i) out[i] = v[i];
-  if (n_out) *n_out = 14;
+  const uint64_t v[kNStats] = {dm_shard_sum(g->h_sh, SH_U),  dm_shard_sum(g->h_sh, SH_T),
+                               dm_shard_sum(g->h_sh, SH_TH), ic[CNT_SEGS],
+                               ic[CNT_ACTIVE],               items,
+                               ic[CNT_HEAVY],                g->h_cnt[CNT_FL0],
+                               dm_shard_sum(fs, SH_SLOT),    g->h_cnt[CNT_CLUSTERS]};
+  for (int32_t i = 0; i < cap && i < kNStats; ++i) out[i] = v[i];
+  if (n_out) *n_out = kNStats;
   return DM_OK;
 }
 
@@ -995,10 +922,35 @@ int dm_frontiers_export_device(dm_grid* g, void* d_export, int64_t rec_cap) {
   // can have every ring slot pending on its band 0)
   dm_select_slot(g, g->rb_count < dm_grid::kRbSlots ? (g->rb_head + g->rb_count) % dm_grid::kRbSlots
                                                     : dm_grid::kRbSync);
-  if ((rc = dm_enqueue_frontiers(g, false, false))) return rc;
-  if ((rc = dm_launch_export(g, d_export, rec_cap))) return rc;
-  DM_HIP(dm_mark_ws_free(g));
+  // with overlap, split as dm_frontiers_begin: the labelling, sort and
+  // export on the pass stream, beside the next batch's map update
+  hipStream_t es = g->stream;
+  if ((rc = dm_enqueue_frontiers(g, false, false, g->overlap, &es))) return rc;
+  if ((rc = dm_launch_export(g, es, d_export, rec_cap))) return rc;
+  if (es != g->stream) {
+    // the parity set is free again, and the grid stream may use the shared
+    // pass arrays, once the pass stream is past this export
+    dm_grid::FrWs& f = g->fw[g->fparity];
+    DM_HIP(hipEventRecord(f.ev_split, es));
+    f.busy = f.ev_split;
+    f.busy_pending = true;
+    f.busy_pass = g->fr_pass;
+    g->p_tail = f.ev_split;
+    g->p_pending = true;
+    g->p_tail_pass = g->fr_pass;
+  } else {
+    DM_HIP(dm_mark_ws_free(g));
+  }
   g->frontier_valid = true;
+  return DM_OK;
+}
+
+int dm_exchange_stream(dm_grid* g, void** stream) {
+  if (int rc0 = not_on_sharded(g, "dm_exchange_stream")) return rc0;
+  int rc = check_grid(g);
+  if (rc) return rc;
+  if (!stream) return dm_set_error(DM_ERR_INVALID_ARG, "stream is NULL");
+  *stream = (void*)dm_exchange_stream_of(g);
   return DM_OK;
 }
 
@@ -1080,10 +1032,18 @@ int dm_merge_bands_begin(dm_grid* g, const void* d_gathered, int32_t nranks, int
   if (n >= (1ll << 31)) return dm_set_error(DM_ERR_SHAPE, "nranks * rec_cap must be < 2^31");
   int slot = 0;
   if ((rc = grow_merge(g, n)) || (rc = claim_slot(g, &slot))) return rc;
-  DM_HIP(dm_join_pass_stream(g));  // the sort workspace is shared with the frontier passes
-  if ((rc = dm_launch_merge(g, d_gathered, nranks, rec_cap, min_size))) return rc;
+  // on the exchange stream: the grid stream's with overlap off (after the
+  // pass stream: the sort workspace is shared with the frontier passes), the
+  // pass stream's with overlap on (the exports' own order)
+  hipStream_t ms = dm_exchange_stream_of(g);
+  if (ms == g->stream) DM_HIP(dm_join_pass_stream(g));
+  if ((rc = dm_launch_merge(g, ms, d_gathered, nranks, rec_cap, min_size))) return rc;
   dm_grid::RbSlot& r = g->rb[slot];
-  DM_HIP(hipEventRecord(r.ev, g->stream));
+  DM_HIP(hipEventRecord(r.ev, ms));
+  if (ms != g->stream) {
+    g->p_tail = r.ev;
+    g->p_pending = true;
+  }
   r.kind = 2;
   r.merge_n = n;
   r.gen = g->rb_gen;
@@ -1116,10 +1076,20 @@ int dm_merge_bands(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t r
   if (n >= (1ll << 31)) return dm_set_error(DM_ERR_SHAPE, "nranks * rec_cap must be < 2^31");
   if ((rc = grow_merge(g, n))) return rc;
   dm_select_slot(g, dm_grid::kRbSync);  // its own slot: asynchronous passes may be in flight
-  DM_HIP(dm_join_pass_stream(g));  // the sort workspace is shared with the frontier passes
-  if ((rc = dm_launch_merge(g, d_gathered, nranks, rec_cap, min_size))) return rc;
-  DM_HIP(hipStreamSynchronize(g->stream));
+  hipStream_t ms = dm_exchange_stream_of(g);  // as dm_merge_bands_begin
+  if (ms == g->stream) DM_HIP(dm_join_pass_stream(g));
+  if ((rc = dm_launch_merge(g, ms, d_gathered, nranks, rec_cap, min_size))) return rc;
+  DM_HIP(hipStreamSynchronize(ms));
   return merge_readback(g, dm_grid::kRbSync, n, out, cap, n_out);
+}
+
+int dm_merge_max_band_k(const dm_grid* g, int64_t* max_k) {
+  if (int rc0 = not_on_sharded(g, "dm_merge_max_band_k")) return rc0;
+  int rc = check_grid(g);
+  if (rc) return rc;
+  if (!max_k) return dm_set_error(DM_ERR_INVALID_ARG, "max_k is NULL");
+  *max_k = (int64_t)g->h_mcnt[3];  // the header merge_readback copied (M_MAXK)
+  return DM_OK;
 }
 
 int dm_frontiers_begin(dm_grid* g) {

@@ -1185,7 +1185,7 @@ __global__ __launch_bounds__(256) void k_frontier_compact(FGeom g, const int32_t
 __device__ inline void write_rb_header(int64_t K, int64_t cap, unsigned long long* sorted,
                                        const unsigned long long* __restrict__ cnt, int ncnt,
                                        int sorted_idx, const unsigned long long* __restrict__ fsh,
-                                       dm_cluster* host_out) {
+                                       dm_raw_record* host_out) {
   const int tid = threadIdx.x;
   if (tid == 0) *sorted = K <= cap ? 1ull : 0ull;
   if (!host_out) return;
@@ -1259,7 +1259,7 @@ __device__ inline void fix_raw_records(long long* clusters, const long long* sum
 __device__ inline void put_sorted(double ox, double oy, double res, const long long* clusters,
                                   const long long* sums, const long long* labels,
                                   int64_t i, int64_t rank, dm_cluster* __restrict__ out,
-                                  int32_t* __restrict__ rank_of, dm_cluster* __restrict__ host_out,
+                                  int32_t* __restrict__ rank_of, dm_raw_record* __restrict__ host_out,
                                   int64_t host_cap) {
   dm_cluster c;
   long long lab, sz, sx, sy;
@@ -1268,12 +1268,11 @@ __device__ inline void put_sorted(double ox, double oy, double res, const long l
   c.size = sz;
   c.sum_x = sx;
   c.sum_y = sy;
-  const double mx = (double)c.sum_x / (double)c.size;
-  const double my = (double)c.sum_y / (double)c.size;
-  c.cx_m = ox + (mx + 0.5) * res;
-  c.cy_m = oy + (my + 0.5) * res;
+  c.cx_m = dm_centroid(ox, c.sum_x, c.size, res);
+  c.cy_m = dm_centroid(oy, c.sum_y, c.size, res);
   out[rank] = c;
-  if (host_out && rank < host_cap) host_out[rank] = c;  // mapped host readback
+  // mapped host readback: the 32-byte record (the host adds the centroids)
+  if (host_out && rank < host_cap) host_out[rank] = dm_raw_record{lab, sz, sx, sy};
   if (rank_of) rank_of[i] = (int32_t)rank;
 }
 
@@ -1300,9 +1299,6 @@ __device__ inline void put_sorted(double ox, double oy, double res, const long l
 #define DM_SORT_CHUNK 4096
 #endif
 constexpr int kSortChunk = DM_SORT_CHUNK;
-// clusters (predicted from the last collected pass) from which a band pass's
-// records reach the host by a DMA copy instead of the sort kernel's stores
-constexpr int64_t kDmaReadbackMin = 32768;
 constexpr int kSortThreads = DM_SORT_THREADS;
 constexpr int kSortWaves = kSortThreads / 64;
 constexpr int64_t kRankSortCap = 1 << 16;
@@ -1317,7 +1313,7 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
                                                             const unsigned long long* __restrict__ cnt,
                                                             int ncnt, int sorted_idx,
                                                             const unsigned long long* __restrict__ fsh,
-                                                            dm_cluster* __restrict__ host_out,
+                                                            dm_raw_record* __restrict__ host_out,
                                                             int64_t host_cap) {
   __shared__ long long keys[kSortChunk];
   __shared__ int32_t part[kSortWaves][64];
@@ -1369,248 +1365,12 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_sort(double ox, double oy
   }
 }
 
-// ---- LSD radix sort for many clusters (K > the handle's sort_min, DM_SORT_MIN) ----------------
-// The rank sort is O(K^2): ~0.1 ms at 23k clusters, far more at the 2e5+
-// clusters of a sparse 1 cm map (C5).  Labels are unique row-major cell
-// indices in [base, base + span) (span = rows * W: the band's or the map's
-// label range), so the sort key is label - base, `bits` = ceil(log2 span)
-// wide: ceil(bits / 8) stable counting passes of db = ceil(bits / passes)
-// bits each (C5's 2^32 labels: 4 x 8 bits; C3's 2^28: 4 x 7), each pass
-// (a block's kRxItems keys are loaded into registers in one round, so a
-// pass is a few load latencies, not one per key):
-//   k_rx_hist     per block of kRxItems keys: LDS digit histogram ->
-//                 hist[digit][block] (digit-major, so one linear exclusive
-//                 scan gives every (digit, block) its output offset)
-//   k_rx_scan     one workgroup: that exclusive scan
-//   k_rx_scatter  the block's keys again, in order, 256 per round: rank
-//                 among equal digits by wave ballots (db ballots give each
-//                 lane its peers), across the block's 4 waves by LDS counts,
-//                 across rounds by a running LDS count: a STABLE placement
-// then k_rx_emit writes every record at its sorted position (the same record
-// write + readback header as k_rank_sort).  The round-2 bucket sort (4096
-// label buckets, O(b^2) ranking inside a bucket, same-address atomics per
-// record) took 0.31 ms at C5's 219k clusters: robots cluster their
-// frontiers in a few buckets.  Every kernel reads the device-side count;
-// K > cap leaves the result unsorted (flag 0), as the rank sort does.
-// Exclusive scan of n int32 counts by ONE 1024-thread workgroup, in
-// registers: each round a thread takes 32 consecutive counts (eight 16-byte
-// loads), sums them, and the workgroup scans the 1024 sums with wave scans and
-// a 16-entry LDS table; rounds carry.  (The earlier form staged 32768 counts
-// in 128 KiB of LDS: such a workgroup waits for a CU with its LDS free, which
-// on a busy chip -- the next batch's kernels beside the pass -- took 95-250 us
-// for C5's 65536 rows.)  in == out is allowed; zero_in also zeroes the input.
-constexpr int kScanThreads = 1024;
-constexpr int kScanPer = 32;
-__device__ inline void block_exclusive_scan(int32_t* in, int32_t* out, int64_t n, bool zero_in,
-                                            int32_t* total_out) {
-  __shared__ int32_t wsum[kScanThreads / 64];
-  const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
-  int32_t carry = 0;
-  for (int64_t c0 = 0; c0 < n; c0 += (int64_t)kScanThreads * kScanPer) {
-    const int64_t b = c0 + (int64_t)tid * kScanPer;
-    int32_t v[kScanPer];
-    if (b + kScanPer <= n) {
-#pragma unroll
-      for (int q = 0; q < kScanPer / 4; ++q) {
-        const int4 t = reinterpret_cast<const int4*>(in + b)[q];
-        v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
-      }
-      if (zero_in) {
-#pragma unroll
-        for (int q = 0; q < kScanPer / 4; ++q) reinterpret_cast<int4*>(in + b)[q] = make_int4(0, 0, 0, 0);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < kScanPer; ++i) {
-        v[i] = b + i < n ? in[b + i] : 0;
-        if (zero_in && b + i < n) in[b + i] = 0;
-      }
-    }
-    int32_t seg = 0;
-#pragma unroll
-    for (int i = 0; i < kScanPer; ++i) seg += v[i];
-    int32_t incl = seg;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int32_t t = __shfl_up(incl, d);
-      if (lane >= d) incl += t;
-    }
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    int32_t run = carry + incl - seg, total = 0;
-#pragma unroll
-    for (int q = 0; q < kScanThreads / 64; ++q) {
-      const int32_t ws = wsum[q];
-      run += q < w ? ws : 0;
-      total += ws;
-    }
-    if (b + kScanPer <= n) {
-#pragma unroll
-      for (int q = 0; q < kScanPer / 4; ++q) {
-        int4 t;
-        t.x = run; run += v[4 * q];
-        t.y = run; run += v[4 * q + 1];
-        t.z = run; run += v[4 * q + 2];
-        t.w = run; run += v[4 * q + 3];
-        reinterpret_cast<int4*>(out + b)[q] = t;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < kScanPer; ++i) {
-        if (b + i < n) out[b + i] = run;
-        run += v[i];
-      }
-    }
-    carry += total;
-    __syncthreads();  // wsum is rewritten next round
-  }
-  if (total_out && tid == 0) *total_out = carry;
-}
-
-constexpr int kRxThreads = 256;
-constexpr int kRxRounds = 8;                      // keys per thread, all loaded up front
-constexpr int kRxItems = kRxThreads * kRxRounds;  // keys per block
-constexpr int kRxMaxRadix = 2048;  // digits of up to 11 bits (DM_RX_BITS)
-
-__global__ __launch_bounds__(kRxThreads) void k_rx_init(const long long* __restrict__ clusters,
-                                                        const long long* __restrict__ labels,
-                                                        const unsigned long long* __restrict__ count, int64_t cap,
-                                                        long long base, unsigned long long* __restrict__ keys,
-                                                        int32_t* __restrict__ vals) {
-  const int64_t K = (int64_t)*count;
-  if (K > cap) return;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < K; i += (int64_t)gridDim.x * blockDim.x) {
-    keys[i] = (unsigned long long)(record_key(clusters, labels, i) - base);
-    vals[i] = (int32_t)i;
-  }
-}
-
-// Block blk's keys, thread t's q-th key = blk * kRxItems + q * kRxThreads + t
-// (coalesced; this order is also the stable order the scatter keeps).
-__global__ __launch_bounds__(kRxThreads) void k_rx_hist(const unsigned long long* __restrict__ count, int64_t cap,
-                                                        const unsigned long long* __restrict__ keys, int shift,
-                                                        int db, int32_t* __restrict__ hist) {
-  __shared__ int32_t h[kRxMaxRadix];
-  const int64_t K = (int64_t)*count;
-  if (K > cap) return;
-  const int64_t nblk = (K + kRxItems - 1) / kRxItems;
-  const int R = 1 << db;
-  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-    unsigned long long k[kRxRounds];
-    const int64_t i0 = blk * kRxItems + threadIdx.x;
-#pragma unroll
-    for (int q = 0; q < kRxRounds; ++q) k[q] = i0 + q * kRxThreads < K ? keys[i0 + q * kRxThreads] : ~0ull;
-    for (int d = threadIdx.x; d < R; d += kRxThreads) h[d] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < kRxRounds; ++q)
-      if (i0 + q * kRxThreads < K) atomicAdd(&h[(int)((k[q] >> shift) & (unsigned long long)(R - 1))], 1);
-    __syncthreads();
-    for (int d = threadIdx.x; d < R; d += kRxThreads) hist[(int64_t)d * nblk + blk] = h[d];
-    __syncthreads();
-  }
-}
-
-// Exclusive scan of hist[0, R * nblk) in place, one workgroup
-// (block_exclusive_scan: registers, no large LDS footprint).
-__global__ __launch_bounds__(kScanThreads) void k_rx_scan(const unsigned long long* __restrict__ count,
-                                                         int64_t cap, int db, int32_t* __restrict__ hist) {
-  const int64_t K = (int64_t)*count;
-  if (K > cap) return;
-  const int64_t nblk = (K + kRxItems - 1) / kRxItems;
-  block_exclusive_scan(hist, hist, ((int64_t)1 << db) * nblk, false, nullptr);
-}
-
-__global__ __launch_bounds__(kRxThreads) void k_rx_scatter(const unsigned long long* __restrict__ count, int64_t cap,
-                                                           const unsigned long long* __restrict__ keys_in,
-                                                           const int32_t* __restrict__ vals_in, int shift, int db,
-                                                           const int32_t* __restrict__ hist,
-                                                           unsigned long long* __restrict__ keys_out,
-                                                           int32_t* __restrict__ vals_out) {
-  __shared__ int32_t off[kRxMaxRadix];                    // the block's output offset per digit, advancing
-  __shared__ int32_t wcnt[kRxThreads / 64][kRxMaxRadix];  // this round's count per (wave, digit)
-  const int64_t K = (int64_t)*count;
-  if (K > cap) return;
-  const int64_t nblk = (K + kRxItems - 1) / kRxItems;
-  const int R = 1 << db;
-  const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-    // every key and value of the block in registers first: one load round
-    unsigned long long k[kRxRounds];
-    int32_t v[kRxRounds];
-    const int64_t i0 = blk * kRxItems + tid;
-#pragma unroll
-    for (int q = 0; q < kRxRounds; ++q) {
-      const bool ok = i0 + q * kRxThreads < K;
-      k[q] = ok ? keys_in[i0 + q * kRxThreads] : 0ull;
-      v[q] = ok ? vals_in[i0 + q * kRxThreads] : 0;
-    }
-    for (int d = tid; d < R; d += kRxThreads) {
-      off[d] = hist[(int64_t)d * nblk + blk];
-#pragma unroll
-      for (int q = 0; q < kRxThreads / 64; ++q) wcnt[q][d] = 0;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < kRxRounds; ++r) {
-      const bool ok = i0 + r * kRxThreads < K;
-      const int dg = (int)((k[r] >> shift) & (unsigned long long)(R - 1));
-      // lanes of this wave holding the same digit (valid lanes only)
-      unsigned long long peers = __ballot(ok);
-      for (int b = 0; b < db; ++b) {
-        const unsigned long long m = __ballot((dg >> b) & 1);
-        peers &= ((dg >> b) & 1) ? m : ~m;
-      }
-      const int wrank = __popcll(peers & lt);
-      if (ok && wrank == 0) wcnt[w][dg] = __popcll(peers);
-      __syncthreads();
-      if (ok) {
-        int before = 0;
-        for (int q = 0; q < w; ++q) before += wcnt[q][dg];
-        const int64_t pos = (int64_t)off[dg] + before + wrank;
-        keys_out[pos] = k[r];
-        vals_out[pos] = v[r];
-      }
-      __syncthreads();
-      for (int d = tid; d < R; d += kRxThreads) {
-        int t = 0;
-#pragma unroll
-        for (int q = 0; q < kRxThreads / 64; ++q) {
-          t += wcnt[q][d];
-          wcnt[q][d] = 0;
-        }
-        off[d] += t;
-      }
-      __syncthreads();
-    }
-  }
-}
-
-__global__ __launch_bounds__(kRxThreads) void k_rx_emit(double ox, double oy, double res, long long* clusters,
-                                                        const long long* sums, const long long* labels,
-                                                        const unsigned long long* __restrict__ count, int64_t cap,
-                                                        const int32_t* __restrict__ vals, dm_cluster* __restrict__ out,
-                                                        int32_t* __restrict__ rank_of, unsigned long long* sorted,
-                                                        const unsigned long long* __restrict__ cnt, int ncnt,
-                                                        int sorted_idx, const unsigned long long* __restrict__ fsh,
-                                                        dm_cluster* __restrict__ host_out, int64_t host_cap) {
-  const int64_t K = (int64_t)*count;
-  if (blockIdx.x == 0) write_rb_header(K, cap, sorted, cnt, ncnt, sorted_idx, fsh, host_out);
-  if (K > cap) {
-    fix_raw_records(clusters, sums, labels, K);
-    return;
-  }
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < K; p += (int64_t)gridDim.x * blockDim.x)
-    put_sorted(ox, oy, res, clusters, sums, labels, vals[p], p, out, rank_of, host_out, host_cap);
-}
-
 // ---- row-bucket sort for many clusters (the default for K > sort_min) --------------------------
 // A label is the row-major index y * W + x of a component's first cell, so
 // label order is (row, column) order: one counting pass by row puts every
 // record in its row's range, and a record's place inside that range is the
 // number of records of the same row with a smaller column.  Four kernels
-// whatever the key width (the radix sort above needs 1 + 3 * passes + 1):
+// whatever the key width:
 //   k_rs_count  per record: key = label - base, row = key / W, slot = its
 //               arrival in the row (atomic on the row's counter)
 //   k_rs_scan   exclusive scan of the row counts -> row offsets (rows + 1
@@ -1632,8 +1392,8 @@ __global__ __launch_bounds__(256) void k_rs_count(const long long* __restrict__ 
                                                   unsigned long long* status, int n_status) {
   const int64_t K = (int64_t)*count;
   if (K > cap) return;
-  if (blockIdx.x == 0)  // k_rs_scan's published-total words, for this sort
-    for (int e = threadIdx.x; e < n_status; e += blockDim.x) status[e] = 0ull;
+  if (blockIdx.x == 0)  // k_rs_scan's published-total words and its failure word, for this sort
+    for (int e = threadIdx.x; e <= n_status; e += blockDim.x) status[e] = 0ull;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < K; i += (int64_t)gridDim.x * blockDim.x) {
     const unsigned long long key = (unsigned long long)(record_key(clusters, labels, i) - base);
     const int64_t row = (int64_t)(key / (unsigned long long)W);
@@ -1696,7 +1456,9 @@ __global__ __launch_bounds__(256) void k_rs_scan(const unsigned long long* __res
     __hip_atomic_store(&status[blk], (1ull << 63) | (unsigned long long)(uint32_t)total, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   // the earlier workgroups' totals (bounded polls: they were dispatched
-  // before this one, so they publish)
+  // before this one, so they publish).  A poll that gives up marks the sort
+  // failed (status[gridDim.x]): k_rs_rank then reports the records unsorted
+  // and the host sorts them, instead of placing them by wrong offsets
   long long pre = 0;
   for (int64_t e = tid; e < blk; e += 256) {
     unsigned long long sv = 0ull;
@@ -1705,6 +1467,8 @@ __global__ __launch_bounds__(256) void k_rs_scan(const unsigned long long* __res
       if (sv >> 63) break;
       __builtin_amdgcn_s_sleep(1);
     }
+    if (!(sv >> 63))
+      __hip_atomic_store(&status[gridDim.x], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     pre += (long long)(sv & 0xFFFFFFFFull);
   }
   for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
@@ -1758,8 +1522,12 @@ __global__ __launch_bounds__(256) void k_rs_rank(double ox, double oy, double re
                                                  dm_cluster* __restrict__ out, int32_t* __restrict__ rank_of,
                                                  unsigned long long* sorted, const unsigned long long* __restrict__ cnt,
                                                  int ncnt, int sorted_idx, const unsigned long long* __restrict__ fsh,
-                                                 dm_cluster* __restrict__ host_out, int64_t host_cap) {
+                                                 dm_raw_record* __restrict__ host_out, int64_t host_cap,
+                                                 const unsigned long long* __restrict__ scan_failed) {
   const int64_t K = (int64_t)*count;
+  // k_rs_scan gave up on a workgroup total: the offsets are wrong, so the
+  // records stay raw and unsorted (the host sorts them), as when K > cap
+  if (*scan_failed) cap = -1;
   if (blockIdx.x == 0) write_rb_header(K, cap, sorted, cnt, ncnt, sorted_idx, fsh, host_out);
   if (K > cap) {
     fix_raw_records(clusters, sums, labels, K);
@@ -1801,8 +1569,6 @@ int grid_for(int64_t n, int threads, int64_t cap) {
 
 static_assert(sizeof(FGeom) == 88, "FGeom has no implicit padding");
 
-int64_t dm_rx_items() { return kRxItems; }
-
 static FGeom make_fgeom(const dm_grid* g, bool want_mask, bool want_labels) {
   FGeom fg;
   fg.W = (int32_t)g->W;
@@ -1839,7 +1605,7 @@ int dm_launch_rank_sort(hipStream_t stream, long long* clusters, const long long
                         const long long* labels, const unsigned long long* d_count,
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
                         int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
-                        int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
+                        int ncnt, int sorted_idx, const unsigned long long* fsh, dm_raw_record* host_out,
                         int64_t host_cap, int64_t expect) {
   const int64_t cap = std::min<int64_t>(max_records, kRankSortCap);
   // one workgroup per 64 expected records (twice the last pass's count, at
@@ -1856,66 +1622,30 @@ int dm_launch_bucket_sort(dm_grid* g, hipStream_t stream, long long* clusters, c
                           const long long* labels, const unsigned long long* d_count,
                           int64_t max_records, int64_t row_base, int64_t rows, dm_cluster* out,
                           int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
-                          int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
+                          int ncnt, int sorted_idx, const unsigned long long* fsh, dm_raw_record* host_out,
                           int64_t host_cap) {
-  if (max_records > g->bs_cap)
-    return dm_set_error(DM_ERR_INVALID_ARG, "radix sort: %lld records exceed its workspace",
-                        (long long)max_records);
-  // key = label - base over [0, span)
+  if (max_records > g->bs_cap || rows > g->rs_rows)
+    return dm_set_error(DM_ERR_INVALID_ARG, "row sort: %lld records over %lld rows exceed its workspace",
+                        (long long)max_records, (long long)rows);
+  // key = label - base over [0, rows * W)
   const long long base = row_base * g->W;
-  if (g->row_sort && rows <= g->rs_rows) {
-    // grids follow the expected count (the kernels stride; blocks past the
-    // device-side count return)
-    const int64_t expect = std::min<int64_t>(max_records, std::max<int64_t>(2 * g->sort_hint, 4096));
-    const int eg = grid_for(expect, 256, 4096);
-    const int nsb = (int)((rows + kRsChunk - 1) / kRsChunk);
-    DM_LAUNCH(k_rs_count, dim3(eg), dim3(256), 0, stream, clusters, labels, d_count, max_records, base, g->W,
-              g->rs_cnt, g->bs_key, g->bs_idx2, g->rs_status, nsb);
-    DM_HIP(hipGetLastError());
-    DM_LAUNCH(k_rs_scan, dim3(nsb), dim3(256), 0, stream, d_count, max_records, rows, g->rs_cnt, g->rs_off,
-              g->rs_status);
-    DM_HIP(hipGetLastError());
-    DM_LAUNCH(k_rs_place, dim3(eg), dim3(256), 0, stream, d_count, max_records, g->W, g->bs_key, g->bs_idx2,
-              g->rs_off, g->bs_key2, g->bs_idx);
-    DM_HIP(hipGetLastError());
-    DM_LAUNCH(k_rs_rank, dim3(eg), dim3(256), 0, stream, g->p.origin_x, g->p.origin_y, g->p.resolution, clusters,
-              sums, labels, d_count, max_records, g->W, g->bs_key2, g->bs_idx, g->rs_off, out, rank_of, d_sorted, cnt,
-              ncnt, sorted_idx, fsh, host_out, host_cap);
-    DM_HIP(hipGetLastError());
-    return DM_OK;
-  }
-  const unsigned long long span = (unsigned long long)rows * (unsigned long long)g->W;
-  int bits = 1;
-  while (bits < 64 && (span - 1) >> bits) ++bits;
-  const int passes = (bits + g->rx_bits - 1) / g->rx_bits;
-  const int db = (bits + passes - 1) / passes;
   // grids follow the expected count (the kernels stride; blocks past the
   // device-side count return)
-  const int64_t expect = std::min<int64_t>(max_records, std::max<int64_t>(2 * g->sort_hint, kRxItems));
-  const int eg = grid_for(expect, kRxThreads, 4096);
-  const int bg = grid_for(expect, kRxItems, 4096);
-  unsigned long long* ka = g->bs_key;
-  unsigned long long* kb = g->bs_key2;
-  int32_t* va = g->bs_idx;
-  int32_t* vb = g->bs_idx2;
-  DM_LAUNCH(k_rx_init, dim3(eg), dim3(kRxThreads), 0, stream, clusters, labels, d_count, max_records, base, ka, va);
+  const int64_t expect = std::min<int64_t>(max_records, std::max<int64_t>(2 * g->sort_hint, 4096));
+  const int eg = grid_for(expect, 256, 4096);
+  const int nsb = (int)((rows + kRsChunk - 1) / kRsChunk);
+  DM_LAUNCH(k_rs_count, dim3(eg), dim3(256), 0, stream, clusters, labels, d_count, max_records, base, g->W,
+            g->rs_cnt, g->bs_key, g->bs_idx2, g->rs_status, nsb);
   DM_HIP(hipGetLastError());
-  for (int p = 0; p < passes; ++p) {
-    const int shift = p * db;
-    const int dbp = std::min(db, bits - shift);
-    DM_LAUNCH(k_rx_hist, dim3(bg), dim3(kRxThreads), 0, stream, d_count, max_records, ka, shift, dbp, g->bs_hist);
-    DM_HIP(hipGetLastError());
-    DM_LAUNCH(k_rx_scan, dim3(1), dim3(kScanThreads), 0, stream, d_count, max_records, dbp, g->bs_hist);
-    DM_HIP(hipGetLastError());
-    DM_LAUNCH(k_rx_scatter, dim3(bg), dim3(kRxThreads), 0, stream, d_count, max_records, ka, va, shift, dbp,
-              g->bs_hist, kb, vb);
-    DM_HIP(hipGetLastError());
-    std::swap(ka, kb);
-    std::swap(va, vb);
-  }
-  DM_LAUNCH(k_rx_emit, dim3(eg), dim3(kRxThreads), 0, stream, g->p.origin_x, g->p.origin_y, g->p.resolution,
-            clusters, sums, labels, d_count, max_records, va, out, rank_of, d_sorted, cnt, ncnt, sorted_idx, fsh,
-            host_out, host_cap);
+  DM_LAUNCH(k_rs_scan, dim3(nsb), dim3(256), 0, stream, d_count, max_records, rows, g->rs_cnt, g->rs_off,
+            g->rs_status);
+  DM_HIP(hipGetLastError());
+  DM_LAUNCH(k_rs_place, dim3(eg), dim3(256), 0, stream, d_count, max_records, g->W, g->bs_key, g->bs_idx2,
+            g->rs_off, g->bs_key2, g->bs_idx);
+  DM_HIP(hipGetLastError());
+  DM_LAUNCH(k_rs_rank, dim3(eg), dim3(256), 0, stream, g->p.origin_x, g->p.origin_y, g->p.resolution, clusters,
+            sums, labels, d_count, max_records, g->W, g->bs_key2, g->bs_idx, g->rs_off, out, rank_of, d_sorted, cnt,
+            ncnt, sorted_idx, fsh, host_out, host_cap, g->rs_status + nsb);
   DM_HIP(hipGetLastError());
   return DM_OK;
 }
@@ -1926,8 +1656,6 @@ int dm_launch_bucket_sort(dm_grid* g, hipStream_t stream, long long* clusters, c
 int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool split, hipStream_t* end_stream) {
   const FGeom fg = make_fgeom(g, want_mask, want_labels);
   const int64_t cells = g->R * g->W;
-  // the kernels below go out as one graph per stream (dm_batch.h)
-  DmBatchScope batch(&g->batch, !g->profile);
   // the prep and the bit rows run on g->stream after everything shared with
   // the pass stream (labelling of earlier passes) -- except for split passes,
   // which keep that order on the pass stream itself
@@ -1953,12 +1681,11 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
                      g->bits_flag + kStampWord, prep_iters);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
-  if (want_mask || want_labels) DM_HIP(dm_batch_flush_all());
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));
   // one wave per listed tile; the grid follows the last collected pass's
-  // list length (+25 %; the kernels grid-stride, so any count is covered)
-  // (quantised: the grid is part of the cached graph's key, dm_batch.h)
+  // list length (+25 %, quantised; the kernels grid-stride, so any count is
+  // covered)
   const int64_t want_waves = g->ftile_hint > 0 ? dm_quantize_up(g->ftile_hint + g->ftile_hint / 4 + 64) : g->NT;
   const int wave_grid = grid_for(std::min<int64_t>(want_waves, g->NT), kFW, 8192);
   // fmask while the passes list many tiles (dm_internal.h, fmask_on); a
@@ -1999,21 +1726,14 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   hipStream_t ps = g->stream;
   if (split) {
     ps = g->pass_stream;
-    DM_HIP(dm_batch_flush_all());
     hipEvent_t eb = g->ev_bits[g->fparity];
     DM_HIP(hipEventRecord(eb, g->stream));
     // the integrate workspaces are free once the grid stream is past the
-    // accumulations (both hand-off forms: a timed-out gate below must not
-    // free them early).  (Re-recorded two passes later: a front-end waiting
-    // on it then waits longer than needed, never too little -- every record
-    // follows the accumulations it frees in stream order.)
+    // accumulations.  (Re-recorded two passes later: a front-end waiting on it
+    // then waits longer than needed, never too little -- every record follows
+    // the accumulations it frees in stream order.)
     DM_HIP(dm_mark_ws_free(g, eb));
-    if (g->pass_gate) {
-      if (int rc = dm_launch_signal(g->stream, g->bits_flag)) return rc;
-      if (int rc = dm_launch_gate(ps, g->bits_flag, g->cnt + CNT_OVERFLOW, kOvGate)) return rc;
-    } else {
-      DM_HIP(hipStreamWaitEvent(ps, eb, 0));
-    }
+    DM_HIP(hipStreamWaitEvent(ps, eb, 0));
   }
   if (end_stream) *end_stream = ps;
   if (!dense) {
@@ -2024,23 +1744,15 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
     // the grid follows the last pass's count (the kernel grid-strides)
     const int big_grid =
         grid_for(std::min<int64_t>(g->NT, dm_quantize_up(g->big_hint + g->big_hint / 4 + 64)), 1, 8192);
-    auto launch_big = [&](hipStream_t bs) -> int {
-      dm_timer_begin(g, "frontier_big", &t, bs);
-      DM_LAUNCH(k_frontier_tile_big, dim3(big_grid), dim3(kFT), 0, bs, fg, g->fbits, g->big_tiles,
-                g->ftiles, list_n, g->border, g->rel, g->slot_label, g->slot_parent, g->slot_own,
-                g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh, 0);
-      dm_timer_end(g, &t);
-      DM_HIP(hipGetLastError());
-      return DM_OK;
-    };
-    if (g->big_concurrent) {
-      DM_HIP(dm_batch_flush_all());
-      DM_HIP(hipEventRecord(g->ev_bigfork, ps));
-      DM_HIP(hipStreamWaitEvent(g->big_stream, g->ev_bigfork, 0));
-      if (int rc = launch_big(g->big_stream)) return rc;
-      DM_HIP(dm_batch_flush_all());
-      DM_HIP(hipEventRecord(g->ev_big, g->big_stream));
-    }
+    DM_HIP(hipEventRecord(g->ev_bigfork, ps));
+    DM_HIP(hipStreamWaitEvent(g->big_stream, g->ev_bigfork, 0));
+    dm_timer_begin(g, "frontier_big", &t, g->big_stream);
+    DM_LAUNCH(k_frontier_tile_big, dim3(big_grid), dim3(kFT), 0, g->big_stream, fg, g->fbits, g->big_tiles,
+              g->ftiles, list_n, g->border, g->rel, g->slot_label, g->slot_parent, g->slot_own,
+              g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh, 0);
+    dm_timer_end(g, &t);
+    DM_HIP(hipGetLastError());
+    DM_HIP(hipEventRecord(g->ev_big, g->big_stream));
     dm_timer_begin(g, "frontier_tile", &t, ps);
     DM_LAUNCH(k_frontier_tile, dim3(wave_grid), dim3(kFW * 64), 0, ps, fg, g->fbits,
                        g->ftiles, list_n, g->border, g->rel,
@@ -2048,12 +1760,7 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
                        g->edge_slot, g->cnt, g->fsh, g->big_tiles);
     dm_timer_end(g, &t);
     DM_HIP(hipGetLastError());
-    if (g->big_concurrent) {
-      DM_HIP(dm_batch_flush_all());
-      DM_HIP(hipStreamWaitEvent(ps, g->ev_big, 0));
-    } else if (int rc = launch_big(ps)) {
-      return rc;
-    }
+    DM_HIP(hipStreamWaitEvent(ps, g->ev_big, 0));
   } else {
     dm_timer_begin(g, "frontier_tile", &t, ps);
     // one workgroup per listed tile of the last collected pass (+25 %; the
@@ -2091,34 +1798,18 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   }
   dm_timer_begin(g, "sort_clusters", &t, ps);
   // the last collected pass predicts this one's cluster count (either sort
-  // is exact for any count; only their speed differs).  With
-  // DM_DMA_READBACK=1 and many records (C5's 2e5+) the sort kernel writes
-  // only the readback header into mapped host memory and the records go over
-  // PCIe by a DMA copy after it (A/B: the kernels are 5x shorter, but the
-  // pass ends later than with the kernel's own stores, which overlap it)
-  const bool dma = g->dma_readback && g->sort_hint > g->sort_min && g->sort_hint >= kDmaReadbackMin;
-  const int64_t kcap = dma ? 0 : g->h_out_cap;
+  // is exact for any count; only their speed differs)
   const int rc = g->sort_hint > g->sort_min
       ? dm_launch_bucket_sort(g, ps, g->clusters, fuse ? g->slot_acc : nullptr, fuse ? g->slot_label : nullptr,
                               g->cnt + CNT_CLUSTERS, g->slot_cap, g->row0, g->R, g->out_clu,
                               g->rank_of, g->cnt + CNT_SORTED, g->cnt, CNT_N, CNT_SORTED, g->fsh,
-                              g->h_out_dev, kcap)
+                              g->h_out_dev, g->h_out_cap)
       : dm_launch_rank_sort(ps, g->clusters, fuse ? g->slot_acc : nullptr, fuse ? g->slot_label : nullptr,
                             g->cnt + CNT_CLUSTERS, g->slot_cap, g->p.origin_x,
                             g->p.origin_y, g->p.resolution, g->out_clu, g->rank_of, g->cnt + CNT_SORTED,
-                            g->cnt, CNT_N, CNT_SORTED, g->fsh, g->h_out_dev, kcap, g->sort_hint);
+                            g->cnt, CNT_N, CNT_SORTED, g->fsh, g->h_out_dev, g->h_out_cap, g->sort_hint);
   dm_timer_end(g, &t);
-  if (rc) return rc;
-  g->rb[g->cur_slot].dma_copied = -1;
-  if (dma) {
-    // the predicted count and a margin (the host copies any remainder)
-    const int64_t ncopy = std::min<int64_t>(g->h_out_cap, g->sort_hint + g->sort_hint / 4 + 64);
-    DM_HIP(dm_batch_flush_all());
-    DM_HIP(hipMemcpyAsync(g->h_out, g->out_clu, sizeof(dm_cluster) * (size_t)ncopy, hipMemcpyDeviceToHost, ps));
-    g->rb[g->cur_slot].dma_copied = ncopy;
-  }
-  DM_HIP(batch.finish());
-  return DM_OK;
+  return rc;
 }
 
 // After a frontier pass completed: the counters plus a speculative first
@@ -2129,8 +1820,7 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
 int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied) {
   const unsigned long long* hdr = dm_rb_header(g->h_out);
   memcpy(g->h_cnt, hdr, sizeof(unsigned long long) * CNT_N);
-  const int64_t dc = g->rb[g->cur_slot].dma_copied;
-  *copied = std::min<int64_t>(dc >= 0 ? dc : g->h_out_cap, std::min<int64_t>(g->h_out_cap, g->slot_cap));
+  *copied = std::min<int64_t>(g->h_out_cap, g->slot_cap);
   const unsigned long long most = hdr[CNT_N];
   if (g->h_cnt[CNT_OVERFLOW] & kOvPipeline)
     return dm_set_error(DM_ERR_PIPELINE, "the overlapped pipeline's front-end hand-off timed out: a map "
@@ -2142,9 +1832,6 @@ int dm_frontiers_readback(dm_grid* g, int64_t* n_clusters, int64_t* copied) {
   if (g->h_cnt[CNT_OVERFLOW] & kOvUnionFind)
     return dm_set_error(DM_ERR_INCOMPLETE, "frontier union-find did not converge within its bound "
                                            "(dm_uf.h): this pass has no result");
-  if (g->h_cnt[CNT_OVERFLOW] & kOvGate)
-    return dm_set_error(DM_ERR_INCOMPLETE, "frontier pass: the bit-row hand-off to the pass stream "
-                                           "timed out: this pass has no result");
   *n_clusters = (int64_t)g->h_cnt[CNT_CLUSTERS];
   g->sort_hint = *n_clusters;
   // this pass's tile-list length (the other parity's counter is 0 or smaller)

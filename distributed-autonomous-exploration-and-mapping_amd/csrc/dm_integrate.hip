@@ -29,6 +29,7 @@
 #include <algorithm>
 
 DM_PH_DECL(integrate)
+DM_TL_DECL(accum)
 
 namespace {
 
@@ -43,7 +44,6 @@ struct Geom {
   int32_t chunks, chunk_len;  // each beam enumerated as `chunks` k-ranges (dm_integrate_chunks)
   int32_t sparse_pieces;  // light tiles with at most this many pieces are sparse items
   int32_t pad;
-  int64_t stage_blk;  // staged pieces per k_beam_prep workgroup (0: not staged, k_scatter places them)
 };
 
 // Thread v of k_beam_prep / k_scatter: beam v % nb, k-range v / nb (chunk-
@@ -150,39 +150,19 @@ __device__ inline PackedPiece make_piece(const Geom& g, const Beam& bm, int32_t 
   return dm_pack_piece(dm_tile_piece(bm, k0, k1, g.r.row0, tx0, ty0, kLdsPitch));
 }
 
-// stage_sr code of a piece counted straight into tile_count (its tile found
-// no slot in the workgroup's LDS table): k_gather bumps the tile's cursor
-constexpr uint32_t kStageGlobal = 0x80000000u;
-
-__device__ inline PackedPiece no_stage_piece() {
-  PackedPiece q;
-  q.x = 0u; q.y = 0u; q.z = 0u; q.w = 1u;
-  return q;
-}
-
-// Staged mode (kStaged, the default): every piece is also packed and stored
-// in this workgroup's region of `stage`, in enumeration order, with its
-// workgroup histogram slot (or kStageGlobal | tile); k_gather moves it into
-// its tile's bin after k_plan, so the beams are enumerated once per call
-// instead of twice (k_beam_prep, then k_scatter).  A piece's place inside
-// its bin is arbitrary (counts are integers: order-free), so k_gather ranks
-// the pieces of a slot itself.  Emission index: one LDS bump per wave per
-// emitting step, issued before the histogram's so the two latencies overlap.
-template <bool kStaged>
 __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const double* __restrict__ pose4,
                                                    const float* __restrict__ ranges,
                                                    const double* __restrict__ trig,
                                                    Beam* __restrict__ beams, int32_t* tile_count,
                                                    int32_t* act_raw, unsigned long long* ish,
                                                    int2* __restrict__ blk_hist, int32_t* __restrict__ blk_n,
-                                                   PackedPiece* __restrict__ stage, uint32_t* __restrict__ stage_sr,
-                                                   int32_t* __restrict__ blk_np, unsigned long long* cnt) {
+                                                   unsigned long long* cnt) {
   __shared__ int32_t hkey[kHash];
   __shared__ int32_t hcnt[kHash];
-  __shared__ int32_t s_nh, s_np;
+  __shared__ int32_t s_nh;
   const int tid = threadIdx.x;
   for (int e = tid; e < kHash; e += 256) { hkey[e] = -1; hcnt[e] = 0; }
-  if (tid == 0) { s_nh = 0; s_np = 0; }
+  if (tid == 0) s_nh = 0;
   __syncthreads();
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + tid;
   if (v < g.nb * g.chunks) {
@@ -191,44 +171,23 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
     const Beam bm = dm_make_beam(a, pose4, ranges, trig, s, i);
     if (bc.k_lo == 0) beams[bc.b] = bm;
     if ((bm.flags & 1) && bc.k_lo <= bm.n) {
-      dm_for_each_piece(bm, g.r, [&](int32_t tile, int32_t k0, int32_t k1) {
-        int32_t e0 = 0;
-        unsigned long long act = 0ull;
-        int lead = 0;
-        if (kStaged) {  // this wave's emitting lanes take consecutive staging entries
-          act = __ballot(1);
-          lead = __ffsll(act) - 1;
-          if (lane_id() == lead) e0 = atomicAdd(&s_np, __popcll(act));
-        }
+      dm_for_each_piece(bm, g.r, [&](int32_t tile, int32_t, int32_t) {
         const LaneRun run = lane_run(tile);
-        uint32_t sr = 0u;
         if (run.head) {
           const int h = hash_insert(hkey, tile);
           if (h >= 0) {
             atomicAdd(&hcnt[h], run.len);
-            sr = (uint32_t)h;
           } else {
             const int32_t old = atomicAdd(&tile_count[tile], run.len);
             first_touch(g, tile, old, act_raw, ish, cnt);
-            sr = kStageGlobal | (uint32_t)tile;
-          }
-        }
-        if (kStaged) {
-          sr = __shfl(sr, run.head_lane);
-          const int64_t e = (int64_t)__shfl(e0, lead) + __popcll(act & ((1ull << lane_id()) - 1ull));
-          if (e < g.stage_blk) {
-            const int64_t at = (int64_t)blockIdx.x * g.stage_blk + e;
-            stage[at] = make_piece(g, bm, tile, k0, k1);
-            stage_sr[at] = sr;
           }
         }
       }, bc.k_lo, bc.k_hi);
     }
   }
   __syncthreads();
-  // flush the histogram, and keep it (compacted, with each entry's hash slot)
-  // for k_gather / k_scatter: their single placement pass then needs no
-  // counting pass of its own
+  // flush the histogram, and keep it (compacted) for k_scatter: its single
+  // placement pass then needs no counting pass of its own
   int2* my_hist = blk_hist + (int64_t)blockIdx.x * kHash;
   for (int e = tid; e < kHash; e += 256) {
     const int32_t tile = hkey[e];
@@ -238,13 +197,7 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
     my_hist[atomicAdd(&s_nh, 1)] = make_int2(tile, hcnt[e] | (e << 16));
   }
   __syncthreads();
-  if (tid == 0) {
-    blk_n[blockIdx.x] = s_nh;
-    if (kStaged) {
-      blk_np[blockIdx.x] = s_np;
-      if ((int64_t)s_np > g.stage_blk) atomicOr(&cnt[CNT_IOVERFLOW], 2ull);  // cannot happen (grow_integrate's bound)
-    }
-  }
+  if (tid == 0) blk_n[blockIdx.x] = s_nh;
 }
 
 // Work plan for the apply phase (one block).  A tile's pieces are cut into
@@ -252,7 +205,7 @@ __global__ __launch_bounds__(256) void k_beam_prep(RayArgs a, Geom g, const doub
 // A light tile (<= kChunk pieces) is one item that accumulates AND applies;
 // a heavy tile (around a sensor: up to every beam of a scan starts there) is
 // split into several items on different CUs that merge their counts in a
-// per-tile slab, applied by k_heavy_apply.  Per active tile j with c_j
+// per-tile slab, applied by the tile's last item.  Per active tile j with c_j
 // pieces, exclusive scans of: c_j (bin offsets), heavy items, light items,
 // heavy ordinals.  Heavy items are listed first (they are the long ones).
 // Item = {tile, first piece, pieces, slab code or -1 (light / medium)}.
@@ -397,49 +350,6 @@ __device__ inline void put_piece(const Geom& g, PackedPiece* pieces, int64_t idx
     pieces[idx] = make_piece(g, bm, tile, k0, k1);
   } else {
     atomicOr(&cnt[CNT_IOVERFLOW], 2ull);
-  }
-}
-
-// Staged pieces -> per-tile bins (replaces k_scatter's second enumeration):
-// one workgroup per k_beam_prep workgroup; one cursor bump per histogram
-// entry reserves the workgroup's range of each tile's bin (hcur, by hash
-// slot), then every staged piece takes the next place of its slot's range
-// (an LDS cursor: the order inside a bin is free).  Pieces of a tile that
-// found no LDS slot bump the tile's global cursor one by one (rare: the
-// table holds 1024 tiles per 256 beams).  The first round's loads go out
-// before the cursor bumps.
-__global__ __launch_bounds__(256) void k_gather(Geom g, int32_t* tile_cur, const int2* __restrict__ blk_hist,
-                                                const int32_t* __restrict__ blk_n,
-                                                const int32_t* __restrict__ blk_np,
-                                                const PackedPiece* __restrict__ stage,
-                                                const uint32_t* __restrict__ stage_sr,
-                                                PackedPiece* __restrict__ pieces, unsigned long long* cnt) {
-  __shared__ int32_t hcur[kHash];
-  const int tid = threadIdx.x;
-  const int32_t nh = blk_n[blockIdx.x];
-  const int32_t np = (int32_t)min((int64_t)blk_np[blockIdx.x], g.stage_blk);
-  const int64_t sbase = (int64_t)blockIdx.x * g.stage_blk;
-  PackedPiece pc = no_stage_piece();
-  uint32_t sr = 0u;
-  if (tid < np) {
-    pc = stage[sbase + tid];
-    sr = stage_sr[sbase + tid];
-  }
-  const int2* my_hist = blk_hist + (int64_t)blockIdx.x * kHash;
-  for (int e = tid; e < nh; e += 256) {
-    const int2 te = my_hist[e];
-    hcur[te.y >> 16] = atomicAdd(&tile_cur[te.x], te.y & 0xFFFF);
-  }
-  __syncthreads();
-  for (int32_t e = tid; e < np; e += 256) {
-    if (e != tid) {
-      pc = stage[sbase + e];
-      sr = stage_sr[sbase + e];
-    }
-    const int64_t dst = (sr & kStageGlobal) ? (int64_t)atomicAdd(&tile_cur[sr & ~kStageGlobal], 1)
-                                            : (int64_t)atomicAdd(&hcur[sr], 1);
-    if (dst >= 0 && dst < g.seg_cap) pieces[dst] = pc;
-    else atomicOr(&cnt[CNT_IOVERFLOW], 2ull);
   }
 }
 
@@ -837,7 +747,8 @@ __device__ inline void heavy_quarter(const Geom& g, const ApplyArgs& p, int64_t 
 //  * light / medium item (the whole tile): applies the log-odds update to the
 //    tile's cells right away, from L / state loaded before the accumulation;
 //  * heavy item: adds its counts to the tile's slab (row-contiguous global
-//    atomics); k_heavy_apply applies the merged slab.
+//    atomics); the tile's last item to finish (a ticket) applies the merged
+//    slab.
 // The next item's pieces are loaded right after this item's apply, its
 // cells (unconditional loads: a fixed count, so the walk waits for the pieces
 // alone with vmcnt(N)) at the top of its iteration, in flight during its
@@ -852,9 +763,6 @@ __device__ inline void heavy_quarter(const Geom& g, const ApplyArgs& p, int64_t 
 #ifndef DM_EARLY_PIECES
 #define DM_EARLY_PIECES 1
 #endif
-#ifndef DM_TICKET_RELEASE
-#define DM_TICKET_RELEASE 0
-#endif
 constexpr int kAccumPerCu = DM_ACCUM_OCC;  // resident k_tile_accum workgroups per CU (4 waves each)
 __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     Geom g, ApplyArgs p, const int4* __restrict__ list_a, int cnt_a, const int4* __restrict__ list_b,
@@ -866,6 +774,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
   __shared__ int32_t s_T, s_free, s_last;
   __shared__ uint32_t s_U;
   const int tid = threadIdx.x, lane = lane_id();
+  DM_TL_BEGIN();
   // The halt word and the item counts in one round of loads (a workgroup
   // runs about one item at C3, so its first item's dependent loads -- counts,
   // descriptor, pieces -- are on every item's path; the halt check used to
@@ -892,7 +801,10 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
   // a timed-out front-end hand-off (kHaltWord): this call's workspace was
   // never written, so nothing is applied (the host reports DM_ERR_PIPELINE).
   // One exit test on all four loads, so they go out together.
-  if ((hv | idle) != 0ull) return;
+  if ((hv | idle) != 0ull) {
+    DM_TL_END(accum, 0);
+    return;
+  }
   auto item_of = [&](int64_t it) {
     int4 d = it < n_items ? (it < HI ? list_a[it] : list_b[it - HI]) : make_int4(0, 0, 0, -1);
     // an item never reads past the piece array (k_plan keeps p0 + c <= seg_cap)
@@ -925,7 +837,9 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
   if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; s_accT = 0ull; s_accU = 0ull; }
   __syncthreads();
   DM_PH_INIT();
+  [[maybe_unused]] unsigned long long tl_word = 0;  // timeline (phase build): dense items | sparse << 16 | finisher ticks << 32
   for (int64_t it = blockIdx.x; it < n_items; it += G) {
+    tl_word += 1;
     // the descriptor is workgroup-uniform: scalar registers, scalar branches
     const int32_t tile = __builtin_amdgcn_readfirstlane(info.x);
     const int32_t c0 = __builtin_amdgcn_readfirstlane(info.y);
@@ -974,35 +888,31 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
       // address, so the item whose ticket returns n_it - 1 comes after every
       // other item's adds, and its exchanges read their sums.  A release
       // fence here (the L2 write-back of the items' other, plain stores)
-      // measured 42 -> 172 us per call with __threadfence (round 1) and
-      // DM_TICKET_RELEASE=1 builds that form for A/B; DM_HEAVY_SEPARATE=1
-      // (read at dm_create) applies the slabs in a separate k_heavy_apply
-      // launch instead — the kernel boundary orders everything.
-      if (heavy_done) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // measured 42 -> 172 us per call with __threadfence (round 1), and the
+      // release / acquire pair on the ticket 67 vs 45 us (round 3).
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const int32_t n_it = (tile_count[tile] + kChunk - 1) / kChunk;  // k_plan's item count
+        s_last = atomicAdd(&heavy_done[heavy >> 1], 1) == n_it - 1;
+      }
+      __syncthreads();
+      if (s_last) {
+#ifdef DM_PHASE_TIMING
+        const long long tf0 = wall_clock64();
+#endif
+        const int64_t h = heavy >> 1;
+        const bool wide = heavy_list[h] < 0;
+        for (int q = 0; q < 4; ++q)
+          heavy_quarter(g, p, h, q, tile, wide, slabs, L, state, &s_T, &s_free, &s_U);
         __syncthreads();
         if (tid == 0) {
-          const int32_t n_it = (tile_count[tile] + kChunk - 1) / kChunk;  // k_plan's item count
-#if DM_TICKET_RELEASE
-          s_last = __hip_atomic_fetch_add(&heavy_done[heavy >> 1], 1, __ATOMIC_RELEASE,
-                                          __HIP_MEMORY_SCOPE_AGENT) == n_it - 1;
-          if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#else
-          s_last = atomicAdd(&heavy_done[heavy >> 1], 1) == n_it - 1;
+          finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
+          heavy_done[h] = 0;  // ready for the next call
+        }
+#ifdef DM_PHASE_TIMING
+        tl_word += (unsigned long long)(wall_clock64() - tf0) << 32;
 #endif
-        }
-        __syncthreads();
-        if (s_last) {
-          const int64_t h = heavy >> 1;
-          const bool wide = heavy_list[h] < 0;
-          for (int q = 0; q < 4; ++q)
-            heavy_quarter(g, p, h, q, tile, wide, slabs, L, state, &s_T, &s_free, &s_U);
-          __syncthreads();
-          if (tid == 0) {
-            finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
-            heavy_done[h] = 0;  // ready for the next call
-          }
-        }
       }
     } else {
       // light / medium: one piece per thread per round (medium tiles walk
@@ -1081,6 +991,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     int4 d = list_b[(int64_t)g.act_cap - 1 - it];
     d.z = (int64_t)d.y + d.z <= g.seg_cap ? d.z : 0;  // never past the piece array
     const int32_t tile = d.x, c0 = d.y, c = d.z;
+    if (lane == 0 && wv == 0) tl_word += 1ull << 16;
     const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
     const PackedPiece sp = lane < c ? pieces[c0 + lane] : no_piece();
     const int32_t sfree = tile_free[tile];
@@ -1179,43 +1090,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     if (s_accU) atomicAdd(&sh[SH_U], s_accU);
   }
   DM_PH_FLUSH(dm_phase_acc_integrate);
-}
-
-// Heavy tiles: apply the merged slab counts, then clear the slab and the
-// tile's piece count for the next call.  Four workgroups per heavy tile, one
-// per 16-row quarter (a heavy tile is one of a few dozen: the kernel's time is
-// one workgroup's latency chain, which a quarter cuts to 4 cells per thread).
-// Thread tid takes cell (row 4k + tid / 64, column tid % 64) of its quarter:
-// each wave instruction touches 256 contiguous slab bytes, the full-rate shape
-// for the memory-side atomics (lanes strided over rows run many times slower:
-// MI355X_MICROARCH.md §Global atomics), and 256 contiguous bytes of L.
-__global__ __launch_bounds__(kQuarter) void k_heavy_apply(
-    Geom g, ApplyArgs p, const int32_t* __restrict__ heavy_list, int32_t* tile_count, int32_t* tile_free,
-    uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
-    const unsigned long long* __restrict__ cnt, unsigned long long* ish,
-    const unsigned long long* __restrict__ halt) {
-  if (*halt) return;  // as k_tile_accum
-  __shared__ int32_t s_T, s_free;
-  __shared__ uint32_t s_U;
-  const int tid = threadIdx.x;
-  const int64_t nq = 4 * (int64_t)cnt[CNT_HEAVY];
-  DM_PH_INIT();
-  for (int64_t it = blockIdx.x; it < nq; it += gridDim.x) {
-    const int64_t h = it >> 2;
-    const int q = (int)(it & 3);
-    const int32_t hl = __builtin_amdgcn_readfirstlane(heavy_list[h]);
-    const int32_t tile = hl & 0x7FFFFFFF;
-    if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; }
-    __syncthreads();
-    heavy_quarter(g, p, h, q, tile, hl < 0, slabs, L, state, &s_T, &s_free, &s_U);
-    __syncthreads();
-    DM_PH(dm_phase_acc_integrate, 9);
-    if (tid == 0) finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
-    __syncthreads();
-    DM_PH(dm_phase_acc_integrate, 10);
-    DM_PH_COUNT(dm_phase_acc_integrate, 20, q == 0);
-  }
-  DM_PH_FLUSH(dm_phase_acc_integrate);
+  DM_TL_END(accum, tl_word);
 }
 
 // ---- maintenance kernels ----------------------------------------------------
@@ -1406,8 +1281,8 @@ __global__ __launch_bounds__(256) void k_map_image(int64_t R, int64_t W, const i
   }
 }
 
-static_assert(sizeof(Geom) == 80 && sizeof(RayArgs) == 40 && sizeof(ApplyArgs) == 24,
-              "kernel argument structs have no implicit padding (dm_batch.h cache keys)");
+static_assert(sizeof(Geom) == 72 && sizeof(RayArgs) == 40 && sizeof(ApplyArgs) == 24,
+              "kernel argument structs have no implicit padding");
 
 Geom make_geom(const dm_grid* g) {
   Geom ge;
@@ -1425,7 +1300,6 @@ Geom make_geom(const dm_grid* g) {
   ge.chunk_len = 0;
   ge.sparse_pieces = std::min(g->sparse_pieces, kSparseMax);  // byte-packed counts (walk_piece_bytes)
   ge.pad = 0;
-  ge.stage_blk = 0;
   return ge;
 }
 
@@ -1452,16 +1326,14 @@ int grid_for(int64_t n, int threads, int64_t cap = 8192) {
 }  // namespace
 
 DM_PH_READER(integrate)
+DM_TL_READER(accum)
 
 int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                         const float* d_ranges, const double* d_trig) {
   const int64_t nb = (int64_t)S * N;
-  // calls cycle through the workspace sets; this one was last used n_iw
-  // calls ago
-  g->iw_cur = (g->iw_cur + 1) % g->n_iw;
+  // calls alternate between the two workspace sets
+  g->iw_cur = (g->iw_cur + 1) % dm_grid::kIntSets;
   dm_grid::IntWs& w = g->iw[g->iw_cur];
-  // the kernels below go out as one graph per stream (dm_batch.h)
-  DmBatchScope batch(&g->batch, !g->profile);
   // front-end stream: with overlap, its own stream, after the accumulation
   // that last used this set (ev_free), so it runs beside the previous call's
   // accumulation and a frontier pass still in flight on g->stream
@@ -1474,7 +1346,6 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   DM_LAUNCH(k_integrate_reset, dim3(2), dim3(256), 0, fs, w.cnt, w.sh);
   DM_HIP(hipGetLastError());
   if (nb == 0) {
-    DM_HIP(batch.finish());
     if (g->overlap) {  // keep the stream order of the calls
       DM_HIP(hipEventRecord(g->ev_fe, fs));
       DM_HIP(hipStreamWaitEvent(g->stream, g->ev_fe, 0));
@@ -1497,15 +1368,8 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   const int nblk = (int)((nb * ge.chunks + 255) / 256);
   KernelTimer t;
   dm_timer_begin(g, "beam_prep", &t, fs);
-  ge.stage_blk = g->fe_staged ? g->stage_blk : 0;
-  if (ge.stage_blk > 0)
-    DM_LAUNCH(k_beam_prep<true>, dim3(nblk), dim3(256), 0, fs, a, ge, d_pose4, d_ranges,
-              d_trig, g->beams, w.tile_count, g->act_raw, w.sh, g->blk_hist, g->blk_n, g->stage,
-              g->stage_sr, g->blk_np, w.cnt);
-  else
-    DM_LAUNCH(k_beam_prep<false>, dim3(nblk), dim3(256), 0, fs, a, ge, d_pose4, d_ranges,
-              d_trig, g->beams, w.tile_count, g->act_raw, w.sh, g->blk_hist, g->blk_n, g->stage,
-              g->stage_sr, g->blk_np, w.cnt);
+  DM_LAUNCH(k_beam_prep, dim3(nblk), dim3(256), 0, fs, a, ge, d_pose4, d_ranges,
+            d_trig, g->beams, w.tile_count, g->act_raw, w.sh, g->blk_hist, g->blk_n, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "plan", &t, fs);
@@ -1514,21 +1378,14 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                      w.heavy_list, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
-  // (the bench's kernel table keeps the name "scatter" for this stage either way)
   dm_timer_begin(g, "scatter", &t, fs);
-  if (ge.stage_blk > 0)
-    DM_LAUNCH(k_gather, dim3(nblk), dim3(256), 0, fs, ge, w.tile_cur, g->blk_hist, g->blk_n, g->blk_np,
-              g->stage, g->stage_sr, w.pieces, w.cnt);
-  else
-    DM_LAUNCH(k_scatter, dim3(nblk), dim3(256), 0, fs, a, ge, g->beams,
-                       w.tile_cur, g->blk_hist, g->blk_n, w.pieces, w.cnt);
+  DM_LAUNCH(k_scatter, dim3(nblk), dim3(256), 0, fs, a, ge, g->beams,
+            w.tile_cur, g->blk_hist, g->blk_n, w.pieces, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
-  if (g->overlap && !g->fe_gate) {
-    DM_HIP(dm_batch_flush_all());
-    DM_HIP(hipEventRecord(g->ev_fe, fs));
-    DM_HIP(hipStreamWaitEvent(g->stream, g->ev_fe, 0));
-  } else if (g->overlap) {
+  if (g->overlap) {
+    // front-end -> map update by a device-side seq gate (an event wait
+    // measured 211-213 vs 215-218 x 10^9 updates/s, profiles/r02_fe_gate_ab.log)
     if (int rc = dm_launch_signal(fs, g->fe_flag)) return rc;
     // a timeout sets the sticky halt word (not this call's counters: the
     // front-end's own reset, still queued, would clear them)
@@ -1538,34 +1395,20 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   }
   const int vec_ok = (g->W % 4 == 0) ? 1 : 0;
   // heavy chunks and medium tiles first (the long items), then the light
-  // tiles; k_heavy_apply then applies the heavy tiles' merged slabs
+  // tiles; the last item of each heavy tile applies its merged slab
   dm_timer_begin(g, "tile_accum", &t);
-  DM_LAUNCH(k_tile_accum, dim3(grid_for(g->hitem_cap + g->act_cap, 1, g->accum_grid)),
+  DM_LAUNCH(k_tile_accum, dim3(grid_for(g->hitem_cap + g->act_cap, 1, dm_grid::kAccumGrid)),
                      dim3(kQuarter), 0,
                      g->stream, ge, make_apply(g), w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS,
                      (int)CNT_SITEMS, w.pieces, w.tile_count, g->tile_free, w.slabs, g->L, g->state, w.cnt, w.sh, vec_ok,
-                     w.heavy_list, g->fuse_heavy ? w.heavy_done : nullptr, g->fe_flag + kHaltWord);
+                     w.heavy_list, w.heavy_done, g->fe_flag + kHaltWord);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (g->overlap) w.free_owed = true;
-  // A beam meets a (convex) tile in one k-range of <= 64 steps, and chunks
-  // are >= 64 steps long, so a tile gets at most 1 piece per beam (2 when
-  // beams are chunked).  Calls that cannot reach kMedium pieces in any tile
-  // (one 360-beam scan: C1 / C2) have no heavy tile: no k_heavy_apply.
-  const int64_t max_tile_pieces = nb * (ge.chunks > 1 ? 2 : 1);
-  if (max_tile_pieces > kMedium && !g->fuse_heavy) {
-    dm_timer_begin(g, "heavy_apply", &t);
-    DM_LAUNCH(k_heavy_apply, dim3(grid_for(4 * g->heavy_cap, 1, 1024)), dim3(kQuarter), 0, g->stream,
-                       ge, make_apply(g), w.heavy_list, w.tile_count, g->tile_free, w.slabs, g->L, g->state,
-                       w.cnt, w.sh, g->fe_flag + kHaltWord);
-    dm_timer_end(g, &t);
-    DM_HIP(hipGetLastError());
-  }
   // the touched tiles' fmask records (one wave per work item), while the
   // frontier passes read them
   if (!g->fmask_on) {
     g->fmask_valid = false;
-    DM_HIP(batch.finish());
     return DM_OK;
   }
   dm_timer_begin(g, "fmask", &t);
@@ -1575,7 +1418,6 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                      g->fe_flag + kHaltWord);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
-  DM_HIP(batch.finish());
   return DM_OK;
 }
 
@@ -1587,8 +1429,6 @@ int dm_launch_signal(hipStream_t s, unsigned long long* flag) {
 
 int dm_launch_gate(hipStream_t s, unsigned long long* flag, unsigned long long* err, unsigned long long err_bit,
                    unsigned long long ticks, unsigned long long fault) {
-  // the signals it may wait for are submitted first (dm_batch.h)
-  DM_HIP(dm_batch_flush_others(s));
   DM_LAUNCH(k_seq_gate, dim3(1), dim3(64), 0, s, flag, err, err_bit, ticks ? ticks : kGateTicks, fault);
   DM_HIP(hipGetLastError());
   return DM_OK;

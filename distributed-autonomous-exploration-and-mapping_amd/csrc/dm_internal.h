@@ -20,7 +20,6 @@
 
 #include "../../include/dm.h"
 
-#include "dm_batch.h"
 #include "dm_ray.h"
 
 
@@ -49,7 +48,6 @@ enum {
 // CNT_OVERFLOW bits of a frontier pass
 constexpr unsigned long long kOvSlots = 4ull;      // a slot shard region overflowed
 constexpr unsigned long long kOvUnionFind = 8ull;  // a union-find loop hit its bound (dm_uf.h)
-constexpr unsigned long long kOvGate = 16ull;      // the pass stream's hand-off gate timed out
 constexpr unsigned long long kOvPipeline = 32ull;  // the handle's sticky hand-off error was set (kHaltWord)
 // fe_flag[kHaltWord]: sticky error word of the overlapped pipeline.  The
 // integrate front-end -> map update gate sets bit 1 when it times out; from
@@ -60,7 +58,7 @@ constexpr int kHaltWord = 8;
 // Hand-off words (fe_flag, bits_flag): k_seq_signal increments [kSigWord],
 // k_seq_gate increments [kGateWord] and waits until [kSigWord] reaches it:
 // the n-th gate waits for the n-th signal, with no host-side sequence number
-// in the kernel arguments (dm_batch.h: the graphs are reused).
+// in the kernel arguments.
 constexpr int kSigWord = 0;
 constexpr int kGateWord = 4;
 constexpr int kStampWord = 8;  // bits_flag: the last frontier pass's stamp (k_frontier_prep)
@@ -89,6 +87,9 @@ enum { SH_U = 0, SH_T = 1, SH_TH = 2, SH_ACT = 3 };  // integrate shard fields
 // and tiles too run-rich for a tile-wave (the next pass sizes the big kernel's grid)
 enum { SH_SLOT = 0, SH_RUNS = 1, SH_FTF = 2, SH_BIG = 3 };
 
+// dm_last_stats entries (include/dm.h)
+constexpr int kNStats = 10;
+
 // Readback header in front of the sorted cluster records (device out_clu and
 // pinned h_out both point kRbRecords records into their allocation): the
 // frontier counters [CNT_N] and the fullest slot shard [CNT_N], written by
@@ -98,11 +99,27 @@ enum { SH_SLOT = 0, SH_RUNS = 1, SH_FTF = 2, SH_BIG = 3 };
 // (shard sums)
 constexpr int kRbRecords = 6;  // 6 * 48 B = 288 B >= (CNT_N + 3) * 8 B
 static_assert(kRbRecords * sizeof(dm_cluster) >= (CNT_N + 4) * sizeof(unsigned long long), "readback header");
-__host__ __device__ inline unsigned long long* dm_rb_header(dm_cluster* records) {
-  return reinterpret_cast<unsigned long long*>(records - kRbRecords);
+// The mapped host readback carries 32-byte records (label, size, sum_x,
+// sum_y): the host computes the centroids with the SPEC's double formula
+// (one division, then add; no FMA), bit-identical to the device's, so a third
+// fewer bytes cross PCIe than whole dm_cluster records.
+struct dm_raw_record {
+  long long label, size, sum_x, sum_y;
+};
+constexpr int kRbHostRecords = 6;  // 6 * 32 B = 192 B of header in front of the host records
+static_assert(kRbHostRecords * sizeof(dm_raw_record) >= (CNT_N + 4) * sizeof(unsigned long long),
+              "readback header");
+__host__ __device__ inline unsigned long long* dm_rb_header(dm_raw_record* records) {
+  return reinterpret_cast<unsigned long long*>(records - kRbHostRecords);
 }
-__host__ __device__ inline const unsigned long long* dm_rb_header(const dm_cluster* records) {
-  return reinterpret_cast<const unsigned long long*>(records - kRbRecords);
+__host__ __device__ inline const unsigned long long* dm_rb_header(const dm_raw_record* records) {
+  return reinterpret_cast<const unsigned long long*>(records - kRbHostRecords);
+}
+// SPEC a10 centroid: origin + (sum / size + 0.5) * res,
+// one IEEE division, then add (compiled with -ffp-contract=off, host and device)
+__host__ __device__ inline double dm_centroid(double origin, long long sum, long long size, double res) {
+  const double m = (double)sum / (double)size;
+  return origin + (m + 0.5) * res;
 }
 
 struct dm_grid;
@@ -147,8 +164,6 @@ struct dm_grid {
   // DM_FAULT_GATE=1 (read at dm_create; fault-injection tests only): the
   // front-end gate waits for a sequence number that never comes, ~10 us
   bool fault_gate = false;
-  bool fe_gate = true;     // DM_FE_GATE=0: the front-end hand-off by an event wait (ev_fe) instead of a seq gate
-  bool pass_gate = false;  // DM_PASS_GATE=1: the bit rows' hand-off by a seq gate instead of ev_bits
   // ev_bits[parity]: the end of a split pass's bit rows on `stream` (the pass
   // stream waits for it); it also frees the integrate workspaces whose
   // accumulations are ahead of it (dm_mark_ws_free), so the next front-end
@@ -163,8 +178,8 @@ struct dm_grid {
   // h_out_cap / m_out below point at the slot in use (dm_select_slot).
   struct RbSlot {
     dm_cluster* out_clu = nullptr;    // device sorted band records (after kRbRecords header records)
-    dm_cluster* h_out = nullptr;      // mapped host readback (after the header)
-    dm_cluster* h_out_dev = nullptr;  // its device address
+    dm_raw_record* h_out = nullptr;      // mapped host readback (after the header), 32-byte records
+    dm_raw_record* h_out_dev = nullptr;  // its device address
     int64_t h_out_cap = 0;
     dm_cluster* m_out = nullptr;      // device sorted merged records
     hipEvent_t ev = nullptr;
@@ -174,7 +189,6 @@ struct dm_grid {
     uint64_t pass = 0;                // fr_pass / m_pass of the pass
     int64_t merge_n = 0;              // nranks * rec_cap of a merge
     uint64_t wepoch = 0, mepoch = 0;  // passes / merges that wrote out_clu / m_out so far
-    int64_t dma_copied = -1;          // >= 0: the pass's records reached h_out by a DMA copy of this many
   };
 #ifndef DM_RB_SLOTS
 #define DM_RB_SLOTS 2
@@ -220,20 +234,6 @@ struct dm_grid {
   int64_t blk_cap = 0;            // workgroups blk_hist / blk_n hold
   int2* blk_hist = nullptr;       // [beam blocks][1024] k_beam_prep's (tile, pieces | hash slot << 16) histogram
   int32_t* blk_n = nullptr;       // [beam blocks] its entries
-  // Staged front-end (opt-in, DM_FE_STAGED=1; default: k_scatter's second
-  // enumeration instead): k_beam_prep stores every piece it enumerates,
-  // packed, in its workgroup's region of `stage` with its place in the
-  // workgroup's tile histogram (stage_sr: hash slot | rank << 16, or bit 31 |
-  // tile for a tile the LDS table could not hold); k_gather moves them into
-  // the tile bins once k_plan has placed the bins.  Shared by the workspace
-  // sets: k_gather of a call runs before the next call's k_beam_prep (both
-  // on the front-end stream).
-  bool fe_staged = false;
-  PackedPiece* stage = nullptr;   // [beam blocks][stage_blk]
-  uint32_t* stage_sr = nullptr;   // [beam blocks][stage_blk]
-  int32_t* blk_np = nullptr;      // [beam blocks] pieces staged
-  int64_t stage_blk = 0;          // staged pieces per workgroup region (256 threads x pieces per beam bound)
-  int64_t stage_cap = 0;          // pieces `stage` holds
   int64_t segs_cap = 0;           // pieces per workspace
   int32_t* act_raw = nullptr;    // [kShards][act_cap] first-touch lists per shard
   int64_t act_cap = 0;
@@ -260,16 +260,10 @@ struct dm_grid {
     hipEvent_t free_wait = nullptr;
     bool free_owed = false;
   };
-  // calls cycle through n_iw sets (DM_INT_SETS=2|3, read at dm_create):
-  // with 3, call k+1's front-end waits for call k-2's accumulation instead of
-  // call k-1's, so it can run while call k-1's accumulation is dispatched
-  static constexpr int kIntSetsMax = 3;
-  IntWs iw[kIntSetsMax];
-  int n_iw = 2;
+  // calls alternate between the two sets
+  static constexpr int kIntSets = 2;
+  IntWs iw[kIntSets];
   int iw_cur = 0;                // set of the last integrate call
-  // heavy tiles applied by their last k_tile_accum item (default) instead of
-  // a separate k_heavy_apply launch (DM_HEAVY_SEPARATE=1, A/B measurement)
-  bool fuse_heavy = true;
   double* trig = nullptr; int32_t trig_n = -1; float trig_amin = 0, trig_inc = 0;
   int64_t trig_cap = 0;
   double* pose4 = nullptr; int64_t pose_cap = 0;
@@ -300,7 +294,8 @@ struct dm_grid {
     uint64_t* fbits = nullptr;          // [NT][64]
     int32_t* edge_slot = nullptr;       // [2][W]
     int32_t* slot_parent = nullptr;     // [slot_cap]
-    hipEvent_t busy = nullptr;          // the last pass's end (an alias of its readback event)
+    hipEvent_t busy = nullptr;          // the last pass's end (an alias of its readback event or ev_split)
+    hipEvent_t ev_split = nullptr;      // end of a split export pass on the pass stream (owned)
     bool busy_pending = false;
     uint64_t busy_pass = 0;             // fr_pass of that pass
   };
@@ -343,8 +338,8 @@ struct dm_grid {
   int32_t* slot_k = nullptr;      // [slot_cap] root slot -> compact cluster index
   int32_t* rank_of = nullptr;     // [slot_cap] compact cluster index -> sorted position
   dm_cluster* out_clu = nullptr;  // [slot_cap] sorted cluster records (k_rank_sort)
-  dm_cluster* h_out = nullptr;    // pinned (mapped, coherent) readback: header + sorted records
-  dm_cluster* h_out_dev = nullptr;  // its device address
+  dm_raw_record* h_out = nullptr;  // pinned (mapped, coherent) readback: header + sorted 32-byte records
+  dm_raw_record* h_out_dev = nullptr;  // its device address
   int64_t h_out_cap = 0;
   int32_t* cell_slot = nullptr;   // dense [R][W] (only when labels requested)
   int32_t* edge_slot = nullptr;   // [2][W] slots of the band's first / last row
@@ -355,51 +350,37 @@ struct dm_grid {
   int has_halo[2] = {0, 0};
   bool frontier_valid = false;
 
-  // large-K cluster sort (LSD radix, dm_frontier.hip k_rx_*): used when
+  // large-K cluster sort (row buckets, dm_frontier.hip k_rs_*): used when
   // the last collected pass of its kind had more than sort_min clusters
-  unsigned long long* bs_key = nullptr;   // [bs_cap] radix-sort keys (label - base), two buffers
+  unsigned long long* bs_key = nullptr;   // [bs_cap] sort keys (label - base), two buffers
   unsigned long long* bs_key2 = nullptr;
   int32_t* bs_idx = nullptr;      // [bs_cap] their record indices, two buffers
   int32_t* bs_idx2 = nullptr;
-  int32_t* bs_hist = nullptr;     // [2^rx_bits][ceil(bs_cap / kRxItems)] digit x block counts -> offsets
   int64_t bs_cap = 0;
-  // row-bucket sort (k_rs_*, the default large-K sort; DM_LARGE_SORT=radix:
-  // the LSD radix k_rx_*): per-row counters (zero between sorts) and offsets
+  // per-row counters (zero between sorts) and offsets
   int32_t* rs_cnt = nullptr;      // [rs_rows]
   int32_t* rs_off = nullptr;      // [rs_rows + 1]
-  unsigned long long* rs_status = nullptr;  // [rs_rows / 8192 + 1] k_rs_scan's published workgroup totals
+  unsigned long long* rs_status = nullptr;  // [rs_rows / 8192 + 2] k_rs_scan's workgroup totals + failure word
   int64_t rs_rows = 0;
-  bool row_sort = true;
-  // DM_DMA_READBACK=1 (A/B): band passes with many clusters copy their
-  // records to the host with a DMA copy after the sort instead of the sort
-  // kernel's mapped stores.  Off by default: at C5-4096 the sort kernels
-  // drop 230 -> 41 us, but the copy then runs after them instead of
-  // overlapping them and the pass ends later (step 1.48 -> 1.59 ms,
-  // profiles/r03_dma_readback_ab.log)
-  bool dma_readback = false;
   int64_t sort_hint = 0, msort_hint = 0;  // clusters of the last band / merge readback
   int64_t ftile_hint = 0;                 // listed tiles of the last collected frontier pass
   int64_t runs_hint = 0, ftf_hint = 0;    // its runs and tiles with frontier cells
   int64_t big_hint = 0;                   // its tiles left to k_frontier_tile_big by k_frontier_tile
-  // A/B knobs of the pass (read at dm_create): the cluster count above which
-  // the radix sort replaces the rank sort (DM_SORT_MIN), the radix digit
-  // width cap (DM_RX_BITS, 4..11), and whether the run-rich tiles' kernel
-  // runs beside the wave kernel on big_stream (DM_BIG_STREAM=0: after it,
-  // on the pass stream)
+  // the cluster count above which the row sort replaces the rank sort
+  // (DM_SORT_MIN, read at dm_create: tests run small maps through both)
   int64_t sort_min = 4096;
-  int rx_bits = 8;
-  bool big_concurrent = true;
   // tile kernel choice: 0 from those statistics, 1 always the wave-per-tile
   // kernel, 2 always the 256-thread kernel (DM_FRONTIER_KERNEL=auto|wave|wg,
   // read at dm_create, for A/B measurements; all three are exact)
   int frontier_kernel = 0;
-  // k_tile_accum's largest grid (DM_ACCUM_GRID, A/B; the kernel grid-strides)
-  int accum_grid = 16384;
+  // k_tile_accum's largest grid (the kernel grid-strides)
+  static constexpr int kAccumGrid = 16384;
   // beams are split into k-ranges below this many threads per CU
-  // (dm_integrate_chunks; DM_CHUNK_THREADS, A/B)
-  int chunk_threads_per_cu = 512;
+  // (dm_integrate_chunks)
+  static constexpr int kChunkThreadsPerCu = 512;
   // light tiles with at most this many pieces are sparse work items: walked
-  // first, then only their touched cells are loaded (DM_SPARSE_PIECES, A/B)
+  // first, then only their touched cells are loaded (DM_SPARSE_PIECES, read
+  // at dm_create: 0 sends every light tile through the dense path, tests)
   int sparse_pieces = 15;
 
   // cross-band merge workspace (dm_merge.hip), sized nranks * rec_cap
@@ -424,9 +405,6 @@ struct dm_grid {
   double* goal_io = nullptr;          // [4 * 256] robots xy, then centroids xy
   int64_t* goal_idx = nullptr;        // [256]
 
-  // launch batching (dm_batch.h): chains and the graph cache
-  DmBatch batch;
-
   // profiling
   bool profile = false;
   std::vector<KernelTimer> pending;
@@ -449,11 +427,7 @@ inline void dm_select_slot(dm_grid* g, int slot) {
 // accumulation is enqueued on g->stream before this point): `recorded`, an
 // event just recorded on g->stream, or each set's own ev_free recorded now.
 inline hipError_t dm_mark_ws_free(dm_grid* g, hipEvent_t recorded = nullptr) {
-  // `recorded` (a pass-parity or readback-slot event) is re-recorded two
-  // passes later: with 3 sets a front-end would then wait for a later
-  // accumulation than its set's own, so each set records its own event
-  if (g->n_iw > 2) recorded = nullptr;
-  for (int i = 0; i < g->n_iw; ++i) {
+  for (int i = 0; i < dm_grid::kIntSets; ++i) {
     dm_grid::IntWs& w = g->iw[i];
     if (!w.free_owed) continue;
     w.free_owed = false;
@@ -491,7 +465,7 @@ inline hipError_t dm_join_pass_stream(dm_grid* g) {
 // thread per beam would walk up to 2*nmax/64 pieces serially on a mostly
 // idle GPU (sparse scans, 1 cm maps).  Chunks stay >= 64 steps long.
 inline int32_t dm_integrate_chunks(const dm_grid* g, int64_t nb) {
-  const int64_t want = (int64_t)g->chunk_threads_per_cu * (int64_t)(g->n_cu > 0 ? g->n_cu : 256);
+  const int64_t want = (int64_t)dm_grid::kChunkThreadsPerCu * (int64_t)(g->n_cu > 0 ? g->n_cu : 256);
   if (nb <= 0 || nb >= want) return 1;
   const int64_t by_len = (g->nmax + 1) / 64 > 1 ? (g->nmax + 1) / 64 : 1;
   const int64_t by_fill = (want + nb - 1) / nb;
@@ -527,25 +501,26 @@ int dm_launch_rank_sort(hipStream_t stream, long long* clusters, const long long
                         const long long* labels, const unsigned long long* d_count,
                         int64_t max_records, double ox, double oy, double res, dm_cluster* out,
                         int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
-                        int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
+                        int ncnt, int sorted_idx, const unsigned long long* fsh, dm_raw_record* host_out,
                         int64_t host_cap, int64_t expect);
 // Listed tiles from which a frontier pass reads fmask instead of state bytes.
 constexpr int64_t kFmaskOnTiles = 8192;
 int dm_grow_bucket_sort(dm_grid* g, int64_t n);
-int64_t dm_rx_items();  // keys per radix-sort block (dm_frontier.hip)
-// LSD radix sort of the raw records (labels of rows [row_base, row_base +
+// Row-bucket sort of the raw records (labels of rows [row_base, row_base +
 // rows)): same outputs, readback header and flags as dm_launch_rank_sort.
 int dm_launch_bucket_sort(dm_grid* g, hipStream_t stream, long long* clusters, const long long* sums,
                           const long long* labels, const unsigned long long* d_count,
                           int64_t max_records, int64_t row_base, int64_t rows, dm_cluster* out,
                           int32_t* rank_of, unsigned long long* d_sorted, const unsigned long long* cnt,
-                          int ncnt, int sorted_idx, const unsigned long long* fsh, dm_cluster* host_out,
+                          int ncnt, int sorted_idx, const unsigned long long* fsh, dm_raw_record* host_out,
                           int64_t host_cap);
 // cross-band exchange (dm_merge.hip)
 int64_t dm_export_nbytes(int64_t W, int64_t rec_cap);
-int dm_launch_export(dm_grid* g, void* d_export, int64_t rec_cap);
-int dm_launch_merge(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap,
+int dm_launch_export(dm_grid* g, hipStream_t s, void* d_export, int64_t rec_cap);
+int dm_launch_merge(dm_grid* g, hipStream_t s, const void* d_gathered, int32_t nranks, int64_t rec_cap,
                     int64_t min_size);
+// The stream band exports end on and merges run on (dm_exchange_stream).
+inline hipStream_t dm_exchange_stream_of(const dm_grid* g) { return g->overlap ? g->pass_stream : g->stream; }
 // goal selection (dm_goals.hip)
 int dm_launch_goal_topk(dm_grid* g, const dm_cluster* d_recs, int64_t K, const double* d_robots, int32_t R,
                         int32_t T, int64_t min_size, double w, double min_dist,
@@ -598,6 +573,16 @@ void dm_timer_end(dm_grid* g, KernelTimer* t);
     if (_e != hipSuccess) return dm_hip_check(_e, #call);    \
   } while (0)
 
-// Kernel launch (dm_batch.h: recorded into a graph chain inside a
-// DmBatchScope, launched directly otherwise).
-#define DM_LAUNCH(...) DM_HIP(dm_launch(__VA_ARGS__))
+// Kernel launch.
+#define DM_LAUNCH(kernel, grid, block, shmem, stream, ...) \
+  hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__)
+
+// Round n up to a quarter-octave step (1, 1.25, 1.5, 1.75 x 2^k; exact below
+// 8): grid sizes derived from the last pass's statistics take few values.
+inline int64_t dm_quantize_up(int64_t n) {
+  if (n <= 8) return n;
+  int sh = 0;
+  while ((n >> sh) >= 8) ++sh;
+  const int64_t step = (int64_t)1 << sh;  // n in [4, 8) x 2^sh: steps of a quarter octave
+  return ((n + step - 1) / step) * step;
+}

@@ -244,22 +244,22 @@ int grid_for(int64_t n, int threads, int64_t cap) {
 
 int64_t dm_export_nbytes(int64_t W, int64_t rec_cap) { return export_bytes(W, rec_cap); }
 
-int dm_launch_export(dm_grid* g, void* d_export, int64_t rec_cap) {
+int dm_launch_export(dm_grid* g, hipStream_t s, void* d_export, int64_t rec_cap) {
   ExportView v;
   v.W = g->W;
   v.rec_cap = rec_cap;
   v.bytes = export_bytes(g->W, rec_cap);
   KernelTimer t;
-  dm_timer_begin(g, "export", &t);
+  dm_timer_begin(g, "export", &t, s);
   hipLaunchKernelGGL(k_export, dim3(grid_for(std::max<int64_t>(2 * g->W, rec_cap), 256, 256)), dim3(256), 0,
-                     g->stream, v, g->row0, g->R, g->edge_slot, g->slot_root, g->slot_k, g->rank_of,
+                     s, v, g->row0, g->R, g->edge_slot, g->slot_root, g->slot_k, g->rank_of,
                      g->out_clu, g->cnt, static_cast<uint8_t*>(d_export));
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   return DM_OK;
 }
 
-int dm_launch_merge(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap,
+int dm_launch_merge(dm_grid* g, hipStream_t s, const void* d_gathered, int32_t nranks, int64_t rec_cap,
                     int64_t min_size) {
   ++g->m_pass;
   ++g->rb[g->cur_slot].mepoch;  // this merge rewrites the selected slot's records
@@ -271,29 +271,29 @@ int dm_launch_merge(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t 
   m.min_size = min_size < 1 ? 1 : min_size;
   const uint8_t* gat = static_cast<const uint8_t*>(d_gathered);
   const int64_t n = (int64_t)nranks * rec_cap;
-  DM_HIP(hipMemsetAsync(g->m_cnt, 0, sizeof(unsigned long long) * 4, g->stream));
+  DM_HIP(hipMemsetAsync(g->m_cnt, 0, sizeof(unsigned long long) * 4, s));
   KernelTimer t;
-  dm_timer_begin(g, "merge", &t);
+  dm_timer_begin(g, "merge", &t, s);
   const int eg = grid_for(n, 256, 1024);
-  hipLaunchKernelGGL(k_merge_init, dim3(eg), dim3(256), 0, g->stream, m, gat, g->m_parent, g->m_label,
+  hipLaunchKernelGGL(k_merge_init, dim3(eg), dim3(256), 0, s, m, gat, g->m_parent, g->m_label,
                      g->m_acc, g->m_cnt);
   DM_HIP(hipGetLastError());
   if (nranks > 1) {
     hipLaunchKernelGGL(k_merge_pairs, dim3(grid_for((int64_t)(nranks - 1) * g->W, 256, 1024)), dim3(256), 0,
-                       g->stream, m, gat, g->m_parent, g->m_label, g->m_cnt);
+                       s, m, gat, g->m_parent, g->m_label, g->m_cnt);
     DM_HIP(hipGetLastError());
   }
-  hipLaunchKernelGGL(k_merge_resolve, dim3(eg), dim3(256), 0, g->stream, m, gat, g->m_parent, g->m_acc,
+  hipLaunchKernelGGL(k_merge_resolve, dim3(eg), dim3(256), 0, s, m, gat, g->m_parent, g->m_acc,
                      g->m_cnt);
   DM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_merge_compact, dim3(eg), dim3(256), 0, g->stream, m, gat, g->m_parent, g->m_label,
+  hipLaunchKernelGGL(k_merge_compact, dim3(eg), dim3(256), 0, s, m, gat, g->m_parent, g->m_label,
                      g->m_acc, g->m_clu, g->m_cnt);
   DM_HIP(hipGetLastError());
   // merged labels are global row-major indices over the whole map
   const int rc = g->msort_hint > g->sort_min
-      ? dm_launch_bucket_sort(g, g->stream, g->m_clu, nullptr, nullptr, g->m_cnt + M_K, n, 0, g->H, g->m_out, nullptr, g->m_cnt + M_SORTED,
+      ? dm_launch_bucket_sort(g, s, g->m_clu, nullptr, nullptr, g->m_cnt + M_K, n, 0, g->H, g->m_out, nullptr, g->m_cnt + M_SORTED,
                               g->m_cnt, 4, M_SORTED, nullptr, g->h_out_dev, g->h_out_cap)
-      : dm_launch_rank_sort(g->stream, g->m_clu, nullptr, nullptr, g->m_cnt + M_K, n, g->p.origin_x, g->p.origin_y,
+      : dm_launch_rank_sort(s, g->m_clu, nullptr, nullptr, g->m_cnt + M_K, n, g->p.origin_x, g->p.origin_y,
                             g->p.resolution, g->m_out, nullptr, g->m_cnt + M_SORTED, g->m_cnt, 4,
                             M_SORTED, nullptr, g->h_out_dev, g->h_out_cap, g->msort_hint);
   dm_timer_end(g, &t);

@@ -53,7 +53,37 @@
     }                                                                          \
     return 0;                                                                  \
   }
+// Per-workgroup timeline of the last launch of a kernel (DM_TL_*): thread 0
+// of workgroup b < DM_TL_MAX stores {start tick, end tick, XCC id << 32 |
+// HW_ID, user word} (wall clock, 100 MHz); read with dm_debug_timeline_<tu>().
+#define DM_TL_MAX 65536
+#define DM_TL_DECL(tu) __device__ unsigned long long dm_tl_##tu[DM_TL_MAX * 4];
+#define DM_TL_BEGIN() const long long _dm_tl0 = wall_clock64()
+#define DM_TL_END(tu, word)                                                    \
+  do {                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < DM_TL_MAX) {                          \
+      const unsigned long long _hw = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11)); \
+      const unsigned long long _xcc = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11)) & 0xFu; \
+      unsigned long long* _r = dm_tl_##tu + 4 * (unsigned long long)blockIdx.x; \
+      _r[0] = (unsigned long long)_dm_tl0;                                     \
+      _r[1] = (unsigned long long)wall_clock64();                              \
+      _r[2] = (_xcc << 32) | _hw;                                              \
+      _r[3] = (unsigned long long)(word);                                      \
+    }                                                                          \
+  } while (0)
+#define DM_TL_READER(tu)                                                       \
+  extern "C" int dm_debug_timeline_##tu(unsigned long long* out, int n_wg) {   \
+    if (n_wg > DM_TL_MAX) n_wg = DM_TL_MAX;                                    \
+    if (hipDeviceSynchronize() != hipSuccess) return -3;                       \
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(dm_tl_##tu), sizeof(unsigned long long) * 4 * (size_t)n_wg) != hipSuccess) \
+      return -3;                                                               \
+    return 0;                                                                  \
+  }
 #else
+#define DM_TL_DECL(tu)
+#define DM_TL_BEGIN() do {} while (0)
+#define DM_TL_END(tu, word) do {} while (0)
+#define DM_TL_READER(tu)
 #define DM_PH_DECL(tu)
 #define DM_PH_INIT() do {} while (0)
 #define DM_PH(acc, k) do {} while (0)

@@ -77,6 +77,10 @@ struct dm_shard_set {
   std::vector<uint8_t*> exp[kSets];                 // export record of the band
   uint8_t* gathered[kSets] = {nullptr, nullptr};    // P records on band 0's device
   std::vector<hipEvent_t> ev_rows, ev_exp;
+  // dm_sh_ld06_to_scans_device writes its scans on band 0's stream: the next
+  // dm_sh_integrate_device orders every band's input reads after ev_in
+  hipEvent_t ev_in = nullptr;
+  bool in_pending = false;
   int64_t rec_cap = 0, want_rec_cap = 0, nb = 0;
   bool refresh = false;  // run a synchronous pass on every band before the next exchange
   int set = 0;       // parity of the next pass
@@ -148,17 +152,30 @@ int sh_note_incomplete(dm_shard_set* s, int64_t max_k) {
 
 int sh_refresh_bands(dm_shard_set* s, bool synced) {
   if (!s->refresh) return sh_apply_growth(s, synced);
+  // band 0's own pass would become its goal source (dm_assign_goals reads
+  // the last collected result): keep the last merged result's instead
+  dm_grid* b0 = s->band[0];
+  const int goal_slot = b0->goal_slot, goal_kind = b0->goal_kind;
+  const uint64_t goal_epoch = b0->goal_epoch, goal_gen = b0->goal_gen;
+  const int64_t goal_n = b0->goal_n;
   for (int r = 0; r < s->P; ++r) {
     int64_t n = 0;
     const int rc = dm_frontiers(s->band[(size_t)r], nullptr, nullptr, nullptr, 0, &n);
     if (rc && rc != DM_ERR_CAPACITY) return rc;
   }
+  b0->goal_slot = goal_slot;
+  b0->goal_kind = goal_kind;
+  b0->goal_epoch = goal_epoch;
+  b0->goal_gen = goal_gen;
+  b0->goal_n = goal_n;
   s->refresh = false;
   return sh_apply_growth(s, synced);
 }
 
+// One exchange copy on `st`: a peer copy over xGMI between two devices, a
+// device copy when both are the same (hipMemcpyPeerAsync takes both, so the
+// bands-on-one-GPU tests drive this same call).
 hipError_t peer_copy(void* dst, int ddev, const void* src, int sdev, size_t n, hipStream_t st) {
-  if (ddev == sdev) return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, st);
   return hipMemcpyPeerAsync(dst, ddev, src, sdev, n, st);
 }
 
@@ -186,14 +203,18 @@ int sh_enqueue_exchange(dm_shard_set* s, int k) {
     if ((rc = dm_set_halo_device(b, r > 0 ? s->halo[k][r] : nullptr, r + 1 < P ? s->halo[k][r] + W : nullptr)))
       return rc;
     if ((rc = dm_frontiers_export_device(b, s->exp[k][r], s->rec_cap))) return rc;
-    DM_HIP(hipEventRecord(s->ev_exp[r], b->stream));
+    // the record is complete on the band's exchange stream (its pass
+    // stream with overlap on: the split pass)
+    DM_HIP(hipEventRecord(s->ev_exp[r], dm_exchange_stream_of(b)));
   }
+  // gathered on band 0's exchange stream, where its merge runs
   dm_grid* b0 = s->band[0];
   DM_HIP(hipSetDevice(s->dev[0]));
+  hipStream_t ms = dm_exchange_stream_of(b0);
   for (int r = 0; r < P; ++r) {
-    DM_HIP(hipStreamWaitEvent(b0->stream, s->ev_exp[r], 0));
+    DM_HIP(hipStreamWaitEvent(ms, s->ev_exp[r], 0));
     DM_HIP(peer_copy(s->gathered[k] + (size_t)r * (size_t)s->nb, s->dev[0], s->exp[k][r], s->dev[r],
-                     (size_t)s->nb, b0->stream));
+                     (size_t)s->nb, ms));
   }
   return DM_OK;
 }
@@ -253,6 +274,7 @@ int dm_sh_destroy(dm_grid* g) {
     (void)hipSetDevice(s->dev[0]);
     for (auto* p : s->gathered)
       if (p) (void)hipFree(p);
+    if (s->ev_in) (void)hipEventDestroy(s->ev_in);
   }
   for (int r = 0; r < s->P; ++r) (void)dm_destroy(s->band[r]);
   delete s;
@@ -339,6 +361,11 @@ extern "C" int dm_create_sharded(dm_grid** out, const dm_params* p, int32_t nran
       if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
     }
   }
+  (void)hipSetDevice(devices[0]);
+  {
+    const hipError_t e = hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming);
+    if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
+  }
   // peer access between the bands' devices where the platform offers it
   // (the copies work either way; with access they go device to device)
   for (int a = 0; a < nranks; ++a)
@@ -352,7 +379,12 @@ extern "C" int dm_create_sharded(dm_grid** out, const dm_params* p, int32_t nran
         (void)hipGetLastError();
       }
     }
-  if (int rc = sh_alloc_exchange(s, 16384)) return fail(rc);
+  // records per band export, sized for the band up front (an export that
+  // overflows has no result): a cluster per two tiles of the band (C5's
+  // sparsest rays: ~0.2); the exchange copies stay on the node's xGMI
+  int64_t rec_cap = 16384;
+  while (rec_cap < ceil_div(p->width, DM_TILE) * ceil_div(s->rows[0], DM_TILE) / 2) rec_cap *= 2;
+  if (int rc = sh_alloc_exchange(s, rec_cap)) return fail(rc);
   *out = g;
   return DM_OK;
 }
@@ -453,11 +485,25 @@ int dm_sh_integrate_device(dm_grid* g, int32_t S, const double* d_pose4, int32_t
     DM_HIP(hipPointerGetAttributes(&a, d_ranges));
     src = a.device;
   }
+  // scans written by dm_sh_ld06_to_scans_device on band 0's stream: every
+  // band reads them after that kernel (each band's front-end runs on its own
+  // stream, and with overlap on a stream of its own again)
+  const bool wait_in = s->in_pending;
+  s->in_pending = false;
   for (int r = 0; r < s->P; ++r) {
+    dm_grid* b = s->band[(size_t)r];
     const int d = s->dev[(size_t)r];
     const double* pp = d_pose4;
     const float* rp = d_ranges;
+    // the stream the band's front-end (the only reader of the inputs) runs on
+    hipStream_t fs = b->overlap ? b->fe_stream : b->stream;
+    DM_HIP(hipSetDevice(d));
+    if (wait_in) DM_HIP(hipStreamWaitEvent(fs, s->ev_in, 0));
     if (nb > 0 && d != src) {  // inputs on another device: a copy the band owns
+      if ((int64_t)S * 4 > s->d_pose_cap[(size_t)r] || nb > s->d_ranges_cap[(size_t)r]) {
+        // a call in flight may still read the old copy
+        if (int rc = dm_synchronize(b)) return rc;
+      }
       if ((int64_t)S * 4 > s->d_pose_cap[(size_t)r]) {
         if (int rc = dev_alloc_on(d, &s->d_pose[(size_t)r], (int64_t)S * 4, "sharded poses")) return rc;
         s->d_pose_cap[(size_t)r] = (int64_t)S * 4;
@@ -466,15 +512,14 @@ int dm_sh_integrate_device(dm_grid* g, int32_t S, const double* d_pose4, int32_t
         if (int rc = dev_alloc_on(d, &s->d_ranges[(size_t)r], nb, "sharded ranges")) return rc;
         s->d_ranges_cap[(size_t)r] = nb;
       }
-      // the band's front-end may still read the previous copy: after it
-      if (int rc = dm_synchronize(s->band[(size_t)r])) return rc;
-      DM_HIP(hipSetDevice(d));
-      DM_HIP(hipMemcpyPeer(s->d_pose[(size_t)r], d, d_pose4, src, sizeof(double) * 4 * (size_t)S));
-      DM_HIP(hipMemcpyPeer(s->d_ranges[(size_t)r], d, d_ranges, src, sizeof(float) * (size_t)nb));
+      // on the front-end's stream: after the previous call's front-end read
+      // the last copy, before this call's reads it
+      DM_HIP(hipMemcpyPeerAsync(s->d_pose[(size_t)r], d, d_pose4, src, sizeof(double) * 4 * (size_t)S, fs));
+      DM_HIP(hipMemcpyPeerAsync(s->d_ranges[(size_t)r], d, d_ranges, src, sizeof(float) * (size_t)nb, fs));
       pp = s->d_pose[(size_t)r];
       rp = s->d_ranges[(size_t)r];
     }
-    if (int rc = dm_integrate_device(s->band[(size_t)r], S, pp, N, rp, amin, inc)) return rc;
+    if (int rc = dm_integrate_device(b, S, pp, N, rp, amin, inc)) return rc;
     s->active[(size_t)r] = 1;
   }
   return DM_OK;
@@ -538,15 +583,18 @@ int dm_sh_set_overlap(dm_grid* g, int32_t on) {
 
 int dm_sh_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out) {
   dm_shard_set* s = g->sh;
-  uint64_t sum[14] = {0};
+  if (cap > 0 && !out) return dm_set_error(DM_ERR_INVALID_ARG, "out is NULL");
+  // [0, 7): the last integrate call's counters, over the bands it ran on;
+  // the frontier pass's over every band
+  uint64_t sum[kNStats] = {0};
   for (int r = 0; r < s->P; ++r) {
-    uint64_t v[14] = {0};
+    uint64_t v[kNStats] = {0};
     int32_t n = 0;
-    if (int rc = dm_last_stats(s->band[(size_t)r], v, 14, &n)) return rc;
-    for (int i = 0; i < 14; ++i) sum[i] += v[i];
+    if (int rc = dm_last_stats(s->band[(size_t)r], v, kNStats, &n)) return rc;
+    for (int i = s->active[(size_t)r] ? 0 : 7; i < kNStats; ++i) sum[i] += v[i];
   }
-  for (int32_t i = 0; i < cap && i < 14; ++i) out[i] = sum[i];
-  if (n_out) *n_out = 14;
+  for (int32_t i = 0; i < cap && i < kNStats; ++i) out[i] = sum[i];
+  if (n_out) *n_out = kNStats;
   return DM_OK;
 }
 
@@ -745,7 +793,13 @@ int dm_sh_ld06_to_scans(dm_grid* g, int32_t S, const dm_ld06_point* points, cons
 
 int dm_sh_ld06_to_scans_device(dm_grid* g, int32_t S, const dm_ld06_point* d_points, const int64_t* d_offsets,
                                int32_t N, int dir, float* d_ranges, float* d_intensities) {
-  return dm_ld06_to_scans_device(g->sh->band[0], S, d_points, d_offsets, N, dir, d_ranges, d_intensities);
+  dm_shard_set* s = g->sh;
+  if (int rc = dm_ld06_to_scans_device(s->band[0], S, d_points, d_offsets, N, dir, d_ranges, d_intensities))
+    return rc;
+  DM_HIP(hipSetDevice(s->dev[0]));
+  DM_HIP(hipEventRecord(s->ev_in, s->band[0]->stream));
+  s->in_pending = true;
+  return DM_OK;
 }
 
 extern "C" int dm_sharded_info(const dm_grid* g, int32_t* nranks, int64_t* rec_cap) {

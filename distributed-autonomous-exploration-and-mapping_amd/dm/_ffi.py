@@ -152,6 +152,7 @@ SIGNATURES = {
     "dm_save": [_vp, ctypes.c_char_p],
     "dm_load": [_vp, ctypes.c_char_p],
     "dm_set_stream": [_vp, _vp],
+    "dm_exchange_stream": [_vp, ctypes.POINTER(ctypes.c_void_p)],
     "dm_synchronize": [_vp],
     "dm_profile_enable": [_vp, ctypes.c_int],
     "dm_profile_read": [_vp, ctypes.POINTER(DmKernelStat), _i32, ctypes.POINTER(_i32)],
@@ -164,6 +165,7 @@ SIGNATURES = {
     "dm_merge_bands": [_vp, _vp, _i32, _i64, _i64, _vp, _i64, ctypes.POINTER(_i64)],
     "dm_merge_bands_begin": [_vp, _vp, _i32, _i64, _i64],
     "dm_merge_bands_end": [_vp, _vp, _i64, ctypes.POINTER(_i64)],
+    "dm_merge_max_band_k": [_vp, ctypes.POINTER(_i64)],
     "dm_frontiers_begin": [_vp],
     "dm_max_passes_in_flight": [],
     "dm_frontiers_end": [_vp, _vp, _i64, ctypes.POINTER(_i64)],

@@ -180,8 +180,7 @@ class OccupancyMapper:
         return int(U.value), int(T.value)
 
     STAT_NAMES = ("updates", "touched", "touched_heavy", "pieces", "active_tiles", "work_items",
-                  "heavy_tiles", "frontier_tiles", "frontier_slots", "frontier_clusters",
-                  "graph_launches", "direct_launches", "graph_hits", "graph_misses")
+                  "heavy_tiles", "frontier_tiles", "frontier_slots", "frontier_clusters")
 
     def last_stats(self) -> dict:
         """Diagnostics of the most recent integrate call (dm_last_stats)."""
@@ -362,10 +361,19 @@ class OccupancyMapper:
 
     def frontiers_export_device(self, d_export_ptr: int, rec_cap: int):
         """Band frontiers + export record into a device buffer of
-        export_bytes(rec_cap) bytes; asynchronous on the handle's stream."""
+        export_bytes(rec_cap) bytes; asynchronous, complete on
+        exchange_stream() (the pass stream with overlap on)."""
         with self._lock:
             check(self._lib.dm_frontiers_export_device(self._handle(), ctypes.c_void_p(d_export_ptr),
                                                        int(rec_cap)))
+
+    def exchange_stream(self) -> int:
+        """hipStream_t (as an int) on which exports are complete and merges
+        run (dm_exchange_stream): order the records' all-gather on it."""
+        s = ctypes.c_void_p(0)
+        with self._lock:
+            check(self._lib.dm_exchange_stream(self._handle(), ctypes.byref(s)))
+        return int(s.value or 0)
 
     def merge_bands(self, d_gathered_ptr: int, nranks: int, rec_cap: int, min_size: int):
         """Merge all-gathered export records on the device.  Returns
@@ -388,6 +396,13 @@ class OccupancyMapper:
                     continue
                 check(rc)
                 return buf[: int(n.value)].copy(), None
+
+    def merge_max_band_k(self) -> int:
+        """Largest band cluster count of the last collected merge."""
+        k = ctypes.c_int64(0)
+        with self._lock:
+            check(self._lib.dm_merge_max_band_k(self._handle(), ctypes.byref(k)))
+        return int(k.value)
 
     def merge_bands_begin(self, d_gathered_ptr: int, nranks: int, rec_cap: int, min_size: int):
         """Enqueue the device merge of gathered export records and return

@@ -197,11 +197,25 @@ class ShardedMapper:
 
                 self._torch = torch
                 self._tdev = torch.device("cuda", device)
-                # one stream for the band's kernels and the collectives
-                # around them: RCCL orders itself against it
+                # the band's map stream: its map kernels and the halo-row
+                # all-gather between them (RCCL orders itself against it)
                 self.stream = torch.cuda.Stream(device=self._tdev)
                 self.band.set_stream(self.stream.cuda_stream)
-                self.rec_cap = 16384  # records per band export (grown on an incomplete record)
+                # the export records are all-gathered on the band's exchange
+                # stream (its pass stream with overlap on), over a second
+                # communicator: a records gather that waits for a pass's
+                # labelling then never holds up the next pass's halo gather
+                # on the map stream (one communicator runs its collectives
+                # in issue order)
+                self.rec_group = dist.new_group(list(range(world_size)))
+                self._xstreams = {}
+                # records per band export: sized for the band up front (a
+                # cluster per two tiles), then to twice the largest band K
+                # seen (_size_rec_cap; grown on an incomplete record)
+                tiles = -(-self.W // DM_TILE) * -(-self.rows // DM_TILE)
+                self.rec_cap = 16384
+                while self.rec_cap < tiles // 2:
+                    self.rec_cap *= 2
                 self._bufs = {}
                 self.fallbacks = 0
 
@@ -216,19 +230,26 @@ class ShardedMapper:
 
     def _wait(self, work, what: str):
         """Wait for one async collective at most self.timeout seconds (gloo:
-        host-side; RCCL: orders the current stream, the host deadline is
-        enforced by _drain)."""
+        host-side; RCCL: orders the current stream only — the host deadline is
+        enforced by _poll / _drain on an event recorded after it.  An RCCL
+        work's wait(timeout) would block the host until the collective and
+        every kernel queued before it had finished, which serialises the
+        pipelined passes)."""
         try:
+            if self._nccl:
+                work.wait()
+                return
             ok = work.wait(timeout=timedelta(seconds=self.timeout))
         except Exception as e:  # gloo: a timed-out or aborted peer raises here
             self._fail(f"{what} failed: {e}")
         if ok is False:
             self._fail(f"{what} did not complete within {self.timeout:g} s")
 
-    def _all_gather(self, out, t, what: str):
+    def _all_gather(self, out, t, what: str, group=None):
         self._check()
         try:
-            work = self._dist.all_gather_into_tensor(out, t, group=self.group, async_op=True)
+            work = self._dist.all_gather_into_tensor(out, t, group=group if group is not None else self.group,
+                                                     async_op=True)
         except Exception as e:
             self._fail(f"{what} failed: {e}")
         self._wait(work, what)
@@ -298,22 +319,39 @@ class ShardedMapper:
     def _buf(self, name, n, dtype):
         t = self._bufs.get(name)
         if t is None or t.numel() != n:
+            if t is not None:
+                # a pass in flight may still read the old buffer on another
+                # stream (capacities only change after an incomplete pass)
+                self._torch.cuda.synchronize(self._tdev)
             t = self._torch.empty(n, dtype=dtype, device=self._tdev)
             self._bufs[name] = t
         return t
 
-    def _gather_dev(self, t, out):
-        """all-gather a device tensor into out ([P * n], rank order)."""
+    def _gather_dev(self, t, out, group=None):
+        """all-gather a device tensor into out ([P * n], rank order), ordered
+        on the current stream."""
         if self._nccl:
-            self._all_gather(out, t, "device all-gather")
+            self._all_gather(out, t, "device all-gather", group)
         else:  # gloo rehearsal on GPUs: host-staged
             o = self._torch.empty(out.numel(), dtype=t.dtype)
-            self._all_gather(o, t.cpu(), "all-gather")
+            self._all_gather(o, t.cpu(), "all-gather", group)
             out.copy_(o)
 
+    def _xstream(self):
+        """The band's exchange stream (dm_exchange_stream) as a torch stream."""
+        ptr = self.band.exchange_stream()
+        if ptr == self.stream.cuda_stream:
+            return self.stream
+        xs = self._xstreams.get(ptr)
+        if xs is None:
+            xs = self._torch.cuda.ExternalStream(ptr, device=self._tdev)
+            self._xstreams[ptr] = xs
+        return xs
+
     def _device_enqueue(self):
-        """Halo all-gather, band frontiers + export record, record all-gather
-        and the device merge, all enqueued on self.stream (no host wait)."""
+        """Halo all-gather (map stream), band frontiers + export record, and
+        the records' all-gather on the band's exchange stream (no host wait).
+        Returns the gathered buffer and the exchange stream the merge runs on."""
         torch = self._torch
         W, P, r = self.W, self.world_size, self.rank
         with torch.cuda.stream(self.stream):
@@ -328,8 +366,10 @@ class ShardedMapper:
             exp = self._buf("exp", nb, torch.uint8)
             gexp = self._buf("gexp", P * nb, torch.uint8)
             self.band.frontiers_export_device(exp.data_ptr(), self.rec_cap)
-            self._gather_dev(exp, gexp)
-            return gexp
+        xs = self._xstream()
+        with torch.cuda.stream(xs):
+            self._gather_dev(exp, gexp, self.rec_group)
+        return gexp, xs
 
     def _device_finish(self, result) -> Frontiers | None:
         """Frontiers from a device merge result, or None when a band's export
@@ -340,16 +380,30 @@ class ShardedMapper:
         because a rerun would describe a later map than the pass it collects)."""
         clusters, max_k = result
         if clusters is not None:
+            self._size_rec_cap(self.band.merge_max_band_k())
             return Frontiers(clusters=clusters)
         self.fallbacks += 1
         while self.rec_cap < max_k:
             self.rec_cap *= 2
         return None
 
+    def _size_rec_cap(self, max_k: int):
+        """Records per band export for the next passes, from the largest band
+        K of the pass just collected (the same value on every rank: all merged
+        the same bytes): twice that, a power of two >= 1024, changed only when
+        the band K nears the capacity (grown before it overflows) or the
+        capacity is 4x what is needed (the record is all-gathered every pass:
+        rec_cap x 32 B per rank)."""
+        target = 1024
+        while target < 2 * max_k:
+            target *= 2
+        if max_k > (3 * self.rec_cap) // 4 or self.rec_cap >= 4 * target:
+            self.rec_cap = target
+
     def _frontiers_device(self):
-        gexp = self._device_enqueue()
-        self._drain("frontier exchange")
-        with self._torch.cuda.stream(self.stream):
+        gexp, xs = self._device_enqueue()
+        self._drain("frontier exchange", xs)
+        with self._torch.cuda.stream(xs):  # libdm merges on the exchange stream
             res = self.band.merge_bands(gexp.data_ptr(), self.world_size, self.rec_cap, self.min_size)
         fr = self._device_finish(res)
         # incomplete record (capacity grown now): this call is synchronous, so
@@ -387,11 +441,11 @@ class ShardedMapper:
             self.band.frontiers_begin()
             self._pending.append(("band", None))
         elif self.world_size > 1 and self._dev_path:
-            gexp = self._device_enqueue()
-            with self._torch.cuda.stream(self.stream):
+            gexp, xs = self._device_enqueue()
+            with self._torch.cuda.stream(xs):  # libdm merges on the exchange stream
                 self.band.merge_bands_begin(gexp.data_ptr(), self.world_size, self.rec_cap, self.min_size)
             ev = self._torch.cuda.Event()
-            ev.record(self.stream)  # after this pass's collectives and merge
+            ev.record(xs)  # after this pass's collectives and merge
             self._pending.append(("merge", ev))
         else:  # host exchange (or a non-libdm band): computed now
             self._pending.append(("done", self.frontiers()))

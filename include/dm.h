@@ -152,9 +152,7 @@ int dm_last_counts(dm_grid* g, uint64_t* updates, uint64_t* touched);
 /* Diagnostics of the most recent calls (synchronises the stream):
  * out[0..6] = integrate: U, T, T applied by the heavy-tile pass, pieces (ray
  * pieces binned by tile), active tiles, apply work items, heavy tiles;
- * out[7..9] = frontiers: tiles visited, tile-local components, clusters;
- * out[10..13] = launch batching since dm_create: graph launches, kernels
- * launched directly, graph-cache hits, misses (graph builds). */
+ * out[7..9] = frontiers: tiles visited, tile-local components, clusters. */
 int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out);
 
 /* OccupancyGrid.data for the band: int8[band_rows*width] (-1 / 0 / 100). */
@@ -275,12 +273,24 @@ int dm_get_edge_labels(dm_grid* g, int64_t* first_row, int64_t* last_row);
  * The band handle must have min_frontier_size <= 1 (the size filter applies
  * to merged clusters: dm_merge_bands' min_size). */
 int dm_export_bytes(const dm_grid* g, int64_t rec_cap, int64_t* bytes);
-/* Band frontier extraction + export record, asynchronous on the handle's
- * stream (no host synchronisation).  Halo rows must be set first. */
+/* Band frontier extraction + export record, asynchronous (no host
+ * synchronisation).  Halo rows must be set first.  With dm_set_overlap on,
+ * the pass is split as in dm_frontiers_begin: the map reads stay on the
+ * handle's stream and the labelling, the sort and the export record run on
+ * the handle's exchange stream (dm_exchange_stream), so the next integrate
+ * call's map update overlaps them; the caller's all-gather of the record and
+ * dm_merge_bands(_begin) then belong on that stream. */
 int dm_frontiers_export_device(dm_grid* g, void* d_export, int64_t rec_cap);
+/* The hipStream_t the export record of dm_frontiers_export_device is
+ * complete on and the merges run on: the handle's stream, or with overlap on
+ * its pass stream.  Work ordered after it on that stream (an RCCL all-gather
+ * of the record, dm_merge_bands) needs no other synchronisation. */
+int dm_exchange_stream(dm_grid* g, void** stream);
 /* Merge nranks gathered export records (d_gathered = nranks consecutive
  * records of dm_export_bytes(rec_cap) bytes) into global clusters sorted by
- * label, keeping those with size >= min_size.  Synchronous.  Returns
+ * label, keeping those with size >= min_size.  Synchronous; runs on
+ * dm_exchange_stream, so the gathered buffer must be complete in that
+ * stream's order (e.g. all-gathered on it).  Returns
  * DM_ERR_INCOMPLETE (*n_out = largest band K) when a record is flagged
  * incomplete, DM_ERR_CAPACITY (*n_out = clusters) when cap is too small. */
 int dm_merge_bands(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap,
@@ -293,6 +303,10 @@ int dm_merge_bands(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t r
 int dm_merge_bands_begin(dm_grid* g, const void* d_gathered, int32_t nranks, int64_t rec_cap,
                          int64_t min_size);
 int dm_merge_bands_end(dm_grid* g, dm_cluster* out, int64_t cap, int64_t* n_out);
+/* The largest band cluster count K of the last collected merge (every rank
+ * merges the same gathered records, so every rank reads the same value: a
+ * caller can size rec_cap for the next exports from it consistently). */
+int dm_merge_max_band_k(const dm_grid* g, int64_t* max_k);
 
 /* LD06 driver point (ldlidar::PointData fields the LaserScan conversion uses). */
 typedef struct dm_ld06_point {

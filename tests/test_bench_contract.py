@@ -78,6 +78,18 @@ def test_r02_headline_fields():
     assert d["value"] >= 1e10 and d["frontier_ms"] < 2.0 and d["cpu_baseline"]["value"] > 0
 
 
+def test_bench_spawned_ranks_fail_together():
+    """`--gpus 2` without a launcher spawns two rank processes; here (no GPU)
+    they fail at the device call, and bench.py must exit non-zero promptly
+    rather than hang or report a line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = ""
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1",
+                          "--cpu-seconds", "0"], capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode != 0
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+
+
 def test_bench_parser_knows_every_config():
     out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--help"],
                          capture_output=True, text=True, timeout=60)

@@ -146,28 +146,13 @@ def _device_exchange(handles, rec_cap):
 
 
 def _exchange_like_sharded_mapper(handles, rec_cap):
-    """The multi-process layer's protocol (dm/sharded.py): a pass whose band
-    record is incomplete (slot arrays or record capacity too small on fresh
-    band handles) has no result; the host fallback runs every band's own
-    frontiers() (which grows its slots and sets its sort hint) and the
-    capacity grows; the next device exchange must then succeed."""
+    """The multi-process layer's protocol (dm/sharded.py) on fresh band
+    handles: slot arrays are sized for the map at dm_create and the record
+    capacity for the band (a cluster per two tiles, as ShardedMapper does),
+    so the FIRST device exchange must succeed — no incomplete record, no host
+    fallback."""
     got, got_last, max_k = _device_exchange(handles, rec_cap)
-    reasons = []
-    # dm/sharded.py falls back (host merge, capacities grown) on every
-    # incomplete pass, so more than one fallback is allowed here too: a slot
-    # shard region can overflow again on the next pass (which tiles share a
-    # region depends on the order the tile kernels take them)
-    for _ in range(3):
-        if got is not None:
-            break
-        reasons.append(getattr(handles[0], "last_incomplete", None))
-        for h in handles:
-            h.frontiers()
-        while rec_cap < max_k:
-            rec_cap *= 2
-        got, got_last, max_k = _device_exchange(handles, rec_cap)
-    if reasons:
-        print("device exchange fallbacks:", reasons)
+    assert got is not None, ("device exchange fell back", getattr(handles[0], "last_incomplete", None))
     return got, got_last, max_k
 
 
@@ -241,7 +226,11 @@ def test_c5_full_map_vs_band_oracle_and_band_handles(oracle_lib, n_beams, n_batc
                     h.integrate(poses[keep], ranges[keep], amin, inc)
         for r, h in enumerate(handles):
             np.testing.assert_array_equal(h.state(), st[h.row0:h.row0 + h.rows], err_msg=f"band {r}")
-        got, got_last, max_k = _exchange_like_sharded_mapper(handles, 1 << 14)
+        tiles = -(-handles[0].width // 64) * -(-handles[0].rows // 64)
+        rec_cap = 1 << 14
+        while rec_cap < tiles // 2:  # ShardedMapper's up-front sizing
+            rec_cap *= 2
+        got, got_last, max_k = _exchange_like_sharded_mapper(handles, rec_cap)
         assert got is not None, max_k
         np.testing.assert_array_equal(got, exp_clusters)
         np.testing.assert_array_equal(got_last, exp_clusters)

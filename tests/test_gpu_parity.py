@@ -337,10 +337,10 @@ def test_colocated_scans_heavy_slab_widths(oracle_lib, S):
 
 @pytest.mark.parametrize("S,N", [(1, 360), (1, 512), (1, 513), (2, 256), (1, 1100), (3, 400)])
 def test_heavy_apply_skip_boundary(oracle_lib, S, N):
-    """Co-located scans around the bound below which dm_launch_integrate
-    skips k_heavy_apply (a tile gets <= 1 piece per beam, <= 2 when beams are
-    chunked: no tile can exceed kMedium = 1024 pieces).  Above the bound the
-    sensor tile may be heavy and must be applied."""
+    """Co-located scans around the bound below which no tile can be heavy
+    (a tile gets <= 1 piece per beam, <= 2 when beams are chunked: no tile can
+    exceed kMedium = 1024 pieces).  Above the bound the sensor tile may be
+    heavy and must be applied."""
     p = cases.make_params(700, 600, resolution=0.02)
     rng = np.random.Generator(np.random.PCG64(100 + N + S))
     poses = np.tile(np.array([[0.011, 0.017, 0.2]]), (S, 1))
@@ -356,19 +356,13 @@ def test_heavy_apply_skip_boundary(oracle_lib, S, N):
         assert_frontiers_equal(m.frontiers(want_mask=True, want_labels=True), *om.frontiers())
 
 
-@pytest.mark.parametrize("separate", [False, True])
 @pytest.mark.parametrize("S", [6, 17])
-def test_heavy_apply_fused_and_separate(oracle_lib, monkeypatch, S, separate):
+def test_heavy_apply_ticket(oracle_lib, S):
     """Heavy tiles applied by their last k_tile_accum item (the ticket in
-    heavy_done, default) or by the separate k_heavy_apply launch
-    (DM_HEAVY_SEPARATE=1, read at dm_create): both bit-exact against the
-    oracle over several calls (the tickets are reset by the finisher for the
-    next call), with three sensors sharing the batch (several heavy tiles per
-    call; S=17 puts > 65535 pieces on one tile: wide slab)."""
-    if separate:
-        monkeypatch.setenv("DM_HEAVY_SEPARATE", "1")
-    else:
-        monkeypatch.delenv("DM_HEAVY_SEPARATE", raising=False)
+    heavy_done): bit-exact against the oracle over several calls (the
+    tickets are reset by the finisher for the next call), with three sensors
+    sharing the batch (several heavy tiles per call; S=17 puts > 65535
+    pieces on one tile: wide slab)."""
     p = cases.make_params(500, 400)
     rng = np.random.Generator(np.random.PCG64(31 + S))
     centres = np.array([[0.013, -0.021, 0.3], [4.41, 2.07, 1.1], [-6.3, -3.9, 2.0]])

@@ -252,10 +252,8 @@ def test_front_end_gate_timeout_is_a_sticky_error(oracle_lib, monkeypatch):
     p, batches, amin, inc = cases.world_case(49, 600, 500, 0.05, 4, 720, 2, region_frac=0.7)
     dev = _device_batches(batches)
     monkeypatch.setenv("DM_FAULT_GATE", "1")
-    monkeypatch.setenv("DM_FE_GATE", "1")  # the seq-gate hand-off (events are the default)
     with dm.OccupancyMapper(p) as m:
         monkeypatch.delenv("DM_FAULT_GATE")
-        monkeypatch.delenv("DM_FE_GATE")
         # a first call without overlap fills workspace set 0; the faulted
         # calls then find stale items in both sets
         pose4, rng = dev[0]

@@ -159,3 +159,40 @@ def test_mapping_node_shards_over_dm_devices(oracle_lib):
         assert [c.label for c in node.frontier_pub.messages[-1]] == exp["label"].tolist()
     finally:
         node.destroy_node()
+
+
+def test_sharded_ld06_device_then_integrate_device_without_host_sync(oracle_lib):
+    """dm_ld06_to_scans_device writes the scans on band 0's stream; the next
+    dm_integrate_device must order every band's reads after it (ADVICE r3:
+    bands 1..P-1 run on their own streams).  No host synchronisation between
+    the two calls; the ranges buffer starts with values the LD06 kernel
+    overwrites, so a band that read early would integrate them."""
+    import torch
+
+    p = cases.make_params(500, 1200)
+    world = synth.make_world(5, -12.5, -30.0, 12.5, 30.0)
+    rng = np.random.Generator(np.random.PCG64(8))
+    S, N = 24, 450
+    poses = np.array([[rng.uniform(-10, 10), rng.uniform(-28, 28), rng.uniform(-3, 3)] for _ in range(S)])
+    revs = [synth.ld06_points(world, x, y, yaw, rng) for x, y, yaw in poses]
+    pts = np.ascontiguousarray(np.concatenate(revs), dtype=np.dtype(_ffi.LD06_POINT_DTYPE))
+    off = np.cumsum([0] + [len(r) for r in revs]).astype(np.int64)
+    inc = float(synth.ld06_angle_increment(N))
+    er, _ = oracle_lib.ld06_to_scans(pts, off, N, True)
+    om = oracle_lib.OracleMap(p)
+    om.integrate(poses, er, 0.0, inc)
+    d_pts = torch.from_numpy(pts.view(np.uint8).copy()).cuda()
+    d_off = torch.from_numpy(off).cuda()
+    d_pose4 = torch.from_numpy(synth.pose4(poses)).cuda()
+    for devices in ([0, 0, 0], [0, 0, 0, 0, 0]):
+        d_rng = torch.full((S, N), 5.0, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        with dm.OccupancyMapper(p, devices=devices) as sh:
+            sh.set_overlap(True)
+            lib, h = sh._lib, sh._handle()
+            assert lib.dm_ld06_to_scans_device(h, S, ctypes.c_void_p(d_pts.data_ptr()),
+                                               ctypes.c_void_p(d_off.data_ptr()), N, 1,
+                                               ctypes.c_void_p(d_rng.data_ptr()), None) == 0
+            sh.integrate_device(d_pose4.data_ptr(), S, d_rng.data_ptr(), N, 0.0, inc)
+            np.testing.assert_array_equal(sh.state(), om.state)
+            np.testing.assert_array_equal(sh.logodds().view(np.uint32), om.L.view(np.uint32))

@@ -3,9 +3,7 @@
 The frontier pipeline orders its cluster records by label with one of three
 device sorts (csrc/dm_frontier.hip): the O(K^2) rank sort, or, once the last
 collected pass of the handle had more than sort_min (4096) clusters, the
-row-bucket sort (k_rs_count / k_rs_scan / k_rs_place / k_rs_rank, the
-default) or the LSD radix sort (k_rx_*, DM_LARGE_SORT=radix).  Every large-K
-test runs with both.
+row-bucket sort (k_rs_count / k_rs_scan / k_rs_place / k_rs_rank).
 Either must give the oracle's list bit for bit whatever the count of the pass
 it actually sorts, including a small pass sorted by the bucket path after a
 large one, the pipelined begin/end passes and the cross-band merge.
@@ -33,23 +31,11 @@ def _oracle_clusters(oracle_lib, p, st):
     return om.frontiers()
 
 
-LARGE_SORTS = ["row", "radix"]
-
-
-def _set_large_sort(monkeypatch, large_sort):
-    """DM_LARGE_SORT for the handle created next; "row-dma" is the row sort
-    with the opt-in DMA readback of large record lists (DM_DMA_READBACK=1)."""
-    monkeypatch.setenv("DM_LARGE_SORT", "radix" if large_sort == "radix" else "row")
-    monkeypatch.setenv("DM_DMA_READBACK", "1" if large_sort == "row-dma" else "0")
-
-
 # K: 26k (> kBucketSortMin, < the rank sort's 65536 cap), 105k (> both)
-@pytest.mark.parametrize("large_sort", LARGE_SORTS + ["row-dma"])
 @pytest.mark.parametrize("R,W,seed", [(512, 512, 1), (1024, 1024, 2)])
-def test_bucket_sort_band(oracle_lib, monkeypatch, R, W, seed, large_sort):
+def test_bucket_sort_band(oracle_lib, monkeypatch, R, W, seed):
     import dm
 
-    _set_large_sort(monkeypatch, large_sort)
     big = sparse_state(seed, R, W)
     small = cases.blob_state(seed, R, W, n_blobs=40)      # a few dozen clusters
     mid = cases.random_state(seed + 7, R, W)              # a few thousand
@@ -75,11 +61,9 @@ def test_bucket_sort_band(oracle_lib, monkeypatch, R, W, seed, large_sort):
             np.testing.assert_array_equal(fr.clusters, exp_big[2])
 
 
-@pytest.mark.parametrize("large_sort", LARGE_SORTS)
-def test_bucket_sort_min_size_filter(oracle_lib, monkeypatch, large_sort):
+def test_bucket_sort_min_size_filter(oracle_lib, monkeypatch):
     import dm
 
-    _set_large_sort(monkeypatch, large_sort)
     st = cases.random_state(5, 768, 640, p_free=0.45, p_occ=0.05)
     p = cases.make_params(640, 768, min_frontier_size=3)
     exp = _oracle_clusters(oracle_lib, p, st)
@@ -90,16 +74,14 @@ def test_bucket_sort_min_size_filter(oracle_lib, monkeypatch, large_sort):
         assert_frontiers_equal(m.frontiers(want_mask=True, want_labels=True), *exp)
 
 
-@pytest.mark.parametrize("large_sort", LARGE_SORTS)
 @pytest.mark.parametrize("P", [2, 4])
-def test_bucket_sort_merge(oracle_lib, monkeypatch, P, large_sort):
+def test_bucket_sort_merge(oracle_lib, monkeypatch, P):
     """Cross-band merge of ~105k clusters: rank sort cap exceeded first (host
     sort), then the bucket sort over global rows."""
     import dm
     import torch
     from dm.sharded import band_params
 
-    _set_large_sort(monkeypatch, large_sort)
     R, W = 1024, 1024
     st = sparse_state(2, R, W)
     p = cases.make_params(W, R)
@@ -138,16 +120,14 @@ def test_bucket_sort_merge(oracle_lib, monkeypatch, P, large_sort):
             b.close()
 
 
-@pytest.mark.parametrize("large_sort", LARGE_SORTS)
 @pytest.mark.parametrize("R,W,rows", [(64, 65536, 3), (2048, 16384, 1)])
-def test_radix_sort_clusters_packed_in_few_rows(oracle_lib, monkeypatch, R, W, rows, large_sort):
+def test_row_sort_clusters_packed_in_few_rows(oracle_lib, monkeypatch, R, W, rows):
     """Clusters packed in a few rows (the round-2 bucket sort's worst case:
     one label bucket holding most records; for the row sort, rows of 8-32 k
     records: its O(b^2) worst case, slow but exact) and a wide label range;
     the second pass is sorted by the large-K path (hint from the first)."""
     import dm
 
-    _set_large_sort(monkeypatch, large_sort)
     st = np.full((R, W), -1, np.int8)
     for k in range(rows):
         st[R // 2 + 2 * k, ::2] = 0  # isolated free cells: W / 2 clusters per row

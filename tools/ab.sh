@@ -14,6 +14,6 @@ for r in $(seq $R); do
     tag=${v%%:*}; envs=${v#*:}
     env ${envs//,/ } timeout -k 10 120 python -u bench.py --steps 400 --warmup 40 --cpu-seconds 0 --profile-steps ${AB_PROFILE_STEPS:-0} \
       --no-explored --no-host-inputs ${BENCH_ARGS[$tag]} > gpurun_out/ab_tmp.log 2>&1 || { echo "$tag failed"; tail -5 gpurun_out/ab_tmp.log; exit 1; }
-    python -c "import json; d=json.loads(open('gpurun_out/ab_tmp.log').read().strip().splitlines()[-1]); s=d.get('launch_batching') or {}; print('$tag', round(d['value']/1e9,1), 'e9', round(d['ms_per_step']*1e3,1), 'us/step', 'p50', round(d['step_wall_us']['p50'],1), 'graphs', s.get('graph_launches'), 'hits', s.get('graph_hits'), 'misses', s.get('graph_misses'), {k: round(v*1e3,1) for k, v in (d.get('kernel_avg_ms') or {}).items()})" | tee -a $OUT
+    python -c "import json; d=json.loads(open('gpurun_out/ab_tmp.log').read().strip().splitlines()[-1]); print('$tag', round(d['value']/1e9,1), 'e9', round(d['ms_per_step']*1e3,1), 'us/step', 'p50', round(d['step_wall_us']['p50'],1), {k: round(v*1e3,1) for k, v in (d.get('kernel_avg_ms') or {}).items()})" | tee -a $OUT
   done
 done
