@@ -814,7 +814,7 @@ def run_config(args):
         "data": "synthetic: seeded rectangle world, random-walk robots, LD06-format scans",
     }
     mapper = dm.OccupancyMapper(params, device=dev_i)
-    mapper.set_overlap(True)
+    mapper.set_overlap(not args.no_overlap)  # PMC passes: --no-overlap (one dispatch at a time)
     try:
         if args.config in ("C1", "C2"):
             out = _run_replay(args, np, torch, synth, mapper, params, amin, dev)
@@ -975,6 +975,17 @@ def _run_c5(args, np, torch, synth, m, params, amin, dev, world):
         mean = lambda key: float(np.mean([st[key] for st in stats]))  # noqa: E731
         avg, roof = _profiled_roofline(m, lambda: [(integrate(k), m.frontiers()) for k in range(5)],
                                        mean("updates"), mean("touched"))
+        # PMC traffic of this sweep point (tools/pmc_passes.sh over
+        # `bench.py --config C5 --sweep N`, workload "C5-N"), when measured
+        # on these sources
+        wl = f"C5-{N}"
+        traffic, tsrc = pmc_traffic("k_tile_accum", wl)
+        roof["traffic"], roof["traffic_source"] = traffic, tsrc
+        if traffic and roof["avg_launch_ms"] > 0:
+            roof["frac_traffic"] = traffic / (roof["avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS
+        F_cells = int(fr.clusters["size"].sum()) if fr is not None and len(fr) else 0
+        roof["frontier"] = frontier_roofline(avg, 65536 * 65536, F_cells, len(fr) if fr is not None else 0,
+                                             fst["frontier_tiles"], wl, float(np.median(tf)))
         rows.append({"beams_per_scan": N, "value": U / elapsed,
                      "ms_per_step": elapsed / args.steps * 1e3,
                      "integrate_ms": float(np.median(ti)) * 1e3,

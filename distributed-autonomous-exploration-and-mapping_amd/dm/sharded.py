@@ -199,7 +199,9 @@ class ShardedMapper:
                 self._tdev = torch.device("cuda", device)
                 # the band's map stream: its map kernels and the halo-row
                 # all-gather between them (RCCL orders itself against it)
-                self.stream = torch.cuda.Stream(device=self._tdev)
+                # (high priority, as libdm's own map stream: the front-end
+                # stream fills what the map chain leaves idle)
+                self.stream = torch.cuda.Stream(device=self._tdev, priority=-1)
                 self.band.set_stream(self.stream.cuda_stream)
                 # the export records are all-gathered on the band's exchange
                 # stream (its pass stream with overlap on), over a second

@@ -48,6 +48,14 @@ for s in "$@"; do
       bash $R/tools/pmc_passes.sh gpurun_out/pmcx python3 $R/tools/frontier_probe.py --passes 5; rc=$?; ok $rc || exit $rc
       python $R/tools/pmc_summary.py $OUT/pmcx $R/profiles/pmc_latest.json C3-explored > $OUT/pmcx_summary.log 2>&1 || exit 1
       cp $R/profiles/pmc_latest.json $OUT/pmc_latest.json ;;
+    pmc5)
+      # PMC passes per C5 sweep point -> profiles/pmc_latest.json [C5-N]
+      for n in 12 48 192 768 4096; do
+        bash $R/tools/pmc_passes.sh gpurun_out/pmc5_$n python3 $R/bench.py --config C5 --sweep $n --steps 5 \
+          --warmup 2 --pool 2 --cpu-seconds 0 --no-overlap || exit 1
+        python $R/tools/pmc_summary.py $OUT/pmc5_$n $R/profiles/pmc_latest.json C5-$n >> $OUT/pmc5_summary.log 2>&1 || exit 1
+      done
+      cp $R/profiles/pmc_latest.json $OUT/pmc_latest.json ;;
     cfg:*)
       c=${s#cfg:}
       timeout -k 10 400 python -u bench.py --config $c --cpu-seconds 10 > $OUT/bench_$c.log 2>&1
