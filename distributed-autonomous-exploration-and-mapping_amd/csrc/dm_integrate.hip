@@ -30,6 +30,7 @@
 
 DM_PH_DECL(integrate)
 DM_TL_DECL(accum)
+DM_TL_DECL(daccum)
 
 namespace {
 
@@ -1260,6 +1261,8 @@ __global__ __launch_bounds__(kQuarter, DM_DIRECT_OCC) void k_direct_accum(
   __shared__ uint32_t s_U;
   __shared__ unsigned long long s_accT, s_accU, s_accP;
   const int tid = threadIdx.x, lane = lane_id();
+  DM_TL_BEGIN();
+  [[maybe_unused]] unsigned long long tl_word = 0;  // timeline (phase build): items | finisher ticks << 32
   // halt word, item counts and this workgroup's first item in ONE round: the
   // item's index does not depend on the counts (regions at fixed offsets)
   const unsigned long long hv = *halt;
@@ -1269,7 +1272,10 @@ __global__ __launch_bounds__(kQuarter, DM_DIRECT_OCC) void k_direct_accum(
   const int64_t end = d.a_cap + NB;
   int4 item;
   bool valid = blockIdx.x < end && item_at(d, items, blockIdx.x, NA, NB, &item);
-  if (hv != 0ull) return;
+  if (hv != 0ull) {
+    DM_TL_END(daccum, 0);
+    return;
+  }
   for (int e = tid; e < kTileWords; e += kQuarter) tl[e] = 0u;
   if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; s_accT = 0ull; s_accU = 0ull; s_accP = 0ull; }
   __syncthreads();
@@ -1279,6 +1285,7 @@ __global__ __launch_bounds__(kQuarter, DM_DIRECT_OCC) void k_direct_accum(
     if (it != (int64_t)blockIdx.x) valid = item_at(d, items, it, NA, NB, &item);
     const int32_t tile = __builtin_amdgcn_readfirstlane(item.x);
     if (!valid || tile < 0) continue;  // past the counts, or a dead region-A slot
+    tl_word += 1;
     const int32_t uid = __builtin_amdgcn_readfirstlane(item.y);
     const int32_t c0 = __builtin_amdgcn_readfirstlane(item.z);
     const int32_t cn = __builtin_amdgcn_readfirstlane(item.w);
@@ -1372,6 +1379,9 @@ __global__ __launch_bounds__(kQuarter, DM_DIRECT_OCC) void k_direct_accum(
       if (tid == 0) s_last = atomicAdd(&heavy_done[slab], 1) == n_it - 1;
       __syncthreads();
       if (s_last) {
+#ifdef DM_PHASE_TIMING
+        const long long tf0 = wall_clock64();
+#endif
         for (int q = 0; q < 4; ++q) heavy_quarter(g, p, slab, q, tile, wide, slabs, L, state, &s_T, &s_free, &s_U);
         __syncthreads();
         if (tid == 0) {
@@ -1381,6 +1391,9 @@ __global__ __launch_bounds__(kQuarter, DM_DIRECT_OCC) void k_direct_accum(
           tile_head[tile] = -1;
           tile_slab[tile] = -1;
         }
+#ifdef DM_PHASE_TIMING
+        tl_word += (unsigned long long)(wall_clock64() - tf0) << 32;
+#endif
       }
     }
     __syncthreads();
@@ -1394,6 +1407,7 @@ __global__ __launch_bounds__(kQuarter, DM_DIRECT_OCC) void k_direct_accum(
     if (s_accU) atomicAdd(&sh[SH_U], s_accU);
     if (s_accP) atomicAdd(&sh[SH_P], s_accP);
   }
+  DM_TL_END(daccum, tl_word);
 }
 
 // fmask records of the tiles the direct front-end's items touched (whole
@@ -1668,6 +1682,7 @@ int grid_for(int64_t n, int threads, int64_t cap = 8192) {
 
 DM_PH_READER(integrate)
 DM_TL_READER(accum)
+DM_TL_READER(daccum)
 
 namespace {
 

@@ -53,6 +53,9 @@ def generate_launch_description():
             'dm_width': LaunchConfiguration('dm_width'),
             'dm_height': LaunchConfiguration('dm_height'),
             'dm_device': LaunchConfiguration('dm_device'),
+            # e.g. dm_devices:=0,1,2,3,4,5,6,7: one map sharded in row bands
+            # over these GPUs (dm_create_sharded); empty: one GPU (dm_device)
+            'dm_devices': LaunchConfiguration('dm_devices'),
             'dm_explore': LaunchConfiguration('dm_explore'),
         }],
     )
@@ -74,6 +77,7 @@ def generate_launch_description():
         DeclareLaunchArgument('dm_width', default_value='4096'),
         DeclareLaunchArgument('dm_height', default_value='4096'),
         DeclareLaunchArgument('dm_device', default_value='0'),
+        DeclareLaunchArgument('dm_devices', default_value=''),
         DeclareLaunchArgument('dm_explore', default_value='false'),
         slam_launch,
         dm_mapper,

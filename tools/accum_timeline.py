@@ -30,7 +30,7 @@ from dm import synth  # noqa: E402
 TICK_US = 0.01  # wall_clock64: 100 MHz
 
 
-def run(steps, overlap=True):
+def run(steps, overlap=True, mode="binned"):
     G, res, S, N = 16384, 0.05, 64, 4096
     half = G * res / 2
     world = synth.make_world(0, -half, -half, half, half)
@@ -41,10 +41,12 @@ def run(steps, overlap=True):
     torch.cuda.synchronize()
     amin, inc = float(synth.LD06_ANGLE_MIN), float(synth.ld06_angle_increment(N))
     lib = dm._ffi.load_library()
-    rd = lib.dm_debug_timeline_accum
+    # binned front-end -> k_tile_accum's record, direct -> k_direct_accum's
+    rd = lib.dm_debug_timeline_accum if mode == "binned" else lib.dm_debug_timeline_daccum
     rd.argtypes = [ctypes.c_void_p, ctypes.c_int]
     m = dm.OccupancyMapper(dm.default_params(G, G, resolution=res))
     m.set_overlap(overlap)
+    m.set_integrate_mode(mode)
     pending = 0
     for k in range(steps):
         p4, r = dpool[k % len(dpool)]
@@ -112,23 +114,25 @@ def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 30
     js = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
     res = {}
-    for mode in ("pipelined", "alone"):
-        tl = run(steps, overlap=(mode == "pipelined"))
-        res[mode] = summarise(tl)
-        r = res[mode]
-        print(f"[{mode}] workgroups {r['workgroups']} (with items {r['with_items']}), span {r['span_us']:.1f} us, "
-              f"last start {r['last_start_us']:.1f} us, idle wgs last start {r['last_idle_start_us']}")
-        print(f"  item wg duration {r['item_wg_duration_us']}")
-        print(f"  item wg end      {r['item_wg_end_us']}")
-        print(f"  idle wg mean duration {r['idle_wg_duration_us_mean']}")
-        print(f"  heavy finishers {r['finishers']}")
-        print(f"  tail {r['tail']}")
-        print(f"  per-XCC end {r['per_xcc_end_us']}")
-        print(f"  per-XCC items {r['per_xcc_items']}")
-        print("  us : starts / item starts / resident / resident with items")
-        for b in range(len(r["resident"])):
-            print(f"  {b:3d}: {r['starts_per_us'][b]:5d} {r['item_starts_per_us'][b]:5d} {r['resident'][b]:5d} "
-                  f"{r['resident_with_items'][b]:5d}")
+    for fe in ("binned", "direct"):
+        for pm in ("pipelined", "alone"):
+            mode = f"{fe} {pm}"
+            tl = run(steps, overlap=(pm == "pipelined"), mode=fe)
+            res[mode] = summarise(tl)
+            r = res[mode]
+            print(f"[{mode}] workgroups {r['workgroups']} (with items {r['with_items']}), span {r['span_us']:.1f} us, "
+                  f"last start {r['last_start_us']:.1f} us, idle wgs last start {r['last_idle_start_us']}")
+            print(f"  item wg duration {r['item_wg_duration_us']}")
+            print(f"  item wg end      {r['item_wg_end_us']}")
+            print(f"  idle wg mean duration {r['idle_wg_duration_us_mean']}")
+            print(f"  heavy finishers {r['finishers']}")
+            print(f"  tail {r['tail']}")
+            print(f"  per-XCC end {r['per_xcc_end_us']}")
+            print(f"  per-XCC items {r['per_xcc_items']}")
+            print("  us : starts / item starts / resident / resident with items")
+            for b in range(len(r["resident"])):
+                print(f"  {b:3d}: {r['starts_per_us'][b]:5d} {r['item_starts_per_us'][b]:5d} {r['resident'][b]:5d} "
+                      f"{r['resident_with_items'][b]:5d}")
     if js:
         with open(js, "w") as f:
             json.dump(res, f)
