@@ -547,6 +547,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   }
   if ((rc = dev_alloc(&g->tile_free, g->NT, "tile free counts"))) return fail(rc);
   if ((rc = dev_alloc(&g->fmask, g->NT * DM_TILE * 16, "tile free / unknown bit rows"))) return fail(rc);
+  if ((rc = dev_alloc(&g->fedge, g->NT * 4, "tile unknown edge words"))) return fail(rc);
   // The five run-time switches (read once, here): DM_SPARSE_PIECES (0: no
   // sparse work items), DM_FMASK=on|off (fmask maintenance forced either way),
   // DM_FRONTIER_KERNEL=wave|wg (one frontier tile kernel for every pass),
@@ -585,10 +586,11 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if ((rc = dev_alloc(&g->edge_label, 2 * g->W, "edge labels"))) return fail(rc);
   if ((rc = dev_alloc(&g->halo, 2 * g->W, "halo rows"))) return fail(rc);
   // slot arrays sized for the map up front (a pass that overflows them has
-  // no result and must be rerun): two tile-local components per tile, ~276 B
-  // each (C3: 36 MB; a 65536^2 map: 0.6 GB of its 288 GB).  C5's sparse rays
-  // need ~8 per listed tile, i.e. at most 0.4 per tile of the map.
-  if ((rc = grow_slots(g, std::max<int64_t>(1 << 16, 2 * g->NT)))) return fail(rc);
+  // no result and must be rerun): kSlotsPerTile tile-local components per
+  // tile, ~276 B each (C3: 72 MB; a 65536^2 map: 1.2 GB of its 288 GB).  A
+  // C5 row band under 64 x 4096-beam fans holds 0.81 clusters per tile and
+  // more than two slots per tile (test_gpu_c5_full.py).
+  if ((rc = grow_slots(g, std::max<int64_t>(1 << 16, kSlotsPerTile * g->NT)))) return fail(rc);
   dm_select_fw(g, g->fparity);
   for (int sl = 0; sl <= dm_grid::kRbSlots; ++sl)
     if ((rc = grow_host_out(g, sl, 1 << 14))) return fail(rc);
@@ -673,7 +675,7 @@ int dm_destroy(dm_grid* g) {
     dev_free(w.units); dev_free(w.ditems); dev_free(w.tile_head); dev_free(w.tile_cand); dev_free(w.tile_slab);
     dev_free(w.pose4); dev_free(w.ranges);
   }
-  dev_free(g->L); dev_free(g->state); dev_free(g->fmask);
+  dev_free(g->L); dev_free(g->state); dev_free(g->fmask); dev_free(g->fedge);
   dev_free(g->tile_free); dev_free(g->beams); dev_free(g->blk_hist); dev_free(g->blk_n);
   dev_free(g->trig);
   dev_free(g->bs_key); dev_free(g->bs_key2); dev_free(g->bs_idx); dev_free(g->bs_idx2);

@@ -704,15 +704,16 @@ __device__ inline uint64_t nib_row(uint4 v, int shift) {
 // with dm_set_overlap the next batch's map update may start right after it,
 // while the labelling kernels below (which read only these rows) run on the
 // pass stream.  The map is read as the per-tile free / unknown bit rows
-// (fmask, kept by the integrate apply): the tile's 2 x 512 B, the unknown
-// rows of its left / right neighbours (bit 63 / bit 0 of each) and one word
-// of each of the six tiles above and below — ~2 KB of coalesced loads
-// instead of the tile's 4 KB of state bytes plus ~130 scattered halo lines.
+// (fmask, kept by the integrate apply): the tile's 1 KB record, and one edge
+// word (fedge) of each of its 8 neighbours — 1 KB of coalesced loads plus 8
+// uniform 8-byte ones instead of the tile's 4 KB of state bytes plus ~130
+// scattered halo lines (or the neighbours' whole records for one byte per row).
 // Tiles next to a band halo (sharded maps) read the state bytes and the
 // halo rows instead.  Also copies the list length into the pass's counters.
 __global__ __launch_bounds__(kFW * 64) void k_frontier_bits(FGeom g, const int8_t* __restrict__ state,
                                                             const int8_t* __restrict__ halo,
                                                             const uint8_t* __restrict__ fmask,
+                                                            const uint64_t* __restrict__ fedge,
                                                             const int32_t* __restrict__ ftiles,
                                                             const unsigned long long* __restrict__ list_n,
                                                             uint64_t* __restrict__ fbits,
@@ -737,22 +738,22 @@ __global__ __launch_bounds__(kFW * 64) void k_frontier_bits(FGeom g, const int8_
       const uint4 v = *reinterpret_cast<const uint4*>(rec + lane * 16);
       Fr = nib_row(v, 0);
       U = nib_row(v, 4);
-      // column -1: the left tile's byte 15 bit 7; column 64: the right tile's
-      // byte 0 bit 4
-      uL = tx > 0 ? (uint32_t)(rec[lane * 16 + 15 - DM_TS * 16] >> 7) : 0u;
-      uR = tx + 1 < g.TX ? (uint32_t)((rec[lane * 16 + DM_TS * 16] >> 4) & 1u) : 0u;
+      // the neighbours from their edge words (fedge: unknown column 0,
+      // column 63, row 0, row 63): column -1 is the left tile's column 63,
+      // column 64 the right tile's column 0
+      uL = tx > 0 ? (uint32_t)((fedge[(int64_t)(tile - 1) * 4 + 1] >> lane) & 1ull) : 0u;
+      uR = tx + 1 < g.TX ? (uint32_t)((fedge[(int64_t)(tile + 1) * 4] >> lane) & 1ull) : 0u;
       // lane 0: row -1 (the tile above, its row 63); lane 63: row 64 (the
       // tile below, its row 0); eL / eR the diagonal neighbours' corner cells
       Ue = 0ull;
       eL = 0u;
       eR = 0u;
-      const int32_t dy = lane == 0 ? -1 : 1;
       if ((lane == 0 && ty > 0) || (lane == 63 && ty + 1 < g.TY)) {
-        const int64_t nt = (int64_t)tile + (int64_t)dy * g.TX;
-        const int row = lane == 0 ? DM_TS - 1 : 0;
-        Ue = nib_row(*reinterpret_cast<const uint4*>(fmask + nt * (DM_TS * 16) + row * 16), 4);
-        if (tx > 0) eL = (uint32_t)(fmask[(nt - 1) * (DM_TS * 16) + row * 16 + 15] >> 7);
-        if (tx + 1 < g.TX) eR = (uint32_t)((fmask[(nt + 1) * (DM_TS * 16) + row * 16] >> 4) & 1u);
+        const int64_t nt = (int64_t)tile + (lane == 0 ? -(int64_t)g.TX : (int64_t)g.TX);
+        const int wr = lane == 0 ? 3 : 2;
+        Ue = fedge[nt * 4 + wr];
+        if (tx > 0) eL = (uint32_t)(fedge[(nt - 1) * 4 + wr] >> 63);
+        if (tx + 1 < g.TX) eR = (uint32_t)(fedge[(nt + 1) * 4 + wr] & 1ull);
       }
     }
     const uint64_t h = dilate_row(U, uL, uR);
@@ -1717,7 +1718,7 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
                       g->ftf_hint <= kDenseMaxTiles);
   dm_timer_begin(g, "frontier_bits", &t);
   DM_LAUNCH(k_frontier_bits, dim3(wave_grid), dim3(kFW * 64), 0, g->stream, fg, g->state, g->halo,
-                     g->fmask, g->ftiles, list_n, g->fbits, g->cnt, g->fmask_on ? 1 : 0,
+                     g->fmask, g->fedge, g->ftiles, list_n, g->fbits, g->cnt, g->fmask_on ? 1 : 0,
                      dense ? nullptr : g->big_tiles);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());

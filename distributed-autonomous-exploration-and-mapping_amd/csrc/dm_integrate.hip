@@ -449,6 +449,49 @@ __device__ inline uint8_t state_nibbles_at(const G& g, const int8_t* __restrict_
   return (uint8_t)(fn | (un << 4));
 }
 
+// Bits 0, 4, ..., 60 of x packed into bits 0..15.
+__device__ inline uint32_t every4th(uint64_t x) {
+  x &= 0x1111111111111111ull;
+  x = (x | (x >> 3)) & 0x0303030303030303ull;
+  x = (x | (x >> 6)) & 0x000F000F000F000Full;
+  x = (x | (x >> 12)) & 0x000000FF000000FFull;
+  return (uint32_t)((x | (x >> 24)) & 0xFFFFull);
+}
+
+// A tile's edge words (fedge, dm_internal.h) from the fmask stores of one
+// wave: lane l holds the 4 nibble bytes `out` of 16-cell chunk l % 4 of tile
+// row 16 q + l / 4 (every lane calls, in step: ballots and shuffles).
+struct EdgeAcc {
+  uint64_t w[4] = {0ull, 0ull, 0ull, 0ull};  // unknown column 0, column 63, row 0, row 63
+};
+__device__ inline void edge_acc(EdgeAcc& e, uint32_t out, int q, int lane) {
+  const int c = lane & 3;
+  const uint64_t b0 = __ballot(c == 0 && ((out >> 4) & 1u));   // cell 0's unknown bit
+  const uint64_t b3 = __ballot(c == 3 && ((out >> 31) & 1u));  // cell 63's
+  e.w[0] |= (uint64_t)every4th(b0) << (16 * q);
+  e.w[1] |= (uint64_t)every4th(b3 >> 3) << (16 * q);
+  if (q == 0 || q == 3) {  // rows 0 (lanes 0..3) and 63 (lanes 60..63)
+    const uint32_t u16 = ((out >> 4) & 0xFu) | ((out >> 8) & 0xF0u) | ((out >> 12) & 0xF00u) | ((out >> 16) & 0xF000u);
+    const int base = q == 0 ? 0 : 60;
+    uint64_t r = 0ull;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r |= (uint64_t)__shfl(u16, base + k) << (16 * k);
+    e.w[q == 0 ? 2 : 3] = r;
+  }
+}
+
+// Lanes 0..3 store the tile's four edge words; `rows` (uniform) are the tile
+// rows this wave rewrote: the others keep their stored bits.
+__device__ inline void edge_store(const EdgeAcc& e, uint64_t* __restrict__ fedge, int64_t tile, uint64_t rows,
+                                  int lane) {
+  if (lane >= 4) return;
+  const uint64_t v = lane == 0 ? e.w[0] : lane == 1 ? e.w[1] : lane == 2 ? e.w[2] : e.w[3];
+  const uint64_t m = lane < 2 ? rows : ((rows >> (lane == 2 ? 0 : 63)) & 1ull) ? ~0ull : 0ull;
+  uint64_t* p = fedge + tile * 4 + lane;
+  if (m == ~0ull) *p = v;
+  else if (m) *p = (*p & ~m) | (v & m);
+}
+
 // Number of zero bytes of x (exact, no false positives).
 __device__ inline int32_t zero_bytes(uint32_t x) {
   uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
@@ -1415,6 +1458,7 @@ __global__ __launch_bounds__(kQuarter, DM_DIRECT_OCC) void k_direct_accum(
 __global__ __launch_bounds__(256) void k_fmask_direct(Geom g, DGeom d, const int4* __restrict__ items,
                                                       const unsigned long long* __restrict__ cnt,
                                                       const int8_t* __restrict__ state, uint8_t* __restrict__ fmask,
+                                                      uint64_t* __restrict__ fedge,
                                                       const unsigned long long* __restrict__ halt) {
   if (*halt) return;
   const int64_t NA = min((int64_t)cnt[CNT_ITEMS], d.a_cap);
@@ -1427,6 +1471,7 @@ __global__ __launch_bounds__(256) void k_fmask_direct(Geom g, DGeom d, const int
     const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
     const int32_t x0 = tx0 + (lane & 3) * 16;
     uint8_t* tm = fmask + (int64_t)tile * (DM_TS * 16);
+    EdgeAcc ea;
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
       const int ly = 16 * qq + (lane >> 2);
@@ -1444,7 +1489,9 @@ __global__ __launch_bounds__(256) void k_fmask_direct(Geom g, DGeom d, const int
         }
       }
       *reinterpret_cast<uint32_t*>(tm + ly * 16 + (lane & 3) * 4) = out;
+      edge_acc(ea, out, qq, lane);
     }
+    edge_store(ea, fedge, tile, ~0ull, lane);
   }
 }
 
@@ -1508,13 +1555,16 @@ __device__ inline uint8_t fmask_byte(uint64_t fm, uint64_t um, int j) {
 // state write (reset, dm_set_state, dm_set_logodds).  Element e of the loop
 // is cell (e & 63, e >> 6): a wave is one row.
 __global__ __launch_bounds__(256) void k_recount(Geom g, const int8_t* __restrict__ state,
-                                                 int32_t* __restrict__ tile_free, uint8_t* __restrict__ fmask) {
+                                                 int32_t* __restrict__ tile_free, uint8_t* __restrict__ fmask,
+                                                 uint64_t* __restrict__ fedge) {
   const int64_t tile = blockIdx.x;
   const int32_t tx0 = (int32_t)(tile % g.r.TX) * DM_TS, ty0 = (int32_t)(tile / g.r.TX) * DM_TS;
   __shared__ int32_t acc;
+  __shared__ uint64_t s_edge[4][4];  // per wave: unknown column 0, column 63, row 0, row 63
   if (threadIdx.x == 0) acc = 0;
   __syncthreads();
   int32_t c = 0;
+  uint64_t ew[4] = {0ull, 0ull, 0ull, 0ull};
   uint8_t* tm = fmask + tile * (DM_TS * 16);
   for (int e = threadIdx.x; e < DM_TS * DM_TS; e += 256) {
     const int32_t x = tx0 + (e & 63), y = ty0 + (e >> 6);
@@ -1522,12 +1572,21 @@ __global__ __launch_bounds__(256) void k_recount(Geom g, const int8_t* __restric
     c += b == 0;
     const uint64_t fm = __ballot(b == 0);
     const uint64_t um = __ballot(b == -1);
-    const int l = e & 63;
-    if (l < 16) tm[(e >> 6) * 16 + l] = fmask_byte(fm, um, l);
+    const int l = e & 63, r = e >> 6;  // a wave is one row
+    if (l < 16) tm[r * 16 + l] = fmask_byte(fm, um, l);
+    ew[0] |= (um & 1ull) << r;
+    ew[1] |= (um >> 63) << r;
+    if (r == 0) ew[2] = um;
+    if (r == DM_TS - 1) ew[3] = um;
   }
   if (c) atomicAdd(&acc, c);
+  const int l4 = __lane_id();
+  if (l4 < 4) s_edge[threadIdx.x >> 6][l4] = l4 == 0 ? ew[0] : l4 == 1 ? ew[1] : l4 == 2 ? ew[2] : ew[3];
   __syncthreads();
   if (threadIdx.x == 0) tile_free[tile] = acc;
+  if (threadIdx.x < 4)
+    fedge[tile * 4 + threadIdx.x] = s_edge[0][threadIdx.x] | s_edge[1][threadIdx.x] | s_edge[2][threadIdx.x] |
+                                    s_edge[3][threadIdx.x];
 }
 
 __device__ inline uint64_t upto_rows(int p) {  // bits 0..p inclusive
@@ -1547,6 +1606,7 @@ __global__ __launch_bounds__(256) void k_fmask_items(Geom g, const int4* __restr
                                                      const PackedPiece* __restrict__ pieces,
                                                      const unsigned long long* __restrict__ cnt,
                                                      const int8_t* __restrict__ state, uint8_t* __restrict__ fmask,
+                                                     uint64_t* __restrict__ fedge,
                                                      const unsigned long long* __restrict__ halt) {
   if (*halt) return;  // as k_tile_accum
   const int64_t HI = min((int64_t)cnt[cnt_a], g.hitem_cap);
@@ -1583,13 +1643,14 @@ __global__ __launch_bounds__(256) void k_fmask_items(Geom g, const int4* __restr
     const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
     const int32_t x0 = tx0 + (lane & 3) * 16;
     uint8_t* tm = fmask + (int64_t)tile * (DM_TS * 16);
+    EdgeAcc ea;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int ly = 16 * q + (lane >> 2);
-      if (!((rows >> ly) & 1ull)) continue;
+      const bool mine = (rows >> ly) & 1ull;
       const int32_t y = ty0 + ly;
       uint32_t out = 0u;
-      if (y < g.r.R) {
+      if (mine && y < g.r.R) {
         const int64_t off = (int64_t)y * g.r.W + x0;
         if (x0 + 16 <= g.r.W && (off & 15) == 0) {
           const uint4 v = *reinterpret_cast<const uint4*>(state + off);
@@ -1600,8 +1661,10 @@ __global__ __launch_bounds__(256) void k_fmask_items(Geom g, const int4* __restr
           for (int k = 0; k < 4; ++k) out |= (uint32_t)state_nibbles_at(g, state, x0 + 4 * k, y) << (8 * k);
         }
       }
-      *reinterpret_cast<uint32_t*>(tm + ly * 16 + (lane & 3) * 4) = out;
+      if (mine) *reinterpret_cast<uint32_t*>(tm + ly * 16 + (lane & 3) * 4) = out;
+      edge_acc(ea, out, q, lane);  // every lane: ballots (rows not rewritten are masked in edge_store)
     }
+    edge_store(ea, fedge, tile, rows, lane);
   }
 }
 
@@ -1728,7 +1791,7 @@ int launch_direct(dm_grid* g, dm_grid::IntWs& w, hipStream_t fs, const RayArgs& 
   }
   dm_timer_begin(g, "fmask", &t);
   DM_LAUNCH(k_fmask_direct, dim3(grid_for(d.a_cap + d.b_cap, 4, 8192)), dim3(256), 0, g->stream, ge, d, w.ditems,
-            w.cnt, g->state, g->fmask, g->fe_flag + kHaltWord);
+            w.cnt, g->state, g->fmask, g->fedge, g->fe_flag + kHaltWord);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   return DM_OK;
@@ -1824,7 +1887,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   dm_timer_begin(g, "fmask", &t);
   DM_LAUNCH(k_fmask_items, dim3(grid_for(g->hitem_cap + g->act_cap, 4, 8192)), dim3(256), 0, g->stream,
                      ge, w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS, (int)CNT_SITEMS, w.pieces, w.cnt,
-                     g->state, g->fmask,
+                     g->state, g->fmask, g->fedge,
                      g->fe_flag + kHaltWord);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
@@ -1847,7 +1910,7 @@ int dm_launch_gate(hipStream_t s, unsigned long long* flag, unsigned long long* 
 int dm_launch_recount(dm_grid* g) {
   const Geom ge = make_geom(g);
   DM_LAUNCH(k_recount, dim3((unsigned)g->NT), dim3(256), 0, g->stream, ge, g->state,
-                     g->tile_free, g->fmask);
+                     g->tile_free, g->fmask, g->fedge);
   DM_HIP(hipGetLastError());
   g->fmask_valid = true;
   return DM_OK;

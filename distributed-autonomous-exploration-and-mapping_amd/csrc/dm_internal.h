@@ -228,6 +228,11 @@ struct dm_grid {
   // kernel.  fmask_valid: the records match the state (a full rebuild,
   // k_recount, precedes switching on otherwise).
   uint8_t* fmask = nullptr;
+  // fedge: per tile 4 words, the unknown bits of its column 0, column 63
+  // (bit = row), row 0 and row 63 (bit = column), written with fmask by the
+  // same kernels: a pass reads its neighbours' edges from these 32 B instead
+  // of from their 1 KB records (one byte of every 16 B row: all 8 lines)
+  uint64_t* fedge = nullptr;
   bool fmask_on = false, fmask_valid = false;
   int fmask_mode = 0;  // DM_FMASK=auto|on|off (read at dm_create; tests / A/B): 0 auto, 1 on, 2 off
   unsigned long long* cnt = nullptr;    // CNT_N device counters (frontier fields)
@@ -542,6 +547,8 @@ int dm_launch_rank_sort(hipStream_t stream, long long* clusters, const long long
                         int64_t host_cap, int64_t expect);
 // Listed tiles from which a frontier pass reads fmask instead of state bytes.
 constexpr int64_t kFmaskOnTiles = 8192;
+// Frontier slots (tile-local components) per map tile allocated at dm_create.
+constexpr int64_t kSlotsPerTile = 4;
 int dm_grow_bucket_sort(dm_grid* g, int64_t n);
 // Row-bucket sort of the raw records (labels of rows [row_base, row_base +
 // rows)): same outputs, readback header and flags as dm_launch_rank_sort.

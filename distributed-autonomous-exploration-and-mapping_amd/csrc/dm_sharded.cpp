@@ -383,7 +383,7 @@ extern "C" int dm_create_sharded(dm_grid** out, const dm_params* p, int32_t nran
   // overflows has no result): a cluster per two tiles of the band (C5's
   // sparsest rays: ~0.2); the exchange copies stay on the node's xGMI
   int64_t rec_cap = 16384;
-  while (rec_cap < ceil_div(p->width, DM_TILE) * ceil_div(s->rows[0], DM_TILE) / 2) rec_cap *= 2;
+  while (rec_cap < ceil_div(p->width, DM_TILE) * ceil_div(s->rows[0], DM_TILE)) rec_cap *= 2;
   if (int rc = sh_alloc_exchange(s, rec_cap)) return fail(rc);
   *out = g;
   return DM_OK;

@@ -152,7 +152,8 @@ def _exchange_like_sharded_mapper(handles, rec_cap):
     so the FIRST device exchange must succeed — no incomplete record, no host
     fallback."""
     got, got_last, max_k = _device_exchange(handles, rec_cap)
-    assert got is not None, ("device exchange fell back", getattr(handles[0], "last_incomplete", None))
+    assert got is not None, ("device exchange fell back", getattr(handles[0], "last_incomplete", None), rec_cap,
+                             [h.last_stats()["frontier_slots"] for h in handles])
     return got, got_last, max_k
 
 
@@ -228,7 +229,7 @@ def test_c5_full_map_vs_band_oracle_and_band_handles(oracle_lib, n_beams, n_batc
             np.testing.assert_array_equal(h.state(), st[h.row0:h.row0 + h.rows], err_msg=f"band {r}")
         tiles = -(-handles[0].width // 64) * -(-handles[0].rows // 64)
         rec_cap = 1 << 14
-        while rec_cap < tiles // 2:  # ShardedMapper's up-front sizing
+        while rec_cap < tiles:  # ShardedMapper's up-front sizing
             rec_cap *= 2
         got, got_last, max_k = _exchange_like_sharded_mapper(handles, rec_cap)
         assert got is not None, max_k

@@ -109,15 +109,16 @@ def test_direct_scanner_layouts(oracle_lib, amin, span, N):
 
 
 def test_direct_and_binned_agree_and_switch(oracle_lib):
-    """auto picks direct for dense scans, binned for sparse ones; switching
-    modes between calls leaves every per-tile array at rest."""
-    p, batches, amin, inc = cases.world_case(61, 1024, 1024, 0.05, 8, 4096, 3, region_frac=0.6)
+    """auto picks direct for dense scans that fill the chip unchunked
+    (32 x 4096 beams), binned for sparse ones; switching modes between calls
+    leaves every per-tile array at rest."""
+    p, batches, amin, inc = cases.world_case(61, 1024, 1024, 0.05, 32, 4096, 3, region_frac=0.6)
     _, sparse, amin_s, inc_s = cases.world_case(62, 1024, 1024, 0.05, 8, 360, 2, region_frac=0.6)
     om = oracle_lib.OracleMap(p)
     with dm.OccupancyMapper(p) as m:
         for k, (poses, ranges) in enumerate(batches):
             assert m.integrate(poses, ranges, amin, inc) == om.integrate(poses, ranges, amin, inc)
-            assert m.last_integrate_direct()  # auto: 4096 beams
+            assert m.last_integrate_direct()  # auto: 4096 beams, 32 scans
             poses_s, ranges_s = sparse[k % 2]
             assert m.integrate(poses_s, ranges_s, amin_s, inc_s) == om.integrate(poses_s, ranges_s, amin_s, inc_s)
             assert not m.last_integrate_direct()  # auto: 360 beams
