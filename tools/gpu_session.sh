@@ -11,6 +11,10 @@
 #   pmc           PMC passes over a short C3 bench -> profiles/pmc_latest.json [C3]
 #   pmcx          PMC passes over the explored-map probe -> [C3-explored]
 #   cfg:CN        bench.py --config CN
+#   abfe          C3 A/B of the integrate front-ends and fmask (tools/ab.sh -> ab.log)
+#   timeline      per-workgroup accumulation timeline (tools/accum_timeline.py)
+#   phase / phase5:N   phase build probe at C3 / C5 with N beams per scan
+#   c5:SWEEP      bench.py --config C5 --sweep SWEEP
 set -o pipefail
 R=$PWD
 OUT=$R/gpurun_out
@@ -56,6 +60,25 @@ for s in "$@"; do
         python $R/tools/pmc_summary.py $OUT/pmc5_$n $R/profiles/pmc_latest.json C5-$n >> $OUT/pmc5_summary.log 2>&1 || exit 1
       done
       cp $R/profiles/pmc_latest.json $OUT/pmc_latest.json ;;
+    abfe)
+      # C3 A/B: binned vs direct front-end, fmask maintained or not (2 alternating rounds)
+      BENCH_ARGS_binned="--integrate-mode binned" BENCH_ARGS_direct="--integrate-mode direct" \
+      BENCH_ARGS_binfm="--integrate-mode binned" BENCH_ARGS_dirfm="--integrate-mode direct" \
+        timeout -k 10 900 bash $R/tools/ab.sh 2 "binned:" "direct:" "binfm:DM_FMASK=on" "dirfm:DM_FMASK=on"
+      rc=$?; echo "abfe rc=$rc"; ok $rc || exit $rc ;;
+    timeline)
+      timeout -k 10 300 python -u $R/tools/accum_timeline.py 30 --json $OUT/accum_timeline.json \
+        > $OUT/accum_timeline.log 2>&1
+      rc=$?; echo "timeline rc=$rc"; ok $rc || exit $rc ;;
+    phase5:*)
+      timeout -k 10 300 python -u $R/tools/phase_probe.py c5 ${s#phase5:} > $OUT/phase_c5_${s#phase5:}.log 2>&1
+      rc=$?; echo "phase5 rc=$rc"; ok $rc || exit $rc ;;
+    phase)
+      timeout -k 10 300 python -u $R/tools/phase_probe.py > $OUT/phase_c3.log 2>&1
+      rc=$?; echo "phase rc=$rc"; ok $rc || exit $rc ;;
+    c5:*)
+      timeout -k 10 600 python -u bench.py --config C5 --sweep ${s#c5:} --cpu-seconds 0 > $OUT/bench_c5.log 2>&1
+      rc=$?; echo "c5 rc=$rc"; tail -1 $OUT/bench_c5.log | cut -c1-300; ok $rc || exit $rc ;;
     cfg:*)
       c=${s#cfg:}
       timeout -k 10 400 python -u bench.py --config $c --cpu-seconds 10 > $OUT/bench_$c.log 2>&1
