@@ -564,9 +564,9 @@ def pmc_traffic(kernel, workload):
 # the pass's kernels in stream order; frontier_big runs on its own stream
 # beside frontier_tile, so the pass's device time counts the
 # longer of the two
-FRONTIER_KERNELS = ("frontier_prep", "frontier_bits", "frontier_tile", "frontier_big", "frontier_resolve",
+FRONTIER_KERNELS = ("frontier_bits", "frontier_tile", "frontier_big", "frontier_resolve",
                     "frontier_compact", "sort_clusters")
-PMC_FRONTIER_KERNELS = ("k_frontier_prep", "k_frontier_bits", "k_frontier_tile", "k_frontier_tile_big",
+PMC_FRONTIER_KERNELS = ("k_frontier_bits", "k_frontier_tile", "k_frontier_tile_big",
                         "k_frontier_resolve", "k_frontier_compact", "k_rank_sort", "k_rs_count", "k_rs_scan",
                         "k_rs_place", "k_rs_rank")
 

@@ -569,12 +569,14 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     DM_HIP(hipMemset(f.cnt, 0, sizeof(unsigned long long) * CNT_N));
     if ((rc = dev_alloc(&f.fsh, kShards * kShardWords, "frontier shard counters"))) return fail(rc);
     DM_HIP(hipMemset(f.fsh, 0, sizeof(unsigned long long) * kShards * kShardWords));
-    if ((rc = dev_alloc(&f.ftiles, g->NT, "frontier tiles"))) return fail(rc);
     if ((rc = dev_alloc(&f.big_tiles, g->NT, "frontier big tiles"))) return fail(rc);
     if ((rc = dev_alloc(&f.fbits, g->NT * DM_TILE, "frontier bit rows"))) return fail(rc);
     if ((rc = dev_alloc(&f.edge_slot, 2 * g->W, "edge slots"))) return fail(rc);
   }
   if ((rc = dev_alloc(&g->fl_n, 48, "frontier list lengths"))) return fail(rc);
+  if ((rc = dev_alloc(&g->ftiles, g->NT, "frontier tile list"))) return fail(rc);
+  if ((rc = dev_alloc(&g->ftiles_n, 16, "frontier tile list length"))) return fail(rc);
+  DM_HIP(hipMemset(g->ftiles_n, 0, sizeof(unsigned long long) * 16));
   DM_HIP(hipMemset(g->fl_n, 0, sizeof(unsigned long long) * 48));
   if ((rc = dev_alloc(&g->bits_flag, 16, "bit-row hand-off word"))) return fail(rc);
   DM_HIP(hipMemset(g->bits_flag, 0, sizeof(unsigned long long) * 16));
@@ -663,10 +665,10 @@ int dm_destroy(dm_grid* g) {
   if (g->big_stream) (void)hipStreamDestroy(g->big_stream);
   for (auto& f : g->fw) {
     if (f.ev_split) (void)hipEventDestroy(f.ev_split);
-    dev_free(f.cnt); dev_free(f.fsh); dev_free(f.ftiles); dev_free(f.big_tiles); dev_free(f.fbits);
+    dev_free(f.cnt); dev_free(f.fsh); dev_free(f.big_tiles); dev_free(f.fbits);
     dev_free(f.edge_slot); dev_free(f.slot_parent);
   }
-  dev_free(g->fl_n); dev_free(g->bits_flag);
+  dev_free(g->fl_n); dev_free(g->bits_flag); dev_free(g->ftiles); dev_free(g->ftiles_n);
   for (int b = 0; b < 2; ++b) { dev_free(g->goal_k[b]); dev_free(g->goal_i[b]); }
   dev_free(g->goal_io); dev_free(g->goal_idx);
   for (auto& w : g->iw) {

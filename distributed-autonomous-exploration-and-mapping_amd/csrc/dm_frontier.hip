@@ -8,20 +8,22 @@
 //   label   = min global row-major index of c's 8-connected component of F
 //   cluster = (label, size, sum_x, sum_y), sorted by label (host side).
 //
-// Pipeline (DESIGN.md §3.3); tiles are the 64x64 tiles of dm_integrate.hip:
-//   k_ftile_list    tiles holding >= 1 free cell (tile_free > 0, maintained
-//                   incrementally by k_tile_apply) -> visit list + map.  Only
-//                   free cells can be frontier cells, so every other tile is
-//                   skipped without reading it.
-//   k_frontier_tile one workgroup per listed tile: state tile + 1-cell halo
-//                   in LDS, frontier test, LDS union-find (atomicMin hooking,
-//                   root = min index), per-component sums, one slot per
-//                   tile-local component; then the unions across its edges
-//                   with the neighbour tiles that finished before it (the
-//                   later tile of each edge unites: a stamped hand-off word
-//                   per tile pair), lock-free CAS union-find keyed by slot
+// Pipeline (DESIGN.md §3.2); tiles are the 64x64 tiles of dm_integrate.hip:
+//   (list)          the persistent tile list: every tile that has held a free
+//                   cell, appended by the integrate apply (dm_internal.h,
+//                   ftiles); only free cells can be frontier cells, so every
+//                   other tile is skipped without reading it
+//   k_frontier_bits one wave per listed tile: frontier bit rows (the only
+//                   kernel that reads the map), plus the pass's resets
+//   k_frontier_tile(_big)  per listed tile: runs, LDS union-find (atomicMin
+//                   hooking, root = min index), per-component sums, one slot
+//                   per tile-local component; then the unions across its
+//                   edges with the neighbour tiles that finished before it
+//                   (the later tile of each edge unites: a stamped hand-off
+//                   word per tile pair), lock-free CAS union-find keyed by slot
 //   k_frontier_resolve / k_frontier_compact  roots, int64 sums and the min
 //                   label of each merged set, cluster list
+//   k_rank_sort / row sort  records by label, centroids, readback
 #include "dm_internal.h"
 #include "dm_uf.h"
 #include "dm_phase.h"
@@ -56,87 +58,6 @@ struct FGeom {
   int64_t clu_cap;
   int64_t min_size;
 };
-
-constexpr int kPrepIters = 16;  // k_frontier_prep: 256-tile rows per workgroup chunk
-
-// Per-call preparation in one launch: reset the frontier counters, slot
-// shards and edge slots, and list the tiles holding >= 1 free cell (only
-// free cells can be frontier cells; tile_free is maintained by the
-// integrate kernels, so every other tile is skipped without reading it).
-// The list length goes to *list_n, which the previous call zeroed; this call
-// zeroes *other_n for the next one (the two alternate by call parity).
-__global__ __launch_bounds__(256) void k_frontier_prep(int64_t NT, const int32_t* __restrict__ tile_free,
-                                                       int32_t* __restrict__ ftiles,
-                                                       unsigned long long* list_n,
-                                                       unsigned long long* other_n, int64_t n_edge,
-                                                       unsigned long long* cnt, unsigned long long* fsh,
-                                                       int32_t* __restrict__ edge_slot,
-                                                       int32_t* __restrict__ slot_parent, int64_t slot_cap,
-                                                       const unsigned long long* __restrict__ halt,
-                                                       unsigned long long* stamp_word, int iters) {
-  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int lane = __lane_id();
-  // slots, clusters, overflow (kOvPipeline while the handle's sticky
-  // hand-off error is set: the map misses a batch, DM_ERR_PIPELINE)
-  if (i0 < 3) cnt[CNT_SLOTS + i0] = (i0 == 2 && *halt) ? kOvPipeline : 0ull;
-  if (i0 == 3) cnt[CNT_BIG] = 0ull;
-  if (i0 == 4) {  // this pass's stamp: every prep runs on the handle's stream, one after the other
-    const unsigned long long st = *stamp_word + 1;
-    *stamp_word = st;
-    cnt[CNT_STAMP] = st;
-  }
-  if (i0 == 0) *other_n = 0ull;
-  if (i0 < kShards * kShardWords) fsh[i0] = 0ull;
-  for (int64_t i = i0; i < n_edge; i += stride) edge_slot[i] = -1;
-  // every slot starts as its own root here, a launch ahead of the tile
-  // kernel's in-kernel unions: their CASes and (possibly stale, L2-served)
-  // finds then only ever see a slot as a root or as hooked (dm_uf.h)
-  for (int64_t i = i0; i < slot_cap; i += stride) slot_parent[i] = (int32_t)i;
-  // ballot compaction over a contiguous chunk of `iters` x 256 tiles per
-  // workgroup and round, ONE list_n atomic per chunk: every workgroup with a
-  // listed tile bumps the same word, and those memory-side atomics
-  // serialise (a 1 M-tile C5 map took 29 us over 4096 one-row chunks; the
-  // host picks iters so there are ~256 chunks: 1 at C3, 16 at C5); each
-  // thread keeps its tiles' bits between the count and the placement (the
-  // loop bounds are uniform within the workgroup: its barriers are safe)
-  __shared__ int32_t s_wn[kPrepIters][4];
-  __shared__ unsigned long long s_base;
-  const int w = threadIdx.x >> 6;
-  const int64_t chunk = (int64_t)iters * blockDim.x;
-  for (int64_t c0 = (int64_t)blockIdx.x * chunk; c0 < NT; c0 += (int64_t)gridDim.x * chunk) {
-    // this thread's tiles of the chunk as a bit mask (the ballots' own bits)
-    uint32_t mine = 0u;
-#pragma unroll 4
-    for (int i = 0; i < iters; ++i) {  // loads first (several in flight), ballots after
-      const int64_t t = c0 + (int64_t)i * blockDim.x + threadIdx.x;
-      mine |= (t < NT && tile_free[t] > 0 ? 1u : 0u) << i;
-    }
-    for (int i = 0; i < iters; ++i) {
-      const unsigned long long bal = __ballot((mine >> i) & 1u);
-      if (lane == 0) s_wn[i][w] = __popcll(bal);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int total = 0;
-      for (int i = 0; i < iters; ++i) total += s_wn[i][0] + s_wn[i][1] + s_wn[i][2] + s_wn[i][3];
-      s_base = total ? atomicAdd(list_n, (unsigned long long)total) : 0ull;
-    }
-    __syncthreads();
-    int64_t pre = (int64_t)s_base;
-    for (int i = 0; i < iters; ++i) {
-      const bool f = (mine >> i) & 1u;
-      const unsigned long long bal = __ballot(f);
-      int before = 0;
-      for (int q = 0; q < w; ++q) before += s_wn[i][q];
-      if (f)
-        ftiles[pre + before + __popcll(bal & ((1ull << lane) - 1ull))] =
-            (int32_t)(c0 + (int64_t)i * blockDim.x + threadIdx.x);
-      pre += s_wn[i][0] + s_wn[i][1] + s_wn[i][2] + s_wn[i][3];
-    }
-    __syncthreads();  // s_wn / s_base are rewritten next round
-  }
-}
 
 // Find with path halving: every other node on the way is re-pointed to its
 // grandparent, so later finds (the unions of the next rows, the final
@@ -220,7 +141,7 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
     long long* __restrict__ slot_own, long long* __restrict__ slot_acc,
     uint8_t* __restrict__ mask, int32_t* __restrict__ cell_slot, int32_t* __restrict__ edge_slot,
     unsigned long long* cnt, unsigned long long* fsh, int count_stats) {
-  const unsigned long long stamp = cnt[CNT_STAMP];  // this pass's (k_frontier_prep)
+  const unsigned long long stamp = cnt[CNT_STAMP];  // this pass's (k_frontier_bits)
   __shared__ uint64_t s_F[DM_TS];          // frontier bit rows
   __shared__ int32_t s_rbase[DM_TS + 1];
   __shared__ int32_t r_par[kMaxRuns];
@@ -382,7 +303,7 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
       const long long gx = (long long)tx0 + r_s[r];
       const uint32_t zx = szx[c];
       const long long sz = zx >> 18;
-      slot_label[slot] = gy * g.W + gx;  // (slot_parent[slot] == slot since k_frontier_prep)
+      slot_label[slot] = gy * g.W + gx;  // (slot_parent[slot] == slot since k_frontier_bits)
       const long long sx = sz * tx0 + (zx & 0x3FFFFu);
       const long long sy = sz * ((long long)g.row0 + ty0) + ssy[c];
       slot_own[3 * slot + 0] = sz; slot_own[3 * slot + 1] = sx; slot_own[3 * slot + 2] = sy;
@@ -710,18 +631,42 @@ __device__ inline uint64_t nib_row(uint4 v, int shift) {
 // scattered halo lines (or the neighbours' whole records for one byte per row).
 // Tiles next to a band halo (sharded maps) read the state bytes and the
 // halo rows instead.  Also copies the list length into the pass's counters.
-__global__ __launch_bounds__(kFW * 64) void k_frontier_bits(FGeom g, const int8_t* __restrict__ state,
-                                                            const int8_t* __restrict__ halo,
-                                                            const uint8_t* __restrict__ fmask,
-                                                            const uint64_t* __restrict__ fedge,
-                                                            const int32_t* __restrict__ ftiles,
-                                                            const unsigned long long* __restrict__ list_n,
-                                                            uint64_t* __restrict__ fbits,
-                                                            unsigned long long* cnt, int use_fmask,
-                                                            int32_t* __restrict__ big_flag) {
+__global__ __launch_bounds__(kFW * 64) void k_frontier_bits(
+    FGeom g, const int8_t* __restrict__ state, const int8_t* __restrict__ halo, const uint8_t* __restrict__ fmask,
+    const uint64_t* __restrict__ fedge, const int32_t* __restrict__ ftiles,
+    const unsigned long long* __restrict__ ftiles_n, unsigned long long* list_n, uint64_t* __restrict__ fbits,
+    unsigned long long* cnt, int use_fmask, int32_t* __restrict__ big_flag, unsigned long long* fsh,
+    int32_t* __restrict__ edge_slot, int64_t n_edge, int32_t* __restrict__ slot_parent,
+    const unsigned long long* __restrict__ halt, unsigned long long* stamp_word) {
   const int w = threadIdx.x >> 6, lane = __lane_id();
-  const int64_t nft = (int64_t)*list_n;
-  if (blockIdx.x == 0 && threadIdx.x == 0) cnt[CNT_FL0] = (unsigned long long)nft;
+  // the persistent tile list's length: appended only by the map updates on
+  // this stream, before and after this kernel, so every workgroup reads the
+  // same value; the pass's kernels read this snapshot (list_n)
+  const int64_t nft = (int64_t)*ftiles_n;
+  // the pass's resets (every workgroup a share): counters, slot shards, edge
+  // slots, and every slot as its own root a launch ahead of the tile
+  // kernels' in-kernel unions (their CASes and possibly stale finds then
+  // only ever see a slot as a root or as hooked, dm_uf.h)
+  {
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    // slots, clusters, overflow (kOvPipeline while the handle's sticky
+    // hand-off error is set: the map misses a batch, DM_ERR_PIPELINE)
+    if (i0 < 3) cnt[CNT_SLOTS + i0] = (i0 == 2 && *halt) ? kOvPipeline : 0ull;
+    if (i0 == 3) cnt[CNT_BIG] = 0ull;
+    if (i0 == 4) {  // this pass's stamp: every pass's bits run on the handle's stream, one after the other
+      const unsigned long long st = *stamp_word + 1;
+      *stamp_word = st;
+      cnt[CNT_STAMP] = st;
+    }
+    if (i0 == 5) {
+      *list_n = (unsigned long long)nft;
+      cnt[CNT_FL0] = (unsigned long long)nft;
+    }
+    if (i0 < kShards * kShardWords) fsh[i0] = 0ull;
+    for (int64_t i = i0; i < n_edge; i += stride) edge_slot[i] = -1;
+    for (int64_t i = i0; i < g.slot_cap; i += stride) slot_parent[i] = (int32_t)i;
+  }
   // four consecutive listed tiles per workgroup: horizontal neighbours share
   // the 128-byte lines of their rows and halo columns
   for (int64_t jj = (int64_t)blockIdx.x * kFW + w; jj < nft; jj += (int64_t)gridDim.x * kFW) {
@@ -784,7 +729,7 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
     long long* __restrict__ slot_own, long long* __restrict__ slot_acc,
     uint8_t* __restrict__ mask, int32_t* __restrict__ cell_slot, int32_t* __restrict__ edge_slot,
     unsigned long long* cnt, unsigned long long* fsh, int32_t* __restrict__ big_list) {
-  const unsigned long long stamp = cnt[CNT_STAMP];  // this pass's (k_frontier_prep)
+  const unsigned long long stamp = cnt[CNT_STAMP];  // this pass's (k_frontier_bits)
   __shared__ int32_t s_par[kFW][kRunsFast];
   __shared__ unsigned long long s_acc[kFW][kRunsFast];  // size << 40 | sum_x << 20 | sum_y (tile-local)
   __shared__ uint64_t s_rootw[kFW][kRunsFast / 64];     // root-run bits
@@ -1670,18 +1615,8 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
     fw.busy_pending = false;
   }
   dm_select_fw(g, g->fparity);
-  unsigned long long* list_n = g->fl_n + 16 * (g->fr_pass % 3);
-  unsigned long long* zero_n = g->fl_n + 16 * ((g->fr_pass + 1) % 3);  // last used by pass fr_pass - 2
+  unsigned long long* list_n = g->fl_n + 16 * (g->fr_pass % 3);  // this pass's list length (k_frontier_bits)
   KernelTimer t;
-  dm_timer_begin(g, "frontier_prep", &t);
-  // ~256 chunks of prep_iters x 256 tiles, at least 256 workgroups for the resets
-  const int prep_iters = (int)std::min<int64_t>(kPrepIters, std::max<int64_t>(1, (g->NT + 65535) / 65536));
-  DM_LAUNCH(k_frontier_prep, dim3(grid_for(std::max<int64_t>((g->NT + prep_iters - 1) / prep_iters, 256 * 256), 256, 1024)), dim3(256), 0,
-                     g->stream, g->NT, g->tile_free, g->ftiles, list_n, zero_n, 2 * g->W, g->cnt, g->fsh,
-                     g->edge_slot, g->slot_parent, g->slot_cap, g->fe_flag + kHaltWord,
-                     g->bits_flag + kStampWord, prep_iters);
-  dm_timer_end(g, &t);
-  DM_HIP(hipGetLastError());
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));
   // one wave per listed tile; the grid follows the last collected pass's
@@ -1689,6 +1624,9 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   // covered)
   const int64_t want_waves = g->ftile_hint > 0 ? dm_quantize_up(g->ftile_hint + g->ftile_hint / 4 + 64) : g->NT;
   const int wave_grid = grid_for(std::min<int64_t>(want_waves, g->NT), kFW, 8192);
+  // k_frontier_bits also resets the pass's arrays (slot parents: 4 per map
+  // tile): at least 64 workgroups
+  const int bits_grid = std::max(wave_grid, 64);
   // fmask while the passes list many tiles (dm_internal.h, fmask_on); a
   // switch on rebuilds the records first unless they still match the state
   const bool want_on = g->fmask_mode == 1 || (g->fmask_mode == 0 && g->ftile_hint >= kFmaskOnTiles);
@@ -1717,9 +1655,10 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
                      (g->frontier_kernel == 0 && g->ftf_hint > 0 && g->runs_hint > kDenseRuns * g->ftf_hint &&
                       g->ftf_hint <= kDenseMaxTiles);
   dm_timer_begin(g, "frontier_bits", &t);
-  DM_LAUNCH(k_frontier_bits, dim3(wave_grid), dim3(kFW * 64), 0, g->stream, fg, g->state, g->halo,
-                     g->fmask, g->fedge, g->ftiles, list_n, g->fbits, g->cnt, g->fmask_on ? 1 : 0,
-                     dense ? nullptr : g->big_tiles);
+  DM_LAUNCH(k_frontier_bits, dim3(bits_grid), dim3(kFW * 64), 0, g->stream, fg, g->state, g->halo, g->fmask,
+            g->fedge, g->ftiles, g->ftiles_n, list_n, g->fbits, g->cnt, g->fmask_on ? 1 : 0,
+            dense ? nullptr : g->big_tiles, g->fsh, g->edge_slot, 2 * g->W, g->slot_parent, g->fe_flag + kHaltWord,
+            g->bits_flag + kStampWord);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   // the map has been read: with split, the rest runs on the pass stream,

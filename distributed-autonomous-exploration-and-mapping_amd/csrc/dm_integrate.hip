@@ -714,17 +714,34 @@ __device__ inline PackedPiece no_piece() {
   return q;
 }
 
+// A tile's new tile_free word after a net change of dfree free cells from
+// `old` (the item applying the tile is its only writer in the call): a tile
+// whose free count rises from 0 while kTileListed is clear is appended to the
+// persistent frontier tile list (dm_internal.h, ftiles) and flagged.  Tiles
+// that were listed stay listed (the pass skips tiles without frontier bits).
+__device__ inline int32_t free_update(int32_t old, int32_t dfree, int32_t tile, int32_t* tlist,
+                                      unsigned long long* tlist_n) {
+  int32_t v = old + dfree;
+  if (dfree > 0 && !(old & kTileListed)) {
+    v |= kTileListed;
+    tlist[atomicAdd(tlist_n, 1ull)] = tile;
+  }
+  return v;
+}
+
+// The heavy finisher's counters; old_free is the tile's tile_free word as
+// loaded before its apply (no other item of the call writes it).
 __device__ inline void finish_tile(const Geom& g, int32_t tile, int32_t T, int32_t dfree, uint32_t U,
-                                   bool heavy, int32_t* tile_count, int32_t* tile_free,
-                                   unsigned long long* ish) {
+                                   bool heavy, int32_t* tile_count, int32_t* tile_free, int32_t old_free,
+                                   int32_t* tlist, unsigned long long* tlist_n, unsigned long long* ish) {
   unsigned long long* sh = ish + (blockIdx.x % kShards) * kShardWords;
   if (T) {
     atomicAdd(&sh[SH_T], (unsigned long long)T);
     if (heavy) atomicAdd(&sh[SH_TH], (unsigned long long)T);
   }
   if (U) atomicAdd(&sh[SH_U], (unsigned long long)U);
-  if (dfree) atomicAdd(&tile_free[tile], dfree);  // no returned value: nothing to wait for
-  tile_count[tile] = 0;                            // ready for the next call
+  if (dfree) tile_free[tile] = free_update(old_free, dfree, tile, tlist, tlist_n);
+  tile_count[tile] = 0;  // ready for the next call
 }
 
 // One 16-row quarter q of heavy tile h (ordinal in heavy_list): apply the
@@ -819,7 +836,8 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     int cnt_b, int cnt_c, const PackedPiece* __restrict__ pieces, int32_t* tile_count, int32_t* tile_free,
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
     const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok,
-    const int32_t* __restrict__ heavy_list, int32_t* heavy_done, const unsigned long long* __restrict__ halt) {
+    const int32_t* __restrict__ heavy_list, int32_t* heavy_done, int32_t* tlist, unsigned long long* tlist_n,
+    const unsigned long long* __restrict__ halt) {
   __shared__ uint32_t tl[kTileWords + 64];  // + one spare word per lane (walk_piece_plain)
   __shared__ int32_t s_T, s_free, s_last;
   __shared__ uint32_t s_U;
@@ -953,11 +971,12 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
 #endif
         const int64_t h = heavy >> 1;
         const bool wide = heavy_list[h] < 0;
+        const int32_t old_free = tid == 0 ? tile_free[tile] : 0;  // in flight during the apply
         for (int q = 0; q < 4; ++q)
           heavy_quarter(g, p, h, q, tile, wide, slabs, L, state, &s_T, &s_free, &s_U);
         __syncthreads();
         if (tid == 0) {
-          finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, ish);
+          finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, old_free, tlist, tlist_n, ish);
           heavy_done[h] = 0;  // ready for the next call
         }
 #ifdef DM_PHASE_TIMING
@@ -1005,7 +1024,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     if (tid == 0 && heavy < 0) {
       s_accT += (unsigned long long)s_T;
       s_accU += (unsigned long long)s_U;
-      if (s_free) tile_free[tile] = tfree + s_free;
+      if (s_free) tile_free[tile] = free_update(tfree, s_free, tile, tlist, tlist_n);
       tile_count[tile] = 0;  // ready for the next call
     }
     // the next item: its pieces go out now (or went out after the walk),
@@ -1123,7 +1142,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
       const uint32_t U = s_wU[wv] + wU;
       atomicAdd(&s_accT, (unsigned long long)T);
       atomicAdd(&s_accU, (unsigned long long)U);
-      if (df) tile_free[tile] = sfree + df;
+      if (df) tile_free[tile] = free_update(sfree, df, tile, tlist, tlist_n);
       tile_count[tile] = 0;  // ready for the next call
       s_wT[wv] = 0;
       s_wfree[wv] = 0;
@@ -1297,8 +1316,8 @@ __global__ __launch_bounds__(kQuarter, DM_DIRECT_OCC) void k_direct_accum(
     const double* __restrict__ trig, const int4* __restrict__ units, const int4* __restrict__ items,
     const unsigned long long* __restrict__ cnt, int32_t* tile_items, int32_t* tile_cand, int32_t* tile_head,
     int32_t* tile_slab, int32_t* heavy_done, uint32_t* __restrict__ slabs, int32_t* tile_free,
-    float* __restrict__ L, int8_t* __restrict__ state, unsigned long long* ish, int vec_ok,
-    const unsigned long long* __restrict__ halt) {
+    float* __restrict__ L, int8_t* __restrict__ state, unsigned long long* ish, int vec_ok, int32_t* tlist,
+    unsigned long long* tlist_n, const unsigned long long* __restrict__ halt) {
   __shared__ uint32_t tl[kTileWords + 64];  // + one spare word per lane (walk_tp_plain)
   __shared__ int32_t s_T, s_free, s_last;
   __shared__ uint32_t s_U;
@@ -1391,7 +1410,7 @@ __global__ __launch_bounds__(kQuarter, DM_DIRECT_OCC) void k_direct_accum(
       if (tid == 0) {
         s_accT += (unsigned long long)s_T;
         s_accU += (unsigned long long)s_U;
-        if (s_free) tile_free[tile] = tfree + s_free;
+        if (s_free) tile_free[tile] = free_update(tfree, s_free, tile, tlist, tlist_n);
         tile_items[tile] = 0;  // the tile's per-call state back at rest
         tile_cand[tile] = 0;
         tile_head[tile] = -1;
@@ -1428,7 +1447,7 @@ __global__ __launch_bounds__(kQuarter, DM_DIRECT_OCC) void k_direct_accum(
         for (int q = 0; q < 4; ++q) heavy_quarter(g, p, slab, q, tile, wide, slabs, L, state, &s_T, &s_free, &s_U);
         __syncthreads();
         if (tid == 0) {
-          finish_tile(g, tile, s_T, s_free, s_U, true, tile_items, tile_free, ish);
+          finish_tile(g, tile, s_T, s_free, s_U, true, tile_items, tile_free, tfree, tlist, tlist_n, ish);
           heavy_done[slab] = 0;  // the tile's per-call state back at rest
           tile_cand[tile] = 0;
           tile_head[tile] = -1;
@@ -1587,6 +1606,55 @@ __global__ __launch_bounds__(256) void k_recount(Geom g, const int8_t* __restric
   if (threadIdx.x < 4)
     fedge[tile * 4 + threadIdx.x] = s_edge[0][threadIdx.x] | s_edge[1][threadIdx.x] | s_edge[2][threadIdx.x] |
                                     s_edge[3][threadIdx.x];
+}
+
+// After k_recount (bulk state writes: counts only, flags clear): the
+// persistent frontier tile list from scratch, every tile with a free cell in
+// tile order, each flagged kTileListed by the thread that places it.  Ballot
+// compaction over chunks of `iters` x 256 tiles per workgroup and round, one
+// list atomic per chunk (the loop bounds are uniform within the workgroup:
+// its barriers are safe).
+constexpr int kListIters = 16;
+__global__ __launch_bounds__(256) void k_list_tiles(int64_t NT, int32_t* __restrict__ tile_free,
+                                                    int32_t* __restrict__ ftiles, unsigned long long* list_n,
+                                                    int iters) {
+  const int lane = __lane_id();
+  __shared__ int32_t s_wn[kListIters][4];
+  __shared__ unsigned long long s_base;
+  const int w = threadIdx.x >> 6;
+  const int64_t chunk = (int64_t)iters * blockDim.x;
+  for (int64_t c0 = (int64_t)blockIdx.x * chunk; c0 < NT; c0 += (int64_t)gridDim.x * chunk) {
+    uint32_t mine = 0u;
+    for (int i = 0; i < iters; ++i) {
+      const int64_t t = c0 + (int64_t)i * blockDim.x + threadIdx.x;
+      mine |= (t < NT && (tile_free[t] & kTileFreeMask) > 0 ? 1u : 0u) << i;
+    }
+    for (int i = 0; i < iters; ++i) {
+      const unsigned long long bal = __ballot((mine >> i) & 1u);
+      if (lane == 0) s_wn[i][w] = __popcll(bal);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int total = 0;
+      for (int i = 0; i < iters; ++i) total += s_wn[i][0] + s_wn[i][1] + s_wn[i][2] + s_wn[i][3];
+      s_base = total ? atomicAdd(list_n, (unsigned long long)total) : 0ull;
+    }
+    __syncthreads();
+    int64_t pre = (int64_t)s_base;
+    for (int i = 0; i < iters; ++i) {
+      const bool f = (mine >> i) & 1u;
+      const unsigned long long bal = __ballot(f);
+      int before = 0;
+      for (int q = 0; q < w; ++q) before += s_wn[i][q];
+      if (f) {
+        const int64_t t = c0 + (int64_t)i * blockDim.x + threadIdx.x;
+        ftiles[pre + before + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)t;
+        tile_free[t] |= kTileListed;
+      }
+      pre += s_wn[i][0] + s_wn[i][1] + s_wn[i][2] + s_wn[i][3];
+    }
+    __syncthreads();  // s_wn / s_base are rewritten next round
+  }
 }
 
 __device__ inline uint64_t upto_rows(int p) {  // bits 0..p inclusive
@@ -1781,7 +1849,7 @@ int launch_direct(dm_grid* g, dm_grid::IntWs& w, hipStream_t fs, const RayArgs& 
   DM_LAUNCH(k_direct_accum, dim3(grid_for(d.a_cap + d.b_cap, 1, dm_grid::kAccumGrid)), dim3(kQuarter), 0,
             g->stream, a, ge, d, make_apply(g), d_pose4, d_ranges, d_trig, w.units, w.ditems, w.cnt, w.tile_count,
             w.tile_cand, w.tile_head, w.tile_slab, w.heavy_done, w.slabs, g->tile_free, g->L, g->state, w.sh, vec_ok,
-            g->fe_flag + kHaltWord);
+            g->ftiles, g->ftiles_n, g->fe_flag + kHaltWord);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (g->overlap) w.free_owed = true;
@@ -1874,7 +1942,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                      dim3(kQuarter), 0,
                      g->stream, ge, make_apply(g), w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS,
                      (int)CNT_SITEMS, w.pieces, w.tile_count, g->tile_free, w.slabs, g->L, g->state, w.cnt, w.sh, vec_ok,
-                     w.heavy_list, w.heavy_done, g->fe_flag + kHaltWord);
+                     w.heavy_list, w.heavy_done, g->ftiles, g->ftiles_n, g->fe_flag + kHaltWord);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (g->overlap) w.free_owed = true;
@@ -1911,6 +1979,12 @@ int dm_launch_recount(dm_grid* g) {
   const Geom ge = make_geom(g);
   DM_LAUNCH(k_recount, dim3((unsigned)g->NT), dim3(256), 0, g->stream, ge, g->state,
                      g->tile_free, g->fmask, g->fedge);
+  DM_HIP(hipGetLastError());
+  // the persistent frontier tile list from the new counts (~256 chunks)
+  DM_HIP(hipMemsetAsync(g->ftiles_n, 0, sizeof(unsigned long long), g->stream));
+  const int iters = (int)std::min<int64_t>(kListIters, std::max<int64_t>(1, (g->NT + 65535) / 65536));
+  DM_LAUNCH(k_list_tiles, dim3(grid_for((g->NT + iters - 1) / iters, 256, 1024)), dim3(256), 0, g->stream,
+            g->NT, g->tile_free, g->ftiles, g->ftiles_n, iters);
   DM_HIP(hipGetLastError());
   g->fmask_valid = true;
   return DM_OK;

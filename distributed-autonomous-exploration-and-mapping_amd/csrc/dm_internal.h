@@ -38,7 +38,7 @@ enum {
   CNT_TH = 10,      // touched cells of heavy tiles
   CNT_SORTED = 11,  // 1: out_clu holds the clusters sorted by label
   CNT_FL0 = 12,     // frontier tile-list length of the pass (copied by k_frontier_bits)
-  CNT_STAMP = 13,   // the pass's stamp (k_frontier_prep: ++ the handle's stamp word), tile-edge hand-offs
+  CNT_STAMP = 13,   // the pass's stamp (k_frontier_bits: ++ the handle's stamp word), tile-edge hand-offs
   CNT_LITEMS = 14,  // light work items (= light tiles)
   CNT_IOVERFLOW = 15,  // integrate capacity overflow flags (1 first-touch list, 2 pieces, 4 work lists)
   CNT_BIG = 16,     // frontier tiles with more runs than a tile-wave holds (big-tile list length)
@@ -52,7 +52,7 @@ constexpr unsigned long long kOvPipeline = 32ull;  // the handle's sticky hand-o
 // fe_flag[kHaltWord]: sticky error word of the overlapped pipeline.  The
 // integrate front-end -> map update gate sets bit 1 when it times out; from
 // then on k_tile_accum and k_fmask_items return at once (the workspace they
-// would read was not written), k_frontier_prep flags every pass kOvPipeline,
+// would read was not written), k_frontier_bits flags every pass kOvPipeline,
 // and the host reports DM_ERR_PIPELINE until dm_reset clears it.
 constexpr int kHaltWord = 8;
 // Hand-off words (fe_flag, bits_flag): k_seq_signal increments [kSigWord],
@@ -61,7 +61,7 @@ constexpr int kHaltWord = 8;
 // in the kernel arguments.
 constexpr int kSigWord = 0;
 constexpr int kGateWord = 4;
-constexpr int kStampWord = 8;  // bits_flag: the last frontier pass's stamp (k_frontier_prep)
+constexpr int kStampWord = 8;  // bits_flag: the last frontier pass's stamp (k_frontier_bits)
 // Integrate counters, zeroed by each integrate call; the others belong to the
 // frontier pass, which may still be running when the next call's front-end
 // starts (dm_set_overlap), so the integrate reset never touches them.
@@ -215,6 +215,8 @@ struct dm_grid {
 
   float* L = nullptr;
   int8_t* state = nullptr;
+  // free cells per tile (bits 0..29) | kTileListed: the tile is on the
+  // persistent frontier tile list (ftiles / ftiles_n below)
   int32_t* tile_free = nullptr;
   // [NT][64 rows][16] per tile: byte j of row y holds the free bits of cells
   // 4j..4j+3 (low nibble) and their unknown bits (high nibble); out-of-grid
@@ -322,7 +324,6 @@ struct dm_grid {
   struct FrWs {
     unsigned long long* cnt = nullptr;  // [CNT_N]
     unsigned long long* fsh = nullptr;  // [kShards][kShardWords]
-    int32_t* ftiles = nullptr;          // [NT]
     int32_t* big_tiles = nullptr;       // [NT]
     uint64_t* fbits = nullptr;          // [NT][64]
     int32_t* edge_slot = nullptr;       // [2][W]
@@ -333,8 +334,8 @@ struct dm_grid {
     uint64_t busy_pass = 0;             // fr_pass of that pass
   };
   FrWs fw[2];
-  // tile-list lengths, a ring of three on separate lines: pass n counts into
-  // fl_n[16 * (n % 3)] and zeroes the next one (last used by pass n - 2)
+  // the pass's list lengths (snapshots of *ftiles_n taken by k_frontier_bits),
+  // a ring of three on separate lines: pass n uses fl_n[16 * (n % 3)]
   unsigned long long* fl_n = nullptr;
   // pass_stream (dm_set_overlap + dm_frontiers_begin): the labelling half of
   // a pass (tile kernels, resolve, sort) runs there, after the prep and the
@@ -351,7 +352,16 @@ struct dm_grid {
   hipEvent_t p_tail = nullptr;        // the last pass_stream pass's end (alias)
   bool p_pending = false;             // pass_stream work `stream` has not been ordered after
   uint64_t p_tail_pass = 0;
-  int32_t* ftiles = nullptr;   // tiles with free cells (built by k_frontier_prep)
+  // The persistent frontier tile list: every tile that has held a free cell
+  // since the last bulk state write, in the order its first free cell
+  // appeared (only free cells can be frontier cells).  Appended by the
+  // integrate apply (the item that raises a tile's free count above 0 while
+  // kTileListed is clear sets it and takes a list position), rebuilt after
+  // bulk writes (dm_launch_recount: k_list_tiles).  Append-only between
+  // rebuilds, so a pass reads the first *ftiles_n entries (its snapshot, taken
+  // on the map stream after its batch) while later batches append behind them.
+  int32_t* ftiles = nullptr;               // [NT]
+  unsigned long long* ftiles_n = nullptr;  // [16]: [0] the list length
   int32_t* big_tiles = nullptr;  // [NT] per list position: 1 = too many runs for a tile-wave (k_frontier_bits)
   uint64_t* fbits = nullptr;   // [NT][64] frontier bit rows of the listed tiles (k_frontier_bits)
   int32_t* border = nullptr;   // [tile][4][64] slot ids of a tile's edges (published sides only)
@@ -472,13 +482,12 @@ inline hipError_t dm_mark_ws_free(dm_grid* g, hipEvent_t recorded = nullptr) {
   return hipSuccess;
 }
 
-// Point the current-set views (cnt, fsh, ftiles, big_tiles, fbits,
+// Point the current-set views (cnt, fsh, big_tiles, fbits,
 // edge_slot, slot_parent) at frontier workspace set `s`.
 inline void dm_select_fw(dm_grid* g, int s) {
   const dm_grid::FrWs& f = g->fw[s];
   g->cnt = f.cnt;
   g->fsh = f.fsh;
-  g->ftiles = f.ftiles;
   g->big_tiles = f.big_tiles;
   g->fbits = f.fbits;
   g->edge_slot = f.edge_slot;
@@ -547,6 +556,9 @@ int dm_launch_rank_sort(hipStream_t stream, long long* clusters, const long long
                         int64_t host_cap, int64_t expect);
 // Listed tiles from which a frontier pass reads fmask instead of state bytes.
 constexpr int64_t kFmaskOnTiles = 8192;
+// tile_free: the listed flag above the free count (<= 4096)
+constexpr int32_t kTileListed = 1 << 30;
+constexpr int32_t kTileFreeMask = kTileListed - 1;
 // Frontier slots (tile-local components) per map tile allocated at dm_create.
 constexpr int64_t kSlotsPerTile = 4;
 int dm_grow_bucket_sort(dm_grid* g, int64_t n);

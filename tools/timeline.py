@@ -26,7 +26,7 @@ for k in range(first, min(first + 2, len(accum) - 1)):
         print(f"  {name:26s} {(s - t0) / 1e3:8.1f} {(e - t0) / 1e3:8.1f}  ({(e - s) / 1e3:5.1f})")
 
 # main-stream gaps per step (pipelined region): rank_sort end -> next
-# k_tile_accum start, heavy_apply end -> frontier_prep start, prep end -> tile start
+# accumulation start, accumulation end -> bit rows start, bit rows end -> tile start
 def gaps(a, b):
     out = []
     ends = [r for r in rows if r[2] == a]
@@ -40,8 +40,10 @@ def gaps(a, b):
     return out
 
 
-for a, b in (("k_rank_sort", "k_tile_accum"), ("k_heavy_apply", "k_frontier_prep"),
-             ("k_frontier_prep", "k_frontier_tile_big"), ("k_frontier_tile_big", "k_frontier_resolve"), ("k_frontier_resolve", "k_rank_sort"), ("k_tile_accum", "k_frontier_prep"), ("k_scatter", "k_tile_accum")):
+for a, b in (("k_rank_sort", "k_tile_accum"), ("k_rank_sort", "k_direct_accum"),
+             ("k_frontier_bits", "k_frontier_tile_big"), ("k_frontier_tile_big", "k_frontier_resolve"),
+             ("k_frontier_resolve", "k_rank_sort"), ("k_tile_accum", "k_frontier_bits"),
+             ("k_direct_accum", "k_frontier_bits"), ("k_scatter", "k_tile_accum"), ("k_scan_plan", "k_direct_accum")):
     g = gaps(a, b)[5:30]
     if g:
         print(f"gap {a} -> {b}: median {statistics.median(g):.1f} us, min {min(g):.1f}")

@@ -1,5 +1,5 @@
 """Per-call GPU timeline from a rocprofv3 kernel trace: for each integrate
-call (k_integrate_reset .. k_heavy_apply) and frontier call (k_frontier_prep
+call (k_integrate_reset .. the accumulation) and frontier call (k_frontier_bits
 .. k_rank_sort), the span from the first kernel's start to the last kernel's
 end, the summed kernel time, and the gaps between consecutive kernels.
 Usage: python tools/trace_gaps.py gpurun_out/prof/run_kernel_trace.csv"""
@@ -13,7 +13,8 @@ for r in csv.DictReader(open(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/p
     m = re.search(r"(k_\w+|__amd\w+)", r["Kernel_Name"])
     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), m.group(1) if m else r["Kernel_Name"][:20]))
 rows.sort()
-calls = {"integrate": ("k_integrate_reset", "k_heavy_apply"), "frontier": ("k_frontier_prep", "k_rank_sort")}
+calls = {"integrate": ("k_integrate_reset", "k_tile_accum"), "integrate_direct": ("k_integrate_reset", "k_direct_accum"),
+         "frontier": ("k_frontier_bits", "k_rank_sort")}
 for name, (first, last) in calls.items():
     spans, busy, gaps, prev_end = [], [], [], {}
     cur = None
