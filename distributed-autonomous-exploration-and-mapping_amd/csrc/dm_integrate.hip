@@ -1977,6 +1977,10 @@ int dm_launch_gate(hipStream_t s, unsigned long long* flag, unsigned long long* 
 
 int dm_launch_recount(dm_grid* g) {
   const Geom ge = make_geom(g);
+  // the tile list is rebuilt from position 0: passes still labelling on the
+  // pass stream read it (bulk calls have already joined every stream; an
+  // fmask switch-on inside dm_enqueue_frontiers may not have)
+  DM_HIP(dm_join_pass_stream(g));
   DM_LAUNCH(k_recount, dim3((unsigned)g->NT), dim3(256), 0, g->stream, ge, g->state,
                      g->tile_free, g->fmask, g->fedge);
   DM_HIP(hipGetLastError());
