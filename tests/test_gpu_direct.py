@@ -143,6 +143,7 @@ def test_direct_pipelined_device_and_host_inputs(oracle_lib):
     dev = _device_batches(batches)
     with dm.OccupancyMapper(p) as m:
         m.set_overlap(True)
+        m.set_integrate_mode("direct")  # 16 x 4096 beams: auto would chunk them (binned)
         got = []
         for k, (pose4, rng) in enumerate(dev):
             m.integrate_device(pose4.data_ptr(), pose4.shape[0], rng.data_ptr(), rng.shape[1], amin, inc)
@@ -174,6 +175,7 @@ def test_direct_async_host_inputs_overlap(oracle_lib):
     pinned = [torch.from_numpy(np.ascontiguousarray(r, np.float32)).pin_memory() for _, r in batches]
     with dm.OccupancyMapper(p) as m:
         m.set_overlap(True)
+        m.set_integrate_mode("direct")
         for k, (poses, ranges) in enumerate(batches):
             m.integrate_async(poses, pinned[k].data_ptr(), poses.shape[0], ranges.shape[1], amin, inc)
             om.integrate(poses, ranges, amin, inc)
