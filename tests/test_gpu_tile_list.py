@@ -95,10 +95,10 @@ def test_listed_tiles_that_lose_their_free_cells(oracle_lib):
             ranges = (np.round(rng.uniform(0.5, far, (2, N)) * 1000) / 1000).astype(np.float32)
             m.integrate(poses, ranges, amin, inc)
             om.integrate(poses, ranges, amin, inc)
-            m.frontiers_begin()
-            exp.append(om.frontiers(want_mask=False, want_labels=False)[2])
             if k >= 2:
                 got.append(m.frontiers_end())
+            m.frontiers_begin()
+            exp.append(om.frontiers(want_mask=False, want_labels=False)[2])
         got += [m.frontiers_end(), m.frontiers_end()]
         for fr, e in zip(got, exp):
             np.testing.assert_array_equal(fr.clusters, e)
