@@ -184,6 +184,13 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
       g->dA_cap = ac;
       g->dB_cap = bc;
     }
+    if ((int64_t)S * N > g->dbeam_cap) {  // the call's beams, once per beam (k_scan_plan)
+      for (auto& w : g->iw) {
+        int rc = dev_alloc(&w.dbeams, (int64_t)S * N, "direct beams");
+        if (rc) { g->dbeam_cap = 0; return rc; }
+      }
+      g->dbeam_cap = (int64_t)S * N;
+    }
     if (!g->direct_tiles) {
       for (auto& w : g->iw) {
         int rc = dev_alloc(&w.tile_head, g->NT, "direct tile lists");
@@ -674,7 +681,7 @@ int dm_destroy(dm_grid* g) {
   for (auto& w : g->iw) {
     dev_free(w.pieces); dev_free(w.hitems); dev_free(w.litems); dev_free(w.heavy_list); dev_free(w.slabs);
     dev_free(w.heavy_done); dev_free(w.tile_count); dev_free(w.tile_cur); dev_free(w.cnt); dev_free(w.sh);
-    dev_free(w.units); dev_free(w.ditems); dev_free(w.tile_head); dev_free(w.tile_cand); dev_free(w.tile_slab);
+    dev_free(w.units); dev_free(w.ditems); dev_free(w.dbeams); dev_free(w.tile_head); dev_free(w.tile_cand); dev_free(w.tile_slab);
     dev_free(w.pose4); dev_free(w.ranges);
   }
   dev_free(g->L); dev_free(g->state); dev_free(g->fmask); dev_free(g->fedge);

@@ -1210,11 +1210,22 @@ __device__ inline int32_t unit_beam(const int4& q1, const int4& q2, int32_t o) {
 
 __global__ __launch_bounds__(kPlanThreads) void k_scan_plan(RayArgs a, Geom g, DGeom d,
                                                             const double* __restrict__ pose4,
+                                                            const float* __restrict__ ranges,
+                                                            const double* __restrict__ trig, int32_t unit_blocks,
+                                                            Beam* __restrict__ dbeams,
                                                             int4* __restrict__ units, int4* __restrict__ items,
                                                             int32_t* tile_items, int32_t* tile_cand,
                                                             int32_t* tile_head, int32_t* tile_slab,
                                                             int32_t* __restrict__ heavy_list,
                                                             unsigned long long* cnt) {
+  // the blocks after the units' make the call's beams, once per beam
+  // (k_direct_accum reads them for every tile a beam may cross: no f64 beam
+  // math in the accumulation, and it never reads the call's inputs)
+  if ((int32_t)blockIdx.x >= unit_blocks) {
+    const int64_t b = (int64_t)(blockIdx.x - unit_blocks) * blockDim.x + threadIdx.x;
+    if (b < (int64_t)a.S * a.N) dbeams[b] = dm_make_beam(a, pose4, ranges, trig, (int32_t)(b / a.N), (int32_t)(b % a.N));
+    return;
+  }
   const int64_t per = (int64_t)d.bb * d.bb;
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int32_t s = (int32_t)(u / per);
@@ -1312,8 +1323,8 @@ __device__ inline bool item_at(const DGeom& d, const int4* __restrict__ items, i
 #define DM_DIRECT_OCC 6
 #endif
 __global__ __launch_bounds__(kQuarter, DM_DIRECT_OCC) void k_direct_accum(
-    RayArgs a, Geom g, DGeom d, ApplyArgs p, const double* __restrict__ pose4, const float* __restrict__ ranges,
-    const double* __restrict__ trig, const int4* __restrict__ units, const int4* __restrict__ items,
+    RayArgs a, Geom g, DGeom d, ApplyArgs p, const Beam* __restrict__ dbeams, const int4* __restrict__ units,
+    const int4* __restrict__ items,
     const unsigned long long* __restrict__ cnt, int32_t* tile_items, int32_t* tile_cand, int32_t* tile_head,
     int32_t* tile_slab, int32_t* heavy_done, uint32_t* __restrict__ slabs, int32_t* tile_free,
     float* __restrict__ L, int8_t* __restrict__ state, unsigned long long* ish, int vec_ok, int32_t* tlist,
@@ -1373,7 +1384,7 @@ __global__ __launch_bounds__(kQuarter, DM_DIRECT_OCC) void k_direct_accum(
         const int32_t o = r0 + tid;
         Beam bm;
         bm.flags = 0;
-        if (o < hi) bm = dm_make_beam(a, pose4, ranges, trig, s, unit_beam(q1, q2, o));
+        if (o < hi) bm = dbeams[(int64_t)s * a.N + unit_beam(q1, q2, o)];
         int32_t k0 = 0, k1 = -1;
         const bool has = (bm.flags & 1) && dm_tile_krange(bm, g.r.row0, tx0, ty0, &k0, &k1);
         TilePiece tp;
@@ -1834,8 +1845,11 @@ int launch_direct(dm_grid* g, dm_grid::IntWs& w, hipStream_t fs, const RayArgs& 
   const int64_t units = (int64_t)a.S * d.bb * d.bb;
   KernelTimer t;
   dm_timer_begin(g, "scan_plan", &t, fs);
-  DM_LAUNCH(k_scan_plan, dim3(grid_for(units, kPlanThreads, 1 << 20)), dim3(kPlanThreads), 0, fs, a, ge, d, d_pose4,
-            w.units, w.ditems, w.tile_count, w.tile_cand, w.tile_head, w.tile_slab, w.heavy_list, w.cnt);
+  const int unit_blocks = grid_for(units, kPlanThreads, 1 << 20);
+  const int beam_blocks = grid_for((int64_t)a.S * a.N, kPlanThreads, 1 << 20);
+  DM_LAUNCH(k_scan_plan, dim3(unit_blocks + beam_blocks), dim3(kPlanThreads), 0, fs, a, ge, d, d_pose4, d_ranges,
+            d_trig, unit_blocks, w.dbeams, w.units, w.ditems, w.tile_count, w.tile_cand, w.tile_head, w.tile_slab,
+            w.heavy_list, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (g->overlap) {
@@ -1847,7 +1861,7 @@ int launch_direct(dm_grid* g, dm_grid::IntWs& w, hipStream_t fs, const RayArgs& 
   const int vec_ok = (g->W % 4 == 0) ? 1 : 0;
   dm_timer_begin(g, "tile_accum", &t);
   DM_LAUNCH(k_direct_accum, dim3(grid_for(d.a_cap + d.b_cap, 1, dm_grid::kAccumGrid)), dim3(kQuarter), 0,
-            g->stream, a, ge, d, make_apply(g), d_pose4, d_ranges, d_trig, w.units, w.ditems, w.cnt, w.tile_count,
+            g->stream, a, ge, d, make_apply(g), w.dbeams, w.units, w.ditems, w.cnt, w.tile_count,
             w.tile_cand, w.tile_head, w.tile_slab, w.heavy_done, w.slabs, g->tile_free, g->L, g->state, w.sh, vec_ok,
             g->ftiles, g->ftiles_n, g->fe_flag + kHaltWord);
   dm_timer_end(g, &t);

@@ -253,7 +253,7 @@ struct dm_grid {
   int64_t hitem_cap = 0;
   int64_t heavy_cap = 0;
   // direct front-end capacities (grown on demand; tile arrays once per set)
-  int64_t unit_cap = 0, dA_cap = 0, dB_cap = 0;
+  int64_t unit_cap = 0, dA_cap = 0, dB_cap = 0, dbeam_cap = 0;
   bool direct_tiles = false;  // tile_head / tile_cand / tile_slab allocated
   // integrate front-end: 0 auto (direct for dense scans), 1 binned, 2 direct
   // (dm_set_integrate_mode)
@@ -282,9 +282,9 @@ struct dm_grid {
     int32_t* tile_head = nullptr;     // [NT] the tile's unit list (light units), -1 at rest
     int32_t* tile_cand = nullptr;     // [NT] candidate beams of the tile this call, 0 at rest
     int32_t* tile_slab = nullptr;     // [NT] slab ordinal of a tile with a split unit, -1 at rest
+    Beam* dbeams = nullptr;           // [dbeam_cap] the call's beams (k_scan_plan), read by k_direct_accum
     // device copies of host inputs (dm_integrate / _async) of the calls using
-    // this set: the direct front-end's accumulation reads them on the map
-    // stream, so they are reused only when the set is (free_wait)
+    // this set, reused only when the set is (free_wait)
     double* pose4 = nullptr;
     float* ranges = nullptr;
     int64_t pose_cap = 0, ranges_cap = 0;
