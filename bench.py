@@ -76,8 +76,6 @@ def parse():
                     help="skip the explored-map frontier measurement (frontier_ms_explored)")
     ap.add_argument("--no-host-inputs", action="store_true",
                     help="skip the PCIe-inclusive measurement (value_host_inputs)")
-    ap.add_argument("--integrate-mode", default="auto", choices=["auto", "binned", "direct"],
-                    help="libdm's integrate front-end (dm_set_integrate_mode; results identical)")
     ap.add_argument("--step-trace", default=None,
                     help="C3 / C4: write every timed step's host start-to-start time (us) to this JSON file")
     return ap.parse_args()
@@ -230,7 +228,6 @@ def main():
                            group=dist.group.WORLD if world_size > 1 else None,
                            timeout=args.collective_timeout)
     band = mapper.band
-    band.set_integrate_mode(args.integrate_mode)
     S, N = args.robots, args.beams
 
     def integrate(k):
@@ -478,8 +475,6 @@ def main():
             },
             "frontier_ms": t_fr * 1e3,
             "integrate_ms": t_int * 1e3,
-            # libdm's integrate front-end on these batches (dm_set_integrate_mode)
-            "integrate_front_end": "direct" if band.last_integrate_direct() else "binned",
             "integrate_updates_per_s": U_mean / t_int,
             "updates_per_batch": U_mean,
             "touched_cells_per_batch": T_mean,
@@ -820,7 +815,6 @@ def run_config(args):
     }
     mapper = dm.OccupancyMapper(params, device=dev_i)
     mapper.set_overlap(not args.no_overlap)  # PMC passes: --no-overlap (one dispatch at a time)
-    mapper.set_integrate_mode(args.integrate_mode)
     try:
         if args.config in ("C1", "C2"):
             out = _run_replay(args, np, torch, synth, mapper, params, amin, dev)

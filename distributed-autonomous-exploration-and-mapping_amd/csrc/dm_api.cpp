@@ -162,60 +162,6 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
     }
     g->heavy_cap = heavy;
   }
-  if (dm_use_direct(g, S, N)) {
-    // direct front-end (dm_integrate.hip): S * bb^2 units, region A for the
-    // heavy units' chunks (two per scan expected; more spill into B), region
-    // B for the tiles' unit lists and any spilled chunks (<= 4 heavy units
-    // per scan: a sensor lies in at most 4 widened tile boxes), as many slabs
-    const int64_t bb = dm_direct_bb(g);
-    const int64_t units = std::max<int64_t>(1, (int64_t)S * bb * bb);
-    const int64_t chunks = (N + 255) / 256;
-    const int64_t a_cap = std::max<int64_t>(64, 2 * (int64_t)S * chunks);
-    const int64_t b_cap = units + 4 * (int64_t)S * chunks;
-    if (units > g->unit_cap || a_cap > g->dA_cap || b_cap > g->dB_cap) {
-      const int64_t uc = std::max(units, g->unit_cap), ac = std::max(a_cap, g->dA_cap),
-                    bc = std::max(b_cap, g->dB_cap);
-      for (auto& w : g->iw) {
-        int rc = dev_alloc(&w.units, 3 * uc, "direct units");
-        if (!rc) rc = dev_alloc(&w.ditems, ac + bc, "direct work items");
-        if (rc) { g->unit_cap = g->dA_cap = g->dB_cap = 0; return rc; }
-      }
-      g->unit_cap = uc;
-      g->dA_cap = ac;
-      g->dB_cap = bc;
-    }
-    if ((int64_t)S * N > g->dbeam_cap) {  // the call's beams, once per beam (k_scan_plan)
-      for (auto& w : g->iw) {
-        int rc = dev_alloc(&w.dbeams, (int64_t)S * N, "direct beams");
-        if (rc) { g->dbeam_cap = 0; return rc; }
-      }
-      g->dbeam_cap = (int64_t)S * N;
-    }
-    if (!g->direct_tiles) {
-      for (auto& w : g->iw) {
-        int rc = dev_alloc(&w.tile_head, g->NT, "direct tile lists");
-        if (!rc) rc = dev_alloc(&w.tile_cand, g->NT, "direct tile candidates");
-        if (!rc) rc = dev_alloc(&w.tile_slab, g->NT, "direct tile slabs");
-        if (rc) return rc;
-        DM_HIP(hipMemset(w.tile_head, 0xFF, sizeof(int32_t) * (size_t)g->NT));
-        DM_HIP(hipMemset(w.tile_cand, 0, sizeof(int32_t) * (size_t)g->NT));
-        DM_HIP(hipMemset(w.tile_slab, 0xFF, sizeof(int32_t) * (size_t)g->NT));
-      }
-      g->direct_tiles = true;
-    }
-    const int64_t slabs = std::min<int64_t>(g->NT, 4 * (int64_t)S + 4);
-    if (slabs > g->heavy_cap) {
-      for (auto& w : g->iw) {
-        int rc = dev_alloc(&w.heavy_list, slabs, "heavy tiles");
-        if (!rc) rc = dev_alloc(&w.slabs, slabs * 2 * DM_TILE * DM_TILE, "heavy-tile slabs");
-        if (!rc) rc = dev_alloc(&w.heavy_done, slabs, "heavy-tile item tickets");
-        if (rc) { g->heavy_cap = 0; return rc; }
-        DM_HIP(hipMemset(w.slabs, 0, sizeof(uint32_t) * (size_t)(slabs * 2 * DM_TILE * DM_TILE)));
-        DM_HIP(hipMemset(w.heavy_done, 0, sizeof(int32_t) * (size_t)slabs));
-      }
-      g->heavy_cap = slabs;
-    }
-  }
   if (2 * (int64_t)N > g->trig_cap) {
     int rc = dev_alloc(&g->trig, 2 * (int64_t)N, "trig table");
     if (rc) return rc;
@@ -681,7 +627,6 @@ int dm_destroy(dm_grid* g) {
   for (auto& w : g->iw) {
     dev_free(w.pieces); dev_free(w.hitems); dev_free(w.litems); dev_free(w.heavy_list); dev_free(w.slabs);
     dev_free(w.heavy_done); dev_free(w.tile_count); dev_free(w.tile_cur); dev_free(w.cnt); dev_free(w.sh);
-    dev_free(w.units); dev_free(w.ditems); dev_free(w.dbeams); dev_free(w.tile_head); dev_free(w.tile_cand); dev_free(w.tile_slab);
     dev_free(w.pose4); dev_free(w.ranges);
   }
   dev_free(g->L); dev_free(g->state); dev_free(g->fmask); dev_free(g->fedge);
@@ -792,8 +737,8 @@ int enqueue_host_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N
     hp[4 * s + 2] = cos(yaw);  // C library, as the oracle
     hp[4 * s + 3] = sin(yaw);
   }
-  // into the set's buffers: their last readers (the front-end on fs, the
-  // direct accumulation of the set's previous call) are done (above)
+  // into the set's buffers: their last readers (the front-end of the set's
+  // previous call, on fs) are done (above)
   if (S > 0)
     DM_HIP(hipMemcpyAsync(w.pose4, hp, sizeof(double) * 4 * (size_t)S, hipMemcpyHostToDevice, fs));
   if (nb > 0)
@@ -863,8 +808,7 @@ int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out) {
   const unsigned long long* fs = g->h_sh + kShards * kShardWords;
   const unsigned long long* ic = g->h_cnt + CNT_N;  // the last integrate call's counters
   const uint64_t items = ic[CNT_ITEMS] + ic[CNT_LITEMS] + ic[CNT_SITEMS];  // heavy + light + sparse items
-  // pieces: binned front-end's count, or the direct accumulation's (shards)
-  const uint64_t pieces = ic[CNT_SEGS] + dm_shard_sum(g->h_sh, SH_P);
+  const uint64_t pieces = ic[CNT_SEGS];
   const uint64_t v[kNStats] = {dm_shard_sum(g->h_sh, SH_U),  dm_shard_sum(g->h_sh, SH_T),
                                dm_shard_sum(g->h_sh, SH_TH), pieces,
                                ic[CNT_ACTIVE],               items,
@@ -1331,24 +1275,6 @@ int dm_set_overlap(dm_grid* g, int32_t on) {
     w.free_owed = false;
     w.free_wait = nullptr;
   }
-  return DM_OK;
-}
-
-int dm_set_integrate_mode(dm_grid* g, int32_t mode) {
-  if (g && g->sh) return dm_sh_set_integrate_mode(g, mode);
-  int rc = check_grid(g);
-  if (rc || (rc = use_device(g))) return rc;
-  if (mode < 0 || mode > 2) return dm_set_error(DM_ERR_INVALID_ARG, "mode must be 0 (auto), 1 (binned) or 2 (direct)");
-  DM_HIP(dm_sync_all(g));
-  g->integrate_mode = mode;
-  return DM_OK;
-}
-
-int dm_last_integrate_direct(const dm_grid* g, int32_t* direct) {
-  int rc = check_grid(g);
-  if (rc) return rc;
-  if (!direct) return dm_set_error(DM_ERR_INVALID_ARG, "direct is NULL");
-  *direct = g->sh ? (g->sh_last_direct ? 1 : 0) : (g->last_direct ? 1 : 0);
   return DM_OK;
 }
 

@@ -987,15 +987,30 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
 }
 
 // Slot s is in use iff its offset inside its shard region is below that
-// shard's allocation count.
-__device__ inline void load_shard_counts(const FGeom& g, const unsigned long long* fsh, int64_t* s_n) {
+// shard's allocation count.  The slot loops walk only the used part of the
+// regions: index v in [0, kShards * span) is offset v % span of shard
+// v / span, with span = the fullest shard's count rounded up to a wave (so a
+// wave stays in one shard), instead of all slot_cap slots (4 per map tile).
+// Returns span (0: no slots in use).
+__device__ inline int64_t load_shard_counts(const FGeom& g, const unsigned long long* fsh, int64_t* s_n) {
+  __shared__ int64_t s_span;
   if (threadIdx.x < kShards)
     s_n[threadIdx.x] = min((int64_t)fsh[threadIdx.x * kShardWords + SH_SLOT], g.slot_per);
   __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t m = 0;
+    for (int i = 0; i < kShards; ++i) m = max(m, s_n[i]);
+    s_span = (m + 63) & ~(int64_t)63;
+  }
+  __syncthreads();
+  return s_span;
 }
 
-__device__ inline bool slot_used(const FGeom& g, const int64_t* s_n, int64_t s) {
-  return s < g.slot_cap && (s % g.slot_per) < s_n[s / g.slot_per];
+// Slot of loop index v (see load_shard_counts) and whether it is in use.
+__device__ inline int64_t slot_at(const FGeom& g, const int64_t* s_n, int64_t span, int64_t v, bool* used) {
+  const int64_t sh = v / span, off = v - sh * span;
+  *used = off < s_n[sh];
+  return sh * g.slot_per + off;
 }
 
 // Roots, and every non-root slot's sums and label folded into its root: the
@@ -1037,13 +1052,13 @@ __global__ __launch_bounds__(256) void k_frontier_resolve(FGeom g, const int32_t
     hacc[0][e] = hacc[1][e] = hacc[2][e] = 0;
     hmin[e] = 0x7FFFFFFFFFFFFFFFll;
   }
-  load_shard_counts(g, fsh, s_n);  // (its barrier also orders the table init)
+  const int64_t span = load_shard_counts(g, fsh, s_n);  // (its barriers also order the table init)
   const int lane = __lane_id();
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   // wave-aligned (the fused compaction below allocates per wave)
-  for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); s0 < g.slot_cap; s0 += stride) {
-    const int64_t s = s0 + lane;
-    const bool used = slot_used(g, s_n, s);
+  for (int64_t v0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); v0 < kShards * span; v0 += stride) {
+    bool used;
+    const int64_t s = slot_at(g, s_n, span, v0 + lane, &used);
     const int32_t r = used ? dm_uf_root(slot_parent, (int32_t)s, &cnt[CNT_OVERFLOW], kOvUnionFind) : -1;
     if (used) slot_root[s] = r;
     if (fuse) {
@@ -1100,12 +1115,13 @@ __global__ __launch_bounds__(256) void k_frontier_compact(FGeom g, const int32_t
                                                           unsigned long long* cnt,
                                                           const unsigned long long* fsh) {
   __shared__ int64_t s_n[kShards];
-  load_shard_counts(g, fsh, s_n);
+  const int64_t span = load_shard_counts(g, fsh, s_n);
   const int lane = __lane_id();
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); s0 < g.slot_cap; s0 += stride) {
-    const int64_t s = s0 + lane;
-    bool keep = slot_used(g, s_n, s) && slot_root[s] == (int32_t)s;
+  for (int64_t v0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); v0 < kShards * span; v0 += stride) {
+    bool used;
+    const int64_t s = slot_at(g, s_n, span, v0 + lane, &used);
+    bool keep = used && slot_root[s] == (int32_t)s;
     const long long sz = keep ? slot_acc[3 * s] : 0;
     keep = keep && sz >= g.min_size;
     const unsigned long long bal = __ballot(keep);

@@ -30,7 +30,6 @@
 
 DM_PH_DECL(integrate)
 DM_TL_DECL(accum)
-DM_TL_DECL(daccum)
 
 namespace {
 
@@ -1162,369 +1161,6 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
   DM_TL_END(accum, tl_word);
 }
 
-// ---- direct front-end (dense scans) ----------------------------------------
-// For scans with many beams (C3 / C4: 4096 per scan) the binned front-end
-// (k_beam_prep -> k_plan -> k_scatter: every beam's pieces enumerated twice
-// and stored, then binned by tile) is a 40 us chain of latency-bound kernels
-// in series with the accumulation.  The direct front-end finds the pieces
-// from the other side: a scan can only reach the tiles of its reach box, and
-// a tile only sees the beams whose angle falls in its angular span from the
-// sensor (dm_tile_candidates, a superset), each of which gives its cells in
-// the tile in closed form (dm_tile_krange).  So:
-//   k_scan_plan    one thread per (scan, reach-box tile) unit: candidate beam
-//                  intervals; a unit whose widened tile box holds the sensor
-//                  (every beam a candidate, every piece starting at the
-//                  sensor's cell) is split into chunks of kDirectChunk
-//                  candidates over workgroups and its tile merges in a slab
-//                  (the heavy tiles of the binned path; a point lies in at
-//                  most 4 widened boxes, so at most 4 slabs per scan); every
-//                  other unit joins its tile's unit list, which ONE work item
-//                  walks, so tiles reached by several scans need no merge.
-//   k_direct_accum one work item per workgroup: the candidates' beams
-//                  (dm_make_beam) and k-ranges, the walk into the LDS count
-//                  tile, then the fused log-odds apply (or the slab, ticket,
-//                  and the last item's apply) — the same apply as k_tile_accum.
-// The pieces found are exactly the binned front-end's (tests/native emulation,
-// test_emulated_kernels.py direct cases), so U, T, L and state are identical.
-constexpr int kDirectChunk = 256;  // candidates per round / per heavy chunk
-
-struct DGeom {
-  int32_t nmax;           // reach in cells (>= any beam's n)
-  int32_t bb;             // tiles per side of a scan's reach box: units per scan = bb * bb
-  int64_t unit_cap;       // unit records
-  int64_t a_cap, b_cap;   // item regions A (heavy chunks) and B (unit lists, spilled chunks)
-  int64_t slab_cap;       // slabs (heavy_cap)
-  double amin, inc;       // beam angles: the trig table's phi_i = amin + i * inc
-};
-static_assert(sizeof(DGeom) == 56, "DGeom has no implicit padding");
-
-// Beam index of candidate ordinal o of a unit (its intervals in order).
-__device__ inline int32_t unit_beam(const int4& q1, const int4& q2, int32_t o) {
-  const int32_t n0 = q1.y - q1.x + 1;
-  if (o < n0) return q1.x + o;
-  o -= n0;
-  const int32_t n1 = q1.w - q1.z + 1;
-  if (o < n1) return q1.z + o;
-  return q2.x + (o - n1);
-}
-
-__global__ __launch_bounds__(kPlanThreads) void k_scan_plan(RayArgs a, Geom g, DGeom d,
-                                                            const double* __restrict__ pose4,
-                                                            const float* __restrict__ ranges,
-                                                            const double* __restrict__ trig, int32_t unit_blocks,
-                                                            Beam* __restrict__ dbeams,
-                                                            int4* __restrict__ units, int4* __restrict__ items,
-                                                            int32_t* tile_items, int32_t* tile_cand,
-                                                            int32_t* tile_head, int32_t* tile_slab,
-                                                            int32_t* __restrict__ heavy_list,
-                                                            unsigned long long* cnt) {
-  // the blocks after the units' make the call's beams, once per beam
-  // (k_direct_accum reads them for every tile a beam may cross: no f64 beam
-  // math in the accumulation, and it never reads the call's inputs)
-  if ((int32_t)blockIdx.x >= unit_blocks) {
-    const int64_t b = (int64_t)(blockIdx.x - unit_blocks) * blockDim.x + threadIdx.x;
-    if (b < (int64_t)a.S * a.N) dbeams[b] = dm_make_beam(a, pose4, ranges, trig, (int32_t)(b / a.N), (int32_t)(b % a.N));
-    return;
-  }
-  const int64_t per = (int64_t)d.bb * d.bb;
-  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int32_t s = (int32_t)(u / per);
-  int32_t t = -1, c = 0, all = 0;
-  BeamSpan sp;
-  sp.n_iv = 0;
-  sp.inside = 0;
-  if (s < a.S) {
-    int32_t xl, xh, yl, yh;
-    if (dm_scan_tiles(a, g.r, pose4, s, d.nmax, &xl, &xh, &yl, &yh)) {
-      const int32_t v = (int32_t)(u - (int64_t)s * per);
-      const int32_t tx = xl + v % d.bb, ty = yl + v / d.bb;
-      if (tx <= xh && ty <= yh) {
-        sp = dm_tile_candidates(a, g.r, pose4, s, tx, ty, d.amin, d.inc);
-        c = sp.count();
-        if (c > 0) {
-          t = ty * g.r.TX + tx;
-          all = sp.inside;
-        }
-      }
-    }
-  }
-  const bool heavy = all && c > kDirectChunk;
-  const int32_t n_chunks = heavy ? (c + kDirectChunk - 1) / kDirectChunk : 0;
-  // unit records, heavy chunks (region A first, the overflow into region B)
-  // and unit-list items (region B) by wave-aggregated bumps
-  unsigned long long* const c2[2] = {&cnt[CNT_ACTIVE], &cnt[CNT_ITEMS]};
-  const unsigned long long w2[2] = {c > 0 ? 1ull : 0ull, (unsigned long long)n_chunks};
-  unsigned long long g2[2];
-  wave_alloc_n<2>(c2, w2, g2);
-  const int64_t ui = (int64_t)g2[0];
-  const bool spill = heavy && (int64_t)g2[1] + n_chunks > d.a_cap;
-  // a light unit's tile gets one list item, made by the unit that found the
-  // list empty
-  int32_t prev = -1;
-  if (c > 0 && !heavy && ui < d.unit_cap) prev = atomicExch(&tile_head[t], (int32_t)ui);
-  const bool list_item = c > 0 && !heavy && prev < 0 && ui < d.unit_cap;
-  unsigned long long* const cb[1] = {&cnt[CNT_LITEMS]};
-  const unsigned long long wb[1] = {(list_item ? 1ull : 0ull) + (spill ? (unsigned long long)n_chunks : 0ull)};
-  unsigned long long gb[1];
-  wave_alloc_n<1>(cb, wb, gb);
-  if (c <= 0) return;
-  if (ui >= d.unit_cap) {
-    atomicOr(&cnt[CNT_IOVERFLOW], 4ull);  // cannot happen (unit_cap = S * bb * bb)
-    return;
-  }
-  units[3 * ui + 0] = make_int4(t, s, c, all | (int32_t)((uint32_t)prev << 1));
-  units[3 * ui + 1] = make_int4(sp.lo[0], sp.hi[0], sp.n_iv > 1 ? sp.lo[1] : 0, sp.n_iv > 1 ? sp.hi[1] : -1);
-  units[3 * ui + 2] = make_int4(sp.n_iv > 2 ? sp.lo[2] : 0, sp.n_iv > 2 ? sp.hi[2] : -1, sp.n_iv, 0);
-  atomicAdd(&tile_cand[t], c);
-  int64_t bpos = (int64_t)gb[0];
-  if (list_item) {
-    if (bpos < d.b_cap) items[d.a_cap + bpos] = make_int4(t, -1, 0, 0);
-    else atomicOr(&cnt[CNT_IOVERFLOW], 4ull);
-    ++bpos;
-    atomicAdd(&tile_items[t], 1);
-  }
-  if (heavy) {
-    // the tile merges in a slab: the first heavy unit of the tile takes one
-    if (atomicCAS(&tile_slab[t], -1, -2) == -1) {
-      const unsigned long long ord = atomicAdd(&cnt[CNT_HEAVY], 1ull);
-      if ((int64_t)ord < d.slab_cap) {
-        heavy_list[ord] = t;
-        atomicExch(&tile_slab[t], (int32_t)ord);
-      } else {
-        atomicOr(&cnt[CNT_IOVERFLOW], 4ull);  // cannot happen (slab_cap >= 4 units per scan)
-      }
-    }
-    atomicAdd(&tile_items[t], n_chunks);
-    for (int32_t q = 0; q < n_chunks; ++q) {
-      const int4 it = make_int4(t, (int32_t)ui, q * kDirectChunk, min(kDirectChunk, c - q * kDirectChunk));
-      const int64_t ai = (int64_t)g2[1] + q;
-      if (!spill) {
-        items[ai] = it;
-        continue;
-      }
-      // region A ran out: the chunks go to region B, and the A slots this
-      // unit was given (counted in CNT_ITEMS) are marked dead
-      if (ai < d.a_cap) items[ai] = make_int4(-1, -1, 0, 0);
-      if (bpos + q < d.b_cap) items[d.a_cap + bpos + q] = it;
-      else atomicOr(&cnt[CNT_IOVERFLOW], 4ull);
-    }
-  }
-}
-
-__device__ inline bool item_at(const DGeom& d, const int4* __restrict__ items, int64_t it, int64_t na, int64_t nb,
-                               int4* out) {
-  const bool in_a = it < d.a_cap;
-  const bool valid = in_a ? it < na : it - d.a_cap < nb;
-  *out = items[it];  // the index is valid memory whatever the counts (a loaded round with them)
-  return valid;
-}
-
-#ifndef DM_DIRECT_OCC
-#define DM_DIRECT_OCC 6
-#endif
-__global__ __launch_bounds__(kQuarter, DM_DIRECT_OCC) void k_direct_accum(
-    RayArgs a, Geom g, DGeom d, ApplyArgs p, const Beam* __restrict__ dbeams, const int4* __restrict__ units,
-    const int4* __restrict__ items,
-    const unsigned long long* __restrict__ cnt, int32_t* tile_items, int32_t* tile_cand, int32_t* tile_head,
-    int32_t* tile_slab, int32_t* heavy_done, uint32_t* __restrict__ slabs, int32_t* tile_free,
-    float* __restrict__ L, int8_t* __restrict__ state, unsigned long long* ish, int vec_ok, int32_t* tlist,
-    unsigned long long* tlist_n, const unsigned long long* __restrict__ halt) {
-  __shared__ uint32_t tl[kTileWords + 64];  // + one spare word per lane (walk_tp_plain)
-  __shared__ int32_t s_T, s_free, s_last;
-  __shared__ uint32_t s_U;
-  __shared__ unsigned long long s_accT, s_accU, s_accP;
-  const int tid = threadIdx.x, lane = lane_id();
-  DM_TL_BEGIN();
-  [[maybe_unused]] unsigned long long tl_word = 0;  // timeline (phase build): items | finisher ticks << 32
-  // halt word, item counts and this workgroup's first item in ONE round: the
-  // item's index does not depend on the counts (regions at fixed offsets)
-  const unsigned long long hv = *halt;
-  const int64_t NA = min((int64_t)cnt[CNT_ITEMS], d.a_cap);
-  const int64_t NB = min((int64_t)cnt[CNT_LITEMS], d.b_cap);
-  const int64_t G = gridDim.x;
-  const int64_t end = d.a_cap + NB;
-  int4 item;
-  bool valid = blockIdx.x < end && item_at(d, items, blockIdx.x, NA, NB, &item);
-  if (hv != 0ull) {
-    DM_TL_END(daccum, 0);
-    return;
-  }
-  for (int e = tid; e < kTileWords; e += kQuarter) tl[e] = 0u;
-  if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; s_accT = 0ull; s_accU = 0ull; s_accP = 0ull; }
-  __syncthreads();
-  const int cx = (tid & 15) * 4;
-  CellRows<4> cells;
-  for (int64_t it = blockIdx.x; it < end; it += G) {
-    if (it != (int64_t)blockIdx.x) valid = item_at(d, items, it, NA, NB, &item);
-    const int32_t tile = __builtin_amdgcn_readfirstlane(item.x);
-    if (!valid || tile < 0) continue;  // past the counts, or a dead region-A slot
-    tl_word += 1;
-    const int32_t uid = __builtin_amdgcn_readfirstlane(item.y);
-    const int32_t c0 = __builtin_amdgcn_readfirstlane(item.z);
-    const int32_t cn = __builtin_amdgcn_readfirstlane(item.w);
-    const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
-    // the tile's state after the plan, one round
-    const int32_t slab = __builtin_amdgcn_readfirstlane(tile_slab[tile]);
-    const int32_t n_it = __builtin_amdgcn_readfirstlane(tile_items[tile]);
-    const int32_t cand = __builtin_amdgcn_readfirstlane(tile_cand[tile]);
-    const int32_t head = uid < 0 ? __builtin_amdgcn_readfirstlane(tile_head[tile]) : uid;
-    const int32_t tfree = tile_free[tile];
-    const bool merged = slab >= 0;  // the tile has a split unit: its items meet in slab `slab`
-    if (!merged) cells.prefetch(g, tx0, ty0, tid >> 4, 16, cx, L, state, vec_ok);
-    // walk: a chunk item its unit's candidates [c0, c0 + cn); a list item
-    // every unit of the tile's list, in rounds of kDirectChunk candidates
-    int32_t u = 0, npc = 0;
-    for (int32_t un = head, guard = 0; un >= 0 && guard <= a.S; ++guard) {  // a list holds <= S units
-      const int4 q0 = units[3 * un], q1 = units[3 * un + 1], q2 = units[3 * un + 2];
-      const int32_t s = __builtin_amdgcn_readfirstlane(q0.y);
-      const int32_t uc = __builtin_amdgcn_readfirstlane(q0.z);
-      const int32_t fl = __builtin_amdgcn_readfirstlane(q0.w);
-      const int32_t lo = uid < 0 ? 0 : c0, hi = uid < 0 ? uc : c0 + cn;
-      for (int32_t r0 = lo; r0 < hi; r0 += kDirectChunk) {
-        const int32_t o = r0 + tid;
-        Beam bm;
-        bm.flags = 0;
-        if (o < hi) bm = dbeams[(int64_t)s * a.N + unit_beam(q1, q2, o)];
-        int32_t k0 = 0, k1 = -1;
-        const bool has = (bm.flags & 1) && dm_tile_krange(bm, g.r.row0, tx0, ty0, &k0, &k1);
-        TilePiece tp;
-        tp.addr0 = 0; tp.addr_end = -1; tp.len = 0; tp.da = 0; tp.db = 0; tp.rem0 = 0; tp.two_adb = 0;
-        tp.two_n = 1;
-        if (has) tp = dm_tile_piece(bm, k0, k1, g.r.row0, tx0, ty0, kLdsPitch);
-        // the sensor's own tiles (every beam a candidate): pieces share their
-        // first cells, the staggered walk; elsewhere the plain one
-        u += (fl & 1) ? walk_tp(tl, tp, has ? tp.len : 0, lane) : walk_tp_plain(tl, tp, has ? tp.len : 0, lane);
-        npc += has ? 1 : 0;
-      }
-      un = uid < 0 ? (fl >> 1) : -1;  // the next unit of the tile's list
-    }
-    for (int o = 32; o > 0; o >>= 1) npc += __shfl_xor(npc, o);
-    const bool inside = tx0 + DM_TS <= g.r.W && ty0 + DM_TS <= g.r.R;  // workgroup-uniform
-    if (inside && !merged) {
-      for (int o = 32; o > 0; o >>= 1) u += __shfl_xor(u, o);
-      if (lane == 0) atomicAdd(&s_U, (uint32_t)u);
-    }
-    if (lane == 0 && npc) atomicAdd(&s_accP, (unsigned long long)npc);
-    __syncthreads();
-    if (!merged) {
-      // the tile's only item (exclusive): apply from the count tile
-      cells.apply(g, p, tx0, ty0, tid >> 4, 16, cx, L, state,
-                  [&](int ly, uint32_t* h4, uint32_t* m4) {
-                    for (int e = 0; e < 4; ++e) {
-                      const uint32_t v = tl[ly * kLdsPitch + cx + e];
-                      h4[e] = v >> 16;
-                      m4[e] = v & 0xFFFFu;
-                    }
-                  },
-                  &s_T, &s_free, inside ? nullptr : &s_U);
-      __syncthreads();
-      if (tid == 0) {
-        s_accT += (unsigned long long)s_T;
-        s_accU += (unsigned long long)s_U;
-        if (s_free) tile_free[tile] = free_update(tfree, s_free, tile, tlist, tlist_n);
-        tile_items[tile] = 0;  // the tile's per-call state back at rest
-        tile_cand[tile] = 0;
-        tile_head[tile] = -1;
-      }
-    } else {
-      // merged: counts into the slab (a cell's count is at most the tile's
-      // candidates: below 65536 packed, hits << 16 | misses), then the
-      // ticket; the last item applies the slab (k_tile_accum's heavy path)
-      const bool wide = cand >= 65536;
-      uint32_t* sh = slabs + (int64_t)slab * (2 * DM_TS * DM_TS);
-      if (wide) {
-        for (int e = tid; e < DM_TS * DM_TS; e += kQuarter) {
-          const uint32_t v = tl[(e >> 6) * kLdsPitch + (e & 63)];
-          const uint32_t h = v >> 16, m = v & 0xFFFFu;
-          if (h) atomicAdd(&sh[e], h);
-          if (m) atomicAdd(&sh[DM_TS * DM_TS + e], m);
-        }
-      } else {
-        for (int e = tid; e < DM_TS * DM_TS; e += kQuarter) {
-          const uint32_t v = tl[(e >> 6) * kLdsPitch + (e & 63)];
-          if (v) atomicAdd(&sh[e], v);
-        }
-      }
-      // every item's adds are performed at the memory side before its
-      // ticket (k_tile_accum: the same hand-off without a release fence)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) s_last = atomicAdd(&heavy_done[slab], 1) == n_it - 1;
-      __syncthreads();
-      if (s_last) {
-#ifdef DM_PHASE_TIMING
-        const long long tf0 = wall_clock64();
-#endif
-        for (int q = 0; q < 4; ++q) heavy_quarter(g, p, slab, q, tile, wide, slabs, L, state, &s_T, &s_free, &s_U);
-        __syncthreads();
-        if (tid == 0) {
-          finish_tile(g, tile, s_T, s_free, s_U, true, tile_items, tile_free, tfree, tlist, tlist_n, ish);
-          heavy_done[slab] = 0;  // the tile's per-call state back at rest
-          tile_cand[tile] = 0;
-          tile_head[tile] = -1;
-          tile_slab[tile] = -1;
-        }
-#ifdef DM_PHASE_TIMING
-        tl_word += (unsigned long long)(wall_clock64() - tf0) << 32;
-#endif
-      }
-    }
-    __syncthreads();
-    for (int e = tid; e < kTileWords; e += kQuarter) tl[e] = 0u;
-    if (tid == 0) { s_T = 0; s_free = 0; s_U = 0u; }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    unsigned long long* sh = ish + (blockIdx.x % kShards) * kShardWords;
-    if (s_accT) atomicAdd(&sh[SH_T], s_accT);
-    if (s_accU) atomicAdd(&sh[SH_U], s_accU);
-    if (s_accP) atomicAdd(&sh[SH_P], s_accP);
-  }
-  DM_TL_END(daccum, tl_word);
-}
-
-// fmask records of the tiles the direct front-end's items touched (whole
-// records; a merged tile's items rewrite the same bytes), one wave per item.
-__global__ __launch_bounds__(256) void k_fmask_direct(Geom g, DGeom d, const int4* __restrict__ items,
-                                                      const unsigned long long* __restrict__ cnt,
-                                                      const int8_t* __restrict__ state, uint8_t* __restrict__ fmask,
-                                                      uint64_t* __restrict__ fedge,
-                                                      const unsigned long long* __restrict__ halt) {
-  if (*halt) return;
-  const int64_t NA = min((int64_t)cnt[CNT_ITEMS], d.a_cap);
-  const int64_t NB = min((int64_t)cnt[CNT_LITEMS], d.b_cap);
-  const int lane = __lane_id();
-  for (int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); q < NA + NB; q += (int64_t)gridDim.x * 4) {
-    const int64_t it = q < NA ? q : d.a_cap + (q - NA);
-    const int32_t tile = __builtin_amdgcn_readfirstlane(items[it].x);
-    if (tile < 0) continue;
-    const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
-    const int32_t x0 = tx0 + (lane & 3) * 16;
-    uint8_t* tm = fmask + (int64_t)tile * (DM_TS * 16);
-    EdgeAcc ea;
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      const int ly = 16 * qq + (lane >> 2);
-      const int32_t y = ty0 + ly;
-      uint32_t out = 0u;
-      if (y < g.r.R) {
-        const int64_t off = (int64_t)y * g.r.W + x0;
-        if (x0 + 16 <= g.r.W && (off & 15) == 0) {
-          const uint4 v = *reinterpret_cast<const uint4*>(state + off);
-          const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int k = 0; k < 4; ++k) out |= (uint32_t)state_nibbles(wd[k]) << (8 * k);
-        } else {
-          for (int k = 0; k < 4; ++k) out |= (uint32_t)state_nibbles_at(g, state, x0 + 4 * k, y) << (8 * k);
-        }
-      }
-      *reinterpret_cast<uint32_t*>(tm + ly * 16 + (lane & 3) * 4) = out;
-      edge_acc(ea, out, qq, lane);
-    }
-    edge_store(ea, fedge, tile, ~0ull, lane);
-  }
-}
-
 // ---- maintenance kernels ----------------------------------------------------
 
 // Per-call reset of the device counters and integrate shards in one launch.
@@ -1824,62 +1460,6 @@ int grid_for(int64_t n, int threads, int64_t cap = 8192) {
 
 DM_PH_READER(integrate)
 DM_TL_READER(accum)
-DM_TL_READER(daccum)
-
-namespace {
-
-// The direct front-end's launches: the plan on the
-// front-end stream, the hand-off, the accumulation (timed as "tile_accum", the
-// roofline kernel either way) and the fmask records on the map stream.
-int launch_direct(dm_grid* g, dm_grid::IntWs& w, hipStream_t fs, const RayArgs& a, const Geom& ge,
-                  const double* d_pose4, const float* d_ranges, const double* d_trig) {
-  DGeom d;
-  d.nmax = g->nmax;
-  d.bb = dm_direct_bb(g);
-  d.unit_cap = g->unit_cap;
-  d.a_cap = g->dA_cap;
-  d.b_cap = g->dB_cap;
-  d.slab_cap = g->heavy_cap;
-  d.amin = (double)g->trig_amin;  // the trig table's angles: (double)amin + i * (double)inc
-  d.inc = (double)g->trig_inc;
-  const int64_t units = (int64_t)a.S * d.bb * d.bb;
-  KernelTimer t;
-  dm_timer_begin(g, "scan_plan", &t, fs);
-  const int unit_blocks = grid_for(units, kPlanThreads, 1 << 20);
-  const int beam_blocks = grid_for((int64_t)a.S * a.N, kPlanThreads, 1 << 20);
-  DM_LAUNCH(k_scan_plan, dim3(unit_blocks + beam_blocks), dim3(kPlanThreads), 0, fs, a, ge, d, d_pose4, d_ranges,
-            d_trig, unit_blocks, w.dbeams, w.units, w.ditems, w.tile_count, w.tile_cand, w.tile_head, w.tile_slab,
-            w.heavy_list, w.cnt);
-  dm_timer_end(g, &t);
-  DM_HIP(hipGetLastError());
-  if (g->overlap) {
-    if (int rc = dm_launch_signal(fs, g->fe_flag)) return rc;
-    if (int rc = dm_launch_gate(g->stream, g->fe_flag, g->fe_flag + kHaltWord, 1ull, g->fault_gate ? 1000ull : 0ull,
-                                g->fault_gate ? (1ull << 40) : 0ull))
-      return rc;
-  }
-  const int vec_ok = (g->W % 4 == 0) ? 1 : 0;
-  dm_timer_begin(g, "tile_accum", &t);
-  DM_LAUNCH(k_direct_accum, dim3(grid_for(d.a_cap + d.b_cap, 1, dm_grid::kAccumGrid)), dim3(kQuarter), 0,
-            g->stream, a, ge, d, make_apply(g), w.dbeams, w.units, w.ditems, w.cnt, w.tile_count,
-            w.tile_cand, w.tile_head, w.tile_slab, w.heavy_done, w.slabs, g->tile_free, g->L, g->state, w.sh, vec_ok,
-            g->ftiles, g->ftiles_n, g->fe_flag + kHaltWord);
-  dm_timer_end(g, &t);
-  DM_HIP(hipGetLastError());
-  if (g->overlap) w.free_owed = true;
-  if (!g->fmask_on) {
-    g->fmask_valid = false;
-    return DM_OK;
-  }
-  dm_timer_begin(g, "fmask", &t);
-  DM_LAUNCH(k_fmask_direct, dim3(grid_for(d.a_cap + d.b_cap, 4, 8192)), dim3(256), 0, g->stream, ge, d, w.ditems,
-            w.cnt, g->state, g->fmask, g->fedge, g->fe_flag + kHaltWord);
-  dm_timer_end(g, &t);
-  DM_HIP(hipGetLastError());
-  return DM_OK;
-}
-
-}  // namespace
 
 int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                         const float* d_ranges, const double* d_trig) {
@@ -1918,8 +1498,6 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   ge.nb = nb;
   ge.chunks = dm_integrate_chunks(g, nb);
   ge.chunk_len = (int32_t)((g->nmax + ge.chunks) / ge.chunks);  // ceil((nmax + 1) / chunks)
-  g->last_direct = dm_use_direct(g, S, N);
-  if (g->last_direct) return launch_direct(g, w, fs, a, ge, d_pose4, d_ranges, d_trig);
   const int nblk = (int)((nb * ge.chunks + 255) / 256);
   KernelTimer t;
   dm_timer_begin(g, "beam_prep", &t, fs);

@@ -74,10 +74,6 @@ constexpr int kIntegrateCounters[] = {CNT_ACTIVE, CNT_U, CNT_T, CNT_SEGS, CNT_IT
 constexpr int kIntegrateChunk = 256;
 constexpr int kIntegrateMedium = 1024;
 
-// The direct integrate front-end (dm_integrate.hip: k_scan_plan ->
-// k_direct_accum) in auto mode: scans with at least this many beams that need
-// no chunking (dm_integrate_chunks == 1)
-constexpr int kDirectMinBeams = 1024;
 
 // Sharded counters: same-address device atomics serialise at the memory side
 // (~12 ns each, MI355X_MICROARCH.md price list "fanin"), so per-workgroup
@@ -86,8 +82,8 @@ constexpr int kDirectMinBeams = 1024;
 constexpr int kShards = 32;
 constexpr int kShardWords = 16;  // 128 B per shard
 static_assert(kShards * kShardWords == 512, "k_integrate_reset covers 512 shard words");
-// integrate shard fields (SH_P: ray pieces the direct front-end walked)
-enum { SH_U = 0, SH_T = 1, SH_TH = 2, SH_ACT = 3, SH_P = 4 };
+// integrate shard fields
+enum { SH_U = 0, SH_T = 1, SH_TH = 2, SH_ACT = 3 };
 // frontier shard fields: slots allocated, runs and tiles with frontier
 // cells (the next pass picks its tile kernel from their ratio)
 // and tiles too run-rich for a tile-wave (the next pass sizes the big kernel's grid)
@@ -252,14 +248,6 @@ struct dm_grid {
   int64_t act_cap = 0;
   int64_t hitem_cap = 0;
   int64_t heavy_cap = 0;
-  // direct front-end capacities (grown on demand; tile arrays once per set)
-  int64_t unit_cap = 0, dA_cap = 0, dB_cap = 0, dbeam_cap = 0;
-  bool direct_tiles = false;  // tile_head / tile_cand / tile_slab allocated
-  // integrate front-end: 0 auto (direct for dense scans), 1 binned, 2 direct
-  // (dm_set_integrate_mode)
-  int integrate_mode = 0;
-  bool last_direct = false;  // the last integrate call took the direct front-end
-  bool sh_last_direct = false;  // (sharded parent) band 0's last call did
   // what the front-end hands to the accumulation, one set per call parity
   struct IntWs {
     PackedPiece* pieces = nullptr;    // [segs_cap] ray pieces binned by tile
@@ -272,17 +260,6 @@ struct dm_grid {
     int32_t* tile_cur = nullptr;      // [NT] k_scatter's bin cursor per active tile (k_plan)
     unsigned long long* cnt = nullptr;  // [CNT_N] the integrate counters (kIntegrateCounters)
     unsigned long long* sh = nullptr;   // [kShards][kShardWords] integrate shards
-    // direct front-end (dm_integrate.hip, k_scan_plan / k_direct_accum): one
-    // record per (scan, tile) unit with candidate beams, the tiles' work items
-    // (region A: heavy units' chunks, region B: per-tile unit lists and
-    // spilled chunks), and per-tile state that is back at its rest value
-    // after every call (head -1, candidates 0, slab -1)
-    int4* units = nullptr;            // [unit_cap][3] {tile, scan, count, flags | next << 1}, intervals
-    int4* ditems = nullptr;           // [dA_cap + dB_cap] {tile, unit or -1 (the tile's unit list), c0, count}
-    int32_t* tile_head = nullptr;     // [NT] the tile's unit list (light units), -1 at rest
-    int32_t* tile_cand = nullptr;     // [NT] candidate beams of the tile this call, 0 at rest
-    int32_t* tile_slab = nullptr;     // [NT] slab ordinal of a tile with a split unit, -1 at rest
-    Beam* dbeams = nullptr;           // [dbeam_cap] the call's beams (k_scan_plan), read by k_direct_accum
     // device copies of host inputs (dm_integrate / _async) of the calls using
     // this set, reused only when the set is (free_wait)
     double* pose4 = nullptr;
@@ -514,14 +491,6 @@ inline int32_t dm_integrate_chunks(const dm_grid* g, int64_t nb) {
   return (int32_t)(by_fill < by_len ? by_fill : by_len);
 }
 
-// The front-end an integrate call of S scans x N beams takes.
-inline bool dm_use_direct(const dm_grid* g, int32_t S, int32_t N) {
-  if (g->integrate_mode == 1 || (int64_t)S * N == 0) return false;
-  if (g->integrate_mode == 2) return true;
-  return N >= kDirectMinBeams && dm_integrate_chunks(g, (int64_t)S * N) == 1;
-}
-// tiles per side of a scan's reach box (a reach of nmax cells either side)
-inline int32_t dm_direct_bb(const dm_grid* g) { return (2 * g->nmax) / 64 + 2; }
 
 // ---- launchers (dm_integrate.hip / dm_frontier.hip) -----------------------
 int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
@@ -607,7 +576,6 @@ int dm_sh_frontiers_poll(dm_grid* g, int32_t* ready);
 int dm_sh_assign_goals(dm_grid* g, const double* robots_xy, int32_t n_robots, int64_t min_size, double w,
                        double min_distance, int64_t* out_index, double* out_xy);
 int dm_sh_set_overlap(dm_grid* g, int32_t on);
-int dm_sh_set_integrate_mode(dm_grid* g, int32_t mode);
 int dm_sh_synchronize(dm_grid* g);
 int dm_sh_profile_enable(dm_grid* g, int enable);
 int dm_sh_profile_read(dm_grid* g, dm_kernel_stat* out, int32_t cap, int32_t* n_out);

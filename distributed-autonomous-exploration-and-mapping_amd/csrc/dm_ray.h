@@ -167,171 +167,6 @@ DM_HD inline void dm_for_each_piece(const Beam& b, const RayGeom& g, Emit&& emit
   }
 }
 
-// k = ceil(n * (2Q - 1) / (2 * adb)): the first step whose minor step count
-// q(k) reaches Q (1 <= Q <= adb; operands < 2^31 as in dm_for_each_piece).
-DM_HD inline int32_t dm_k_reaching(const Beam& b, int32_t Q, int32_t den_b, double rden_b) {
-  const int32_t num = b.n * (2 * Q - 1);
-  return dm_udiv(num + den_b - 1, den_b, rden_b);
-}
-
-// The steps of beam b whose cells lie in the 64x64 tile with global first
-// column tx0 and band-local first row ty0 (band starting at global row
-// row0): [*k0, *k1], or false when there are none.  Both coordinates are
-// monotone in k (major = sa + k*ia, minor = sb + ib*q(k) with q
-// non-decreasing), so those cells are ONE k-interval: the major coordinate's
-// range intersected with the steps whose q lies in the tile's minor range,
-// from the same exact integer arithmetic as dm_for_each_piece (its piece in
-// that tile, for an unchunked beam).
-DM_HD inline bool dm_tile_krange(const Beam& b, int32_t row0, int32_t tx0, int32_t ty0, int32_t* k0,
-                                 int32_t* k1) {
-  const int32_t gx0 = tx0, gx1 = tx0 + DM_TS - 1;
-  const int32_t gy0 = row0 + ty0, gy1 = gy0 + DM_TS - 1;
-  const int32_t a0 = b.xmajor ? gx0 : gy0, a1 = b.xmajor ? gx1 : gy1;
-  const int32_t c0 = b.xmajor ? gy0 : gx0, c1 = b.xmajor ? gy1 : gx1;
-  int32_t lo = 0, hi = b.n;
-  if (b.ia > 0) {
-    lo = a0 - b.sa > lo ? a0 - b.sa : lo;
-    hi = a1 - b.sa < hi ? a1 - b.sa : hi;
-  } else if (b.ia < 0) {
-    lo = b.sa - a1 > lo ? b.sa - a1 : lo;
-    hi = b.sa - a0 < hi ? b.sa - a0 : hi;
-  } else if (b.sa < a0 || b.sa > a1) {
-    return false;
-  }
-  if (lo > hi) return false;
-  if (b.ib == 0) {  // the minor coordinate stays sb
-    if (b.sb < c0 || b.sb > c1) return false;
-  } else {
-    int32_t qlo = b.ib > 0 ? c0 - b.sb : b.sb - c1;
-    int32_t qhi = b.ib > 0 ? c1 - b.sb : b.sb - c0;
-    if (qlo < 0) qlo = 0;
-    if (qhi > b.adb) qhi = b.adb;  // q(k) is in [0, adb]
-    if (qlo > qhi) return false;
-    const int32_t den_b = 2 * b.adb;
-    const double rden_b = 1.0 / (double)den_b;
-    if (qlo > 0) {
-      const int32_t k = dm_k_reaching(b, qlo, den_b, rden_b);
-      lo = k > lo ? k : lo;
-    }
-    if (qhi < b.adb) {
-      const int32_t k = dm_k_reaching(b, qhi + 1, den_b, rden_b) - 1;
-      hi = k < hi ? k : hi;
-    }
-    if (lo > hi) return false;
-  }
-  *k0 = lo;
-  *k1 = hi;
-  return true;
-}
-
-// Beams of one scan that may have a cell in a box (a superset: the caller
-// finds each candidate's exact cells with dm_tile_krange).  The box is in
-// metres relative to the sensor, [bx0, bx1] x [by0, by1], already widened by
-// the cells a Bresenham line can stray from its ray (its cells lie within
-// ~1.2 cells of the segment between the true sensor and endpoint positions).
-// A sensor inside the box: every beam.  Otherwise the box subtends < pi seen
-// from the sensor; its corners' angles about the box centre's direction give
-// [th_lo, th_hi], and beam i (angle yaw + amin + i * inc, the trig table's
-// phi_i) is a candidate when that angle is within it mod 2 pi, widened by one
-// beam each side.  Up to three index intervals (the angle range wrapped by
-// -2 pi, 0, +2 pi against [amin, amin + (N-1) inc]); n_iv = 0 when none.
-struct BeamSpan {
-  int32_t lo[3], hi[3];
-  int32_t n_iv;
-  int32_t inside;  // the sensor lies in the box (every beam starts there)
-  DM_HD int32_t count() const {
-    int32_t c = 0;
-    for (int32_t v = 0; v < n_iv; ++v) c += hi[v] - lo[v] + 1;
-    return c;
-  }
-};
-
-DM_HD inline BeamSpan dm_box_beams(double bx0, double by0, double bx1, double by1, double yaw, double amin,
-                                   double inc, int32_t N) {
-  BeamSpan sp;
-  sp.n_iv = 0;
-  sp.inside = bx0 <= 0.0 && bx1 >= 0.0 && by0 <= 0.0 && by1 >= 0.0 ? 1 : 0;
-  const double kPi = 3.14159265358979323846, k2Pi = 2.0 * kPi;
-  const double span_all = (double)(N - 1) * inc;
-  if (sp.inside || !(inc > 0.0) || !(span_all <= 2.0 * k2Pi)) {
-    sp.lo[0] = 0;
-    sp.hi[0] = N - 1;
-    sp.n_iv = N > 0 ? 1 : 0;
-    return sp;
-  }
-  const double thc = atan2(0.5 * (by0 + by1), 0.5 * (bx0 + bx1));
-  double dmin = 0.0, dmax = 0.0;
-  const double cx[4] = {bx0, bx1, bx0, bx1}, cy[4] = {by0, by0, by1, by1};
-  for (int e = 0; e < 4; ++e) {
-    double d = atan2(cy[e], cx[e]) - thc;
-    if (d > kPi) d -= k2Pi;
-    if (d < -kPi) d += k2Pi;
-    dmin = d < dmin ? d : dmin;
-    dmax = d > dmax ? d : dmax;
-  }
-  // the box's angle range relative to beam 0's direction, lo in [0, 2 pi)
-  double lo = thc + dmin - yaw - amin;
-  double hi = thc + dmax - yaw - amin;
-  const double w = floor(lo / k2Pi);
-  lo -= w * k2Pi;
-  hi -= w * k2Pi;
-  for (int s = -1; s <= 1; ++s) {
-    const double l = lo + s * k2Pi, h = hi + s * k2Pi;
-    if (h < -inc || l > span_all + inc) continue;
-    double fl = ceil(l / inc) - 1.0, fh = floor(h / inc) + 1.0;
-    if (fl < 0.0) fl = 0.0;
-    if (fh > (double)(N - 1)) fh = (double)(N - 1);
-    if (fl > fh) continue;
-    // intervals come in increasing order; the one-beam widening can make
-    // neighbours touch: merge, so no beam is listed twice
-    if (sp.n_iv > 0 && (int32_t)fl <= sp.hi[sp.n_iv - 1] + 1) {
-      if ((int32_t)fh > sp.hi[sp.n_iv - 1]) sp.hi[sp.n_iv - 1] = (int32_t)fh;
-      continue;
-    }
-    sp.lo[sp.n_iv] = (int32_t)fl;
-    sp.hi[sp.n_iv] = (int32_t)fh;
-    ++sp.n_iv;
-  }
-  return sp;
-}
-
-// Cells a Bresenham line strays from its ray (see dm_box_beams), rounded up.
-constexpr int32_t kRayStrayCells = 2;
-
-// The band-local tiles scan s can reach: every cell of its beams lies within
-// nmax cells (>= any beam's n) of its sensor cell.  false for a non-finite
-// pose (dm_make_beam skips those beams) or a box outside the band.
-DM_HD inline bool dm_scan_tiles(const RayArgs& a, const RayGeom& g, const double* pose4, int32_t s, int32_t nmax,
-                                int32_t* tx_lo, int32_t* tx_hi, int32_t* ty_lo, int32_t* ty_hi) {
-  const double x = pose4[4 * s + 0], y = pose4[4 * s + 1];
-  if (!(isfinite(x) && isfinite(y) && isfinite(pose4[4 * s + 2]) && isfinite(pose4[4 * s + 3]))) return false;
-  const double fsx = floor((x - a.ox) / a.res), fsy = floor((y - a.oy) / a.res);
-  if (!(fabs(fsx) < 1073741824.0 && fabs(fsy) < 1073741824.0)) return false;
-  const int32_t sx = (int32_t)fsx, syl = (int32_t)fsy - g.row0;
-  int32_t xl = dm_floordiv32(sx - nmax, DM_TS), xh = dm_floordiv32(sx + nmax, DM_TS);
-  int32_t yl = dm_floordiv32(syl - nmax, DM_TS), yh = dm_floordiv32(syl + nmax, DM_TS);
-  xl = xl < 0 ? 0 : xl;
-  yl = yl < 0 ? 0 : yl;
-  xh = xh > g.TX - 1 ? g.TX - 1 : xh;
-  yh = yh > g.TY - 1 ? g.TY - 1 : yh;
-  if (xl > xh || yl > yh) return false;
-  *tx_lo = xl; *tx_hi = xh; *ty_lo = yl; *ty_hi = yh;
-  return true;
-}
-
-// Candidate beams of scan s for band-local tile (tx, ty) (dm_box_beams over
-// the tile widened by kRayStrayCells).
-DM_HD inline BeamSpan dm_tile_candidates(const RayArgs& a, const RayGeom& g, const double* pose4, int32_t s,
-                                         int32_t tx, int32_t ty, double amin, double inc) {
-  const double x = pose4[4 * s + 0], y = pose4[4 * s + 1];
-  const double yaw = atan2(pose4[4 * s + 3], pose4[4 * s + 2]);
-  const double bx0 = a.ox + (double)(tx * DM_TS - kRayStrayCells) * a.res - x;
-  const double bx1 = a.ox + (double)((tx + 1) * DM_TS + kRayStrayCells) * a.res - x;
-  const double by0 = a.oy + (double)(g.row0 + ty * DM_TS - kRayStrayCells) * a.res - y;
-  const double by1 = a.oy + (double)(g.row0 + (ty + 1) * DM_TS + kRayStrayCells) * a.res - y;
-  return dm_box_beams(bx0, by0, bx1, by1, yaw, amin, inc, a.N);
-}
-
 // Cell (x, band-local y) of step k.
 DM_HD inline void dm_cell(const Beam& b, int32_t k, int32_t row0, int32_t* x, int32_t* yl) {
   const int32_t q = dm_minor_steps(b, k);

@@ -574,13 +574,6 @@ int dm_sh_reset(dm_grid* g) {
 
 int dm_sh_synchronize(dm_grid* g) { return sh_sync(g->sh); }
 
-int dm_sh_set_integrate_mode(dm_grid* g, int32_t mode) {
-  dm_shard_set* s = g->sh;
-  for (int r = 0; r < s->P; ++r)
-    if (int rc = dm_set_integrate_mode(s->band[(size_t)r], mode)) return rc;
-  return DM_OK;
-}
-
 int dm_sh_set_overlap(dm_grid* g, int32_t on) {
   dm_shard_set* s = g->sh;
   for (int r = 0; r < s->P; ++r)

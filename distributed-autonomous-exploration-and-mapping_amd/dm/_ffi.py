@@ -171,8 +171,6 @@ SIGNATURES = {
     "dm_frontiers_end": [_vp, _vp, _i64, ctypes.POINTER(_i64)],
     "dm_frontiers_poll": [_vp, ctypes.POINTER(_i32)],
     "dm_set_overlap": [_vp, _i32],
-    "dm_set_integrate_mode": [_vp, _i32],
-    "dm_last_integrate_direct": [_vp, ctypes.POINTER(_i32)],
     "dm_atomic_peak": [ctypes.c_int, _vp, _i32, ctypes.POINTER(_i32)],
     "dm_assign_goals": [_vp, _vp, _i32, ctypes.c_int64, ctypes.c_double, ctypes.c_double, _vp, _vp],
 }

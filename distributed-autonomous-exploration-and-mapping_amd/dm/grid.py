@@ -321,21 +321,6 @@ class OccupancyMapper:
         with self._lock:
             check(self._lib.dm_set_overlap(self._handle(), 1 if on else 0))
 
-    INTEGRATE_MODES = {"auto": 0, "binned": 1, "direct": 2}
-
-    def set_integrate_mode(self, mode: str = "auto"):
-        """dm_set_integrate_mode: the integrate front-end, "auto" (default),
-        "binned" or "direct" (results identical; include/dm.h)."""
-        with self._lock:
-            check(self._lib.dm_set_integrate_mode(self._handle(), self.INTEGRATE_MODES[mode]))
-
-    def last_integrate_direct(self) -> bool:
-        """True if the last integrate call took the direct front-end."""
-        v = ctypes.c_int32(0)
-        with self._lock:
-            check(self._lib.dm_last_integrate_direct(self._handle(), ctypes.byref(v)))
-        return bool(v.value)
-
     # -- sharding support -------------------------------------------------
     def set_halo(self, before=None, after=None):
         b = None if before is None else np.ascontiguousarray(before, np.int8)

@@ -214,20 +214,6 @@ int dm_max_passes_in_flight(void);
  * reads results returns DM_ERR_PIPELINE until dm_reset. */
 int dm_set_overlap(dm_grid* g, int32_t on);
 
-/* Integrate front-end (default 0 = auto).  Both find the same pieces of every
- * beam (so U, T, L and state are identical); they differ in speed:
- *   1 binned: every beam's pieces enumerated, binned by 64x64 tile
- *     (k_beam_prep, k_plan, k_scatter), then one workgroup per tile;
- *   2 direct: per scan, the tiles of its reach box and the beams whose
- *     angle reaches each tile (k_scan_plan), whose pieces the accumulation
- *     computes itself (k_direct_accum); no per-piece store.
- * Auto takes direct for scans of >= 1024 beams that fill the GPU (C3, C4),
- * binned otherwise.  With direct, the device inputs of dm_integrate_device
- * are read until the call's map update is done (keep them until a later
- * synchronising call). */
-int dm_set_integrate_mode(dm_grid* g, int32_t mode);
-/* 1 if the last integrate call took the direct front-end, else 0. */
-int dm_last_integrate_direct(const dm_grid* g, int32_t* direct);
 
 /* ---- One map sharded over several devices of this process (SURVEY.md §8(b)
  * "sharded variants: dm_create_sharded(..., int nranks, const int* devices)

@@ -22,7 +22,7 @@ def emu():
     lib = ctypes.CDLL(os.path.join(NATIVE, "libemu.so"))
     f = lib.emu_integrate
     i32, d, fl, vp = ctypes.c_int32, ctypes.c_double, ctypes.c_float, ctypes.c_void_p
-    f.argtypes = [i32, i32, i32, d, d, d] + [fl] * 8 + [vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, i32, d, d]
+    f.argtypes = [i32, i32, i32, d, d, d] + [fl] * 8 + [vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, i32]
     return lib
 
 
@@ -48,17 +48,16 @@ class EmuMap:
                                p.resolution, p.range_min, p.range_max, p.l_occ, p.l_free, p.l_min,
                                p.l_max, p.occ_thresh, p.free_thresh, ptr(self.L), ptr(self.state), S,
                                ptr(pose4), N, ptr(ranges), ptr(trig), ctypes.byref(U),
-                               ctypes.byref(T), ctypes.byref(G), self.chunk_len, amin32, inc32)
-        assert rc == 0, f"emulation check {rc} failed (-10x: piece walk vs closed form, -11x: direct pieces)"
+                               ctypes.byref(T), ctypes.byref(G), self.chunk_len)
+        assert rc == 0, f"emulation check {rc} failed (-10x: piece walk vs closed form)"
         return int(U.value), int(T.value)
 
 
-@pytest.mark.parametrize("direct", [False, True])
 @pytest.mark.parametrize("name", ["tiny64", "c1_room", "ragged", "offgrid"])
-def test_emulated_kernels_match_golden(emu, name, direct):
+def test_emulated_kernels_match_golden(emu, name):
     d = np.load(os.path.join(HERE, "golden", "oracle_golden.npz"))
     c = load_case(d, name)
-    m = EmuMap(emu, c["params"], -1 if direct else 0)
+    m = EmuMap(emu, c["params"], 0)
     for k, (poses, ranges) in enumerate(c["batches"]):
         assert m.integrate(poses, ranges, c["amin"], c["inc"]) == tuple(c["counts"][k])
     np.testing.assert_array_equal(m.L.view(np.uint32), c["L"].view(np.uint32))
@@ -69,12 +68,10 @@ def test_emulated_kernels_match_golden(emu, name, direct):
     (257, 513, 6, 700, 0.05, 4, 0, 0), (1000, 300, 4, 2048, 0.02, 5, 0, 0),
     (96, 96, 12, 256, 0.1, 6, 0, 0), (300, 700, 8, 600, 0.05, 7, 320, 192),
     (500, 500, 3, 3000, 0.01, 8, 128, 0)])
-@pytest.mark.parametrize("chunk_len", [0, 64, 97, -1])
+@pytest.mark.parametrize("chunk_len", [0, 64, 97])
 def test_emulated_kernels_random(emu, oracle_lib, W, H, S, N, res, seed, r0, rows, chunk_len):
     """chunk_len > 0: beams enumerated in k-ranges as k_beam_prep / k_scatter
-    do for small batches (dm_integrate_chunks); -1: the direct front-end
-    (pieces found per scan tile from candidate beams, dm_tile_krange), which
-    must find exactly the beam-major pieces."""
+    do for small batches (dm_integrate_chunks)."""
     p = cases.make_params(W, H, resolution=res, band_row0=r0, band_rows=rows)
     om = oracle_lib.OracleMap(p)
     m = EmuMap(emu, p, chunk_len)
@@ -82,26 +79,5 @@ def test_emulated_kernels_random(emu, oracle_lib, W, H, S, N, res, seed, r0, row
         poses, ranges, amin, inc = cases.random_scans(seed * 10 + k, p, S, N,
                                                       spread=4.0 if seed == 6 else 1.0)
         assert m.integrate(poses, ranges, amin, inc) == om.integrate(poses, ranges, amin, inc)
-    np.testing.assert_array_equal(m.L.view(np.uint32), om.L.view(np.uint32))
-    np.testing.assert_array_equal(m.state, om.state)
-
-
-@pytest.mark.parametrize("amin,span,N,seed", [
-    (-2.356194490192345, 4.71238898038469, 1081, 11),   # a 270-degree scanner, 0.25-degree steps
-    (1.0, 6.283185307179586, 720, 12),                  # a full turn that starts at 1 rad
-    (-3.0, 9.0, 900, 13),                               # more than a turn (beams overlap)
-    (0.3, 0.05, 40, 14)])                               # a narrow fan
-def test_emulated_direct_front_end_angle_ranges(emu, oracle_lib, amin, span, N, seed):
-    """The direct front-end's candidate beams (dm_box_beams) for scan layouts
-    other than the LD06's [0, 2 pi]: every beam-major piece is found exactly
-    once, and the map equals the oracle's."""
-    p = cases.make_params(384, 320, resolution=0.03)
-    om = oracle_lib.OracleMap(p)
-    m = EmuMap(emu, p, -1)
-    amin32 = float(np.float32(amin))
-    inc32 = float(np.float32(span / (N - 1)))
-    for k in range(3):
-        poses, ranges, _, _ = cases.random_scans(seed * 10 + k, p, 5, N, spread=0.5)
-        assert m.integrate(poses, ranges, amin32, inc32) == om.integrate(poses, ranges, amin32, inc32)
     np.testing.assert_array_equal(m.L.view(np.uint32), om.L.view(np.uint32))
     np.testing.assert_array_equal(m.state, om.state)

@@ -1,6 +1,5 @@
 """GPU: the frontier pass reading the per-tile free / unknown bit records
-(fmask, DM_FMASK=on: maintained by k_fmask_items / k_fmask_direct after every
-map update and by k_recount after bulk state writes, with the per-tile edge
+(fmask, DM_FMASK=on: maintained by k_fmask_items after every map update and by k_recount after bulk state writes, with the per-tile edge
 words fedge the pass reads for a tile's neighbours) instead of the state bytes, against the
 CPU oracle: integrate sequences on aligned, ragged and unaligned (W % 4 != 0:
 the cell-by-cell path) maps, the state families of the frontier parity tests,
@@ -23,18 +22,16 @@ def fmask_on(monkeypatch):
     monkeypatch.setenv("DM_FMASK", "on")
 
 
-@pytest.mark.parametrize("mode", ["binned", "direct"])
 @pytest.mark.parametrize("W,H,S,N,nb,seed", [(1024, 1024, 8, 1024, 4, 61), (1000, 700, 6, 720, 4, 62),
                                              (1001, 703, 5, 900, 4, 63), (700, 1300, 3, 200, 6, 64)])
-def test_integrate_then_frontiers(oracle_lib, fmask_on, mode, W, H, S, N, nb, seed):
-    """Both front-ends' fmask writers (k_fmask_items with sparse items that
-    rewrite only some rows, k_fmask_direct) and the edge words (fedge) the
-    pass reads for a tile's neighbours."""
+def test_integrate_then_frontiers(oracle_lib, fmask_on, W, H, S, N, nb, seed):
+    """The fmask writer (k_fmask_items, with sparse items that rewrite only
+    some rows) and the edge words (fedge) the pass reads for a tile's
+    neighbours."""
     p, batches, amin, inc = cases.world_case(seed, W, H, 0.05, S, N, nb, region_frac=0.7)
     om = oracle_lib.OracleMap(p)
     with dm.OccupancyMapper(p) as m:
         m.set_overlap(True)
-        m.set_integrate_mode(mode)
         for poses, ranges in batches:
             m.integrate(poses, ranges, amin, inc)
             om.integrate(poses, ranges, amin, inc)

@@ -24,12 +24,10 @@ def _tiles_with_free(st):
     return (pad.reshape(TY, 64, TX, 64) == 0).any(axis=(1, 3))
 
 
-@pytest.mark.parametrize("mode", ["binned", "direct"])
-def test_list_grows_with_every_tile_that_held_a_free_cell(oracle_lib, mode):
+def test_list_grows_with_every_tile_that_held_a_free_cell(oracle_lib):
     p, batches, amin, inc = cases.world_case(71, 1100, 900, 0.05, 12, 1500, 6, region_frac=0.8)
     om = oracle_lib.OracleMap(p)
     with dm.OccupancyMapper(p) as m:
-        m.set_integrate_mode(mode)
         ever = np.zeros_like(_tiles_with_free(om.state))
         for poses, ranges in batches:
             assert m.integrate(poses, ranges, amin, inc) == om.integrate(poses, ranges, amin, inc)

@@ -30,7 +30,7 @@ from dm import synth  # noqa: E402
 TICK_US = 0.01  # wall_clock64: 100 MHz
 
 
-def run(steps, overlap=True, mode="binned"):
+def run(steps, overlap=True):
     G, res, S, N = 16384, 0.05, 64, 4096
     half = G * res / 2
     world = synth.make_world(0, -half, -half, half, half)
@@ -41,12 +41,10 @@ def run(steps, overlap=True, mode="binned"):
     torch.cuda.synchronize()
     amin, inc = float(synth.LD06_ANGLE_MIN), float(synth.ld06_angle_increment(N))
     lib = dm._ffi.load_library()
-    # binned front-end -> k_tile_accum's record, direct -> k_direct_accum's
-    rd = lib.dm_debug_timeline_accum if mode == "binned" else lib.dm_debug_timeline_daccum
+    rd = lib.dm_debug_timeline_accum
     rd.argtypes = [ctypes.c_void_p, ctypes.c_int]
     m = dm.OccupancyMapper(dm.default_params(G, G, resolution=res))
     m.set_overlap(overlap)
-    m.set_integrate_mode(mode)
     pending = 0
     for k in range(steps):
         p4, r = dpool[k % len(dpool)]
@@ -114,10 +112,10 @@ def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 30
     js = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
     res = {}
-    for fe in ("binned", "direct"):
-        for pm in ("pipelined", "alone"):
-            mode = f"{fe} {pm}"
-            tl = run(steps, overlap=(pm == "pipelined"), mode=fe)
+    for pm in ("pipelined", "alone"):
+        if True:
+            mode = pm
+            tl = run(steps, overlap=(pm == "pipelined"))
             res[mode] = summarise(tl)
             r = res[mode]
             print(f"[{mode}] workgroups {r['workgroups']} (with items {r['with_items']}), span {r['span_us']:.1f} us, "

@@ -11,7 +11,7 @@
 #   pmc           PMC passes over a short C3 bench -> profiles/pmc_latest.json [C3]
 #   pmcx          PMC passes over the explored-map probe -> [C3-explored]
 #   cfg:CN        bench.py --config CN
-#   abfe          C3 A/B of the integrate front-ends and fmask (tools/ab.sh -> ab.log)
+#   abfm          C3 A/B of fmask maintenance (tools/ab.sh -> ab.log)
 #   timeline      per-workgroup accumulation timeline (tools/accum_timeline.py)
 #   phase / phase5:N   phase build probe at C3 / C5 with N beams per scan
 #   c5:SWEEP      bench.py --config C5 --sweep SWEEP
@@ -60,12 +60,10 @@ for s in "$@"; do
         python $R/tools/pmc_summary.py $OUT/pmc5_$n $R/profiles/pmc_latest.json C5-$n >> $OUT/pmc5_summary.log 2>&1 || exit 1
       done
       cp $R/profiles/pmc_latest.json $OUT/pmc_latest.json ;;
-    abfe)
-      # C3 A/B: binned vs direct front-end, fmask maintained or not (2 alternating rounds)
-      BENCH_ARGS_binned="--integrate-mode binned" BENCH_ARGS_direct="--integrate-mode direct" \
-      BENCH_ARGS_binfm="--integrate-mode binned" BENCH_ARGS_dirfm="--integrate-mode direct" \
-        timeout -k 10 900 bash $R/tools/ab.sh 2 "binned:" "direct:" "binfm:DM_FMASK=on" "dirfm:DM_FMASK=on"
-      rc=$?; echo "abfe rc=$rc"; ok $rc || exit $rc ;;
+    abfm)
+      # C3 A/B: fmask maintained or not (2 alternating rounds)
+      timeout -k 10 600 bash $R/tools/ab.sh 2 "base:" "fmask:DM_FMASK=on"
+      rc=$?; echo "abfm rc=$rc"; ok $rc || exit $rc ;;
     timeline)
       timeout -k 10 300 python -u $R/tools/accum_timeline.py 30 --json $OUT/accum_timeline.json \
         > $OUT/accum_timeline.log 2>&1

@@ -40,10 +40,9 @@ def gaps(a, b):
     return out
 
 
-for a, b in (("k_rank_sort", "k_tile_accum"), ("k_rank_sort", "k_direct_accum"),
-             ("k_frontier_bits", "k_frontier_tile_big"), ("k_frontier_tile_big", "k_frontier_resolve"),
-             ("k_frontier_resolve", "k_rank_sort"), ("k_tile_accum", "k_frontier_bits"),
-             ("k_direct_accum", "k_frontier_bits"), ("k_scatter", "k_tile_accum"), ("k_scan_plan", "k_direct_accum")):
+for a, b in (("k_rank_sort", "k_tile_accum"), ("k_frontier_bits", "k_frontier_tile_big"),
+             ("k_frontier_tile_big", "k_frontier_resolve"), ("k_frontier_resolve", "k_rank_sort"),
+             ("k_tile_accum", "k_frontier_bits"), ("k_scatter", "k_tile_accum")):
     g = gaps(a, b)[5:30]
     if g:
         print(f"gap {a} -> {b}: median {statistics.median(g):.1f} us, min {min(g):.1f}")

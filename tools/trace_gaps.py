@@ -13,8 +13,7 @@ for r in csv.DictReader(open(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/p
     m = re.search(r"(k_\w+|__amd\w+)", r["Kernel_Name"])
     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), m.group(1) if m else r["Kernel_Name"][:20]))
 rows.sort()
-calls = {"integrate": ("k_integrate_reset", "k_tile_accum"), "integrate_direct": ("k_integrate_reset", "k_direct_accum"),
-         "frontier": ("k_frontier_bits", "k_rank_sort")}
+calls = {"integrate": ("k_integrate_reset", "k_tile_accum"), "frontier": ("k_frontier_bits", "k_rank_sort")}
 for name, (first, last) in calls.items():
     spans, busy, gaps, prev_end = [], [], [], {}
     cur = None
