@@ -558,6 +558,11 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if ((rc = dev_alloc(&g->m_cnt, 4, "merge counters"))) return fail(rc);
   e = hipHostMalloc((void**)&g->h_mcnt, sizeof(unsigned long long) * 4, hipHostMallocDefault);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipHostMalloc(merge counters)"));
+  e = hipHostMalloc((void**)&g->h_hint, sizeof(unsigned long long) * 16, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return fail(dm_hip_check(e, "hipHostMalloc(work hint)"));
+  memset(g->h_hint, 0, sizeof(unsigned long long) * 16);
+  e = hipHostGetDevicePointer((void**)&g->d_hint, g->h_hint, 0);
+  if (e != hipSuccess) return fail(dm_hip_check(e, "hipHostGetDevicePointer(work hint)"));
   e = hipDeviceGetAttribute(&g->n_cu, hipDeviceAttributeMultiprocessorCount, device);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipDeviceGetAttribute(multiprocessor count)"));
   // Stream priorities: the map chain (accumulation, frontier prep and bit
@@ -641,6 +646,7 @@ int dm_destroy(dm_grid* g) {
   dev_free(g->slot_k); dev_free(g->rank_of); dev_free(g->m_parent); dev_free(g->m_label);
   dev_free(g->m_acc); dev_free(g->m_clu); dev_free(g->m_cnt);
   if (g->h_mcnt) (void)hipHostFree(g->h_mcnt);
+  if (g->h_hint) (void)hipHostFree(g->h_hint);
   if (g->h_cnt) (void)hipHostFree(g->h_cnt);
   if (g->h_sh) (void)hipHostFree(g->h_sh);
   for (int i = 0; i < dm_grid::kPoseRing; ++i) {

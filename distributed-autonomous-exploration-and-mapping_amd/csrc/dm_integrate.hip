@@ -836,7 +836,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
     const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok,
     const int32_t* __restrict__ heavy_list, int32_t* heavy_done, int32_t* tlist, unsigned long long* tlist_n,
-    const unsigned long long* __restrict__ halt) {
+    unsigned long long* hint, const unsigned long long* __restrict__ halt) {
   __shared__ uint32_t tl[kTileWords + 64];  // + one spare word per lane (walk_piece_plain)
   __shared__ int32_t s_T, s_free, s_last;
   __shared__ uint32_t s_U;
@@ -863,6 +863,11 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
   // ones: a small call (one 360-beam scan) is one round of items, and its
   // sparse tiles used to queue behind its heavy and medium tiles.
   const int64_t sp_rank = ((int64_t)blockIdx.x - n_items % G + G) % G;
+  if (blockIdx.x == 0 && tid == 0) {  // the work of this call, for the next call's grid (mapped host memory)
+    volatile unsigned long long* h = hint;
+    h[0] = (unsigned long long)(n_items + (SI + 3) / 4);
+    h[1] = (unsigned long long)(n_items + SI);
+  }
   const unsigned long long idle =
       ((int64_t)blockIdx.x >= n_items && sp_rank * (kQuarter / 64) >= SI) ? 1ull : 0ull;
   // a timed-out front-end hand-off (kHaltWord): this call's workspace was
@@ -1530,11 +1535,24 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   // heavy chunks and medium tiles first (the long items), then the light
   // tiles; the last item of each heavy tile applies its merged slab
   dm_timer_begin(g, "tile_accum", &t);
-  DM_LAUNCH(k_tile_accum, dim3(grid_for(g->hitem_cap + g->act_cap, 1, dm_grid::kAccumGrid)),
+  // one workgroup per item (the kernel grid-strides, so any grid is exact):
+  // a grid sized to the capacity (16384 at C3) ran ~3.6 k item workgroups
+  // and ~12.8 k that exit at once, whose dispatch held the kernel's end and
+  // the front-end streams' first workgroups ~6 us longer in the pipelined
+  // step (profiles/r04_accum_timeline.log); the last finished call's count
+  // (+25 % + 256) sizes it instead
+  const volatile unsigned long long* hint = g->h_hint;
+  const int64_t cap = g->hitem_cap + g->act_cap;
+#ifndef DM_ACCUM_HINT
+#define DM_ACCUM_HINT 1  // 0: capacity grids (the round-3 launch, for A/B builds)
+#endif
+  const int64_t hw = DM_ACCUM_HINT ? (int64_t)hint[0] : 0, hi = DM_ACCUM_HINT ? (int64_t)hint[1] : 0;
+  const int64_t accum_wgs = hw > 0 ? std::min(cap, dm_quantize_up(hw + hw / 4 + 256)) : cap;
+  DM_LAUNCH(k_tile_accum, dim3(grid_for(accum_wgs, 1, dm_grid::kAccumGrid)),
                      dim3(kQuarter), 0,
                      g->stream, ge, make_apply(g), w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS,
                      (int)CNT_SITEMS, w.pieces, w.tile_count, g->tile_free, w.slabs, g->L, g->state, w.cnt, w.sh, vec_ok,
-                     w.heavy_list, w.heavy_done, g->ftiles, g->ftiles_n, g->fe_flag + kHaltWord);
+                     w.heavy_list, w.heavy_done, g->ftiles, g->ftiles_n, g->d_hint, g->fe_flag + kHaltWord);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (g->overlap) w.free_owed = true;
@@ -1545,7 +1563,8 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
     return DM_OK;
   }
   dm_timer_begin(g, "fmask", &t);
-  DM_LAUNCH(k_fmask_items, dim3(grid_for(g->hitem_cap + g->act_cap, 4, 8192)), dim3(256), 0, g->stream,
+  const int64_t fmask_items = hi > 0 ? std::min(cap, dm_quantize_up(hi + hi / 4 + 256)) : cap;
+  DM_LAUNCH(k_fmask_items, dim3(grid_for(fmask_items, 4, 8192)), dim3(256), 0, g->stream,
                      ge, w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS, (int)CNT_SITEMS, w.pieces, w.cnt,
                      g->state, g->fmask, g->fedge,
                      g->fe_flag + kHaltWord);

@@ -412,6 +412,13 @@ struct dm_grid {
   dm_cluster* m_out = nullptr;    // [m_cap] merged records, sorted
   unsigned long long* m_cnt = nullptr;    // [4] device: K, flags, sorted, max band K
   unsigned long long* h_mcnt = nullptr;   // pinned mirror
+  // [0] workgroups the last accumulation needed (dense items + sparse items
+  // / 4), [1] its work items: written by k_tile_accum's workgroup 0 into
+  // mapped host memory, read without a wait when the next call is enqueued
+  // (a finished earlier call's value; 0 until one finished) to size the
+  // accumulation and fmask grids to the work instead of to the capacity
+  unsigned long long* h_hint = nullptr;
+  unsigned long long* d_hint = nullptr;   // its device address
 
   // goal selection (dm_goals.hip): the last collected sorted result on the
   // device (a readback slot's out_clu / m_out while that slot's epoch is
