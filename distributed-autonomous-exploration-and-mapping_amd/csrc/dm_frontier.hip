@@ -205,11 +205,12 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
       DM_PH(dm_phase_acc_frontier, 8);
       continue;
     }
-    if (tid < DM_TS) {  // enumerate runs of row tid
-      const int y = tid;
-      const uint64_t F = s_F[y];
-      uint64_t st = run_starts(F);
-      int r = s_rbase[y];
+    {  // enumerate the runs: four threads per row, each the runs starting in its 16 columns
+      const int y = tid >> 2, q = tid & 3;
+      const uint64_t st_all = run_starts(s_F[y]);
+      const uint64_t below = q ? upto_mask(16 * q - 1) : 0ull;
+      uint64_t st = st_all & upto_mask(16 * q + 15) & ~below;
+      int r = s_rbase[y] + __popcll(st_all & below);
       while (st) {
         const int s0 = __ffsll((unsigned long long)st) - 1;
         r_s[r] = (uint8_t)s0;
