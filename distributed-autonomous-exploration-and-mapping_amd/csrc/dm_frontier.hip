@@ -147,7 +147,6 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
   __shared__ int32_t r_par[kMaxRuns];
   __shared__ uint8_t r_s[kMaxRuns], r_y[kMaxRuns];  // run end: run_end(s_F[y], s)
   __shared__ uint64_t s_root[kMaxRuns / 64];        // root-run bits
-  __shared__ uint64_t s_merge[kMaxRuns / 64];       // runs overlapping two or more runs above
   __shared__ int32_t s_rootpre[kMaxRuns / 64];
   // per-component size << 18 | sum of x (size <= 4096 < 2^13, sum of x <=
   // 4096 * 63 < 2^18: one 32-bit LDS add per run for both) and sum of y
@@ -221,7 +220,6 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
       }
     }
     for (int r = tid; r < kMaxRoots; r += kFT) { szx[r] = 0; ssy[r] = 0; }
-    if (tid < kMaxRuns / 64) s_merge[tid] = 0ull;
     __syncthreads();
     const int nruns = s_rbase[DM_TS];
     if (count_stats && tid == 0) {
@@ -231,62 +229,19 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
     DM_PH(dm_phase_acc_frontier, 2);
     DM_PH_COUNT(dm_phase_acc_frontier, 17, nruns);
     DM_PH_COUNT(dm_phase_acc_frontier, 18, 1);
-    // ---- 3. connect each run with the runs of the row above that overlap it
-    // (extended by a cell each side).  Most runs overlap exactly one (a ray
-    // across the tile is a chain of runs, one per row): the run points at it
-    // directly.  That is a forest whose every pointer goes one row up, to a
-    // smaller run index, so its roots are the runs with nothing above (each
-    // component's first run among them).  Pointer jumping (at most 6 rounds:
-    // a chain spans at most 64 rows) flattens it; only the runs that overlap
-    // two or more runs above (components joining) take the union-find, on
-    // the flattened trees.  C5's thin rays (756 runs per tile at 768 beams)
-    // spent a third of this kernel in per-run unions along the chains.
+    // ---- 3. union with overlapping runs of the row above ---------------------
     for (int r = tid; r < nruns; r += kFT) {
       const int y = r_y[r];
-      int32_t par = r;
-      if (y > 0) {
-        const int s0 = r_s[r], e0 = run_end(s_F[y], s0);
-        const int lo = s0 > 0 ? s0 - 1 : 0;
-        const int hi = e0 < 63 ? e0 + 1 : 63;
-        const uint64_t M = upto_mask(hi) & ~(lo > 0 ? upto_mask(lo - 1) : 0ull);
-        uint64_t P = s_F[y - 1] & M;
-        if (P) {
-          const int p = __ffsll((unsigned long long)P) - 1;
-          par = run_of(s_rbase, s_F, y - 1, p);
-          const uint64_t rest = ~(s_F[y - 1] >> p);
-          const int len = rest ? __ffsll((unsigned long long)rest) - 1 : 64 - p;
-          P &= ~(upto_mask(p + len - 1));
-          if (P) atomicOr((unsigned long long*)&s_merge[r >> 6], 1ull << (r & 63));
-        }
-      }
-      r_par[r] = par;
-    }
-    __syncthreads();
-    for (int round = 0; round < 6; ++round) {  // pointer jumping
-      int moved = 0;
-      for (int r = tid; r < nruns; r += kFT) {
-        const int32_t p = ((volatile int32_t*)r_par)[r];
-        const int32_t gp = ((volatile int32_t*)r_par)[p];
-        if (gp != p) {
-          ((volatile int32_t*)r_par)[r] = gp;
-          moved = 1;
-        }
-      }
-      if (!__syncthreads_or(moved)) break;
-    }
-    for (int r = tid; r < nruns; r += kFT) {  // the joins: the further runs above
-      if (!((s_merge[r >> 6] >> (r & 63)) & 1ull)) continue;
-      const int y = r_y[r];
+      if (y == 0) continue;
       const int s0 = r_s[r], e0 = run_end(s_F[y], s0);
       const int lo = s0 > 0 ? s0 - 1 : 0;
       const int hi = e0 < 63 ? e0 + 1 : 63;
       const uint64_t M = upto_mask(hi) & ~(lo > 0 ? upto_mask(lo - 1) : 0ull);
       uint64_t P = s_F[y - 1] & M;
-      bool first = true;
       while (P) {
         const int p = __ffsll((unsigned long long)P) - 1;
-        if (!first) lds_unite(r_par, r, run_of(s_rbase, s_F, y - 1, p));
-        first = false;
+        lds_unite(r_par, r, run_of(s_rbase, s_F, y - 1, p));
+        // skip the rest of that run inside M
         const uint64_t rest = ~(s_F[y - 1] >> p);
         const int len = rest ? __ffsll((unsigned long long)rest) - 1 : 64 - p;
         P &= ~(upto_mask(p + len - 1));
@@ -836,15 +791,10 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
     DM_PH(dm_phase_acc_ftile, 1);
     DM_PH_COUNT(dm_phase_acc_ftile, 17, 1);
     DM_PH_COUNT(dm_phase_acc_ftile, 18, nruns);
-    // ---- 4. connect every run with the runs above it (extended by a cell):
-    // each run points at its first overlapping run above (a forest whose
-    // pointers go one row up), pointer jumping flattens it, and only runs
-    // that overlap two or more runs above take the union-find (as in
-    // k_frontier_tile_big)
+    // ---- 4. union every run with the runs above it (extended by a cell) ------
     const uint64_t Fa = __shfl_up(F, 1);
     const uint64_t sta = __shfl_up(st, 1);
     const int rba = __shfl_up(rbase, 1);
-    bool joins = false;  // a run of this lane's row overlaps two or more runs above
     if (lane > 0 && Fa) {
       uint64_t s_ = st;
       int r = rbase;
@@ -853,44 +803,9 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
         const int e0 = run_end(F, s0);
         const int lo = s0 > 0 ? s0 - 1 : 0, hi = e0 < 63 ? e0 + 1 : 63;
         uint64_t P = Fa & upto_mask(hi) & ~(lo > 0 ? upto_mask(lo - 1) : 0ull);
-        if (P) {
-          const int q = __ffsll((unsigned long long)P) - 1;
-          par[r] = rba + __popcll(sta & upto_mask(q)) - 1;
-          const uint64_t rest = ~(Fa >> q);
-          const int len = rest ? __ffsll((unsigned long long)rest) - 1 : 64 - q;
-          joins |= (P & ~upto_mask(q + len - 1)) != 0ull;
-        }
-        ++r;
-        s_ &= s_ - 1;
-      }
-    }
-    wave_lds_sync();
-    for (int round = 0; round < 6; ++round) {  // pointer jumping (a chain spans <= 64 rows)
-      bool moved = false;
-      for (int r = lane; r < nruns; r += 64) {
-        const int32_t p = ((volatile int32_t*)par)[r];
-        const int32_t gp = ((volatile int32_t*)par)[p];
-        if (gp != p) {
-          ((volatile int32_t*)par)[r] = gp;
-          moved = true;
-        }
-      }
-      wave_lds_sync();
-      if (__ballot(moved) == 0ull) break;
-    }
-    if (joins) {  // the further runs above of the runs that join components
-      uint64_t s_ = st;
-      int r = rbase;
-      while (s_) {
-        const int s0 = __ffsll((unsigned long long)s_) - 1;
-        const int e0 = run_end(F, s0);
-        const int lo = s0 > 0 ? s0 - 1 : 0, hi = e0 < 63 ? e0 + 1 : 63;
-        uint64_t P = Fa & upto_mask(hi) & ~(lo > 0 ? upto_mask(lo - 1) : 0ull);
-        bool first = true;
         while (P) {
           const int q = __ffsll((unsigned long long)P) - 1;
-          if (!first) lds_unite(par, r, rba + __popcll(sta & upto_mask(q)) - 1);
-          first = false;
+          lds_unite(par, r, rba + __popcll(sta & upto_mask(q)) - 1);
           const uint64_t rest = ~(Fa >> q);
           const int len = rest ? __ffsll((unsigned long long)rest) - 1 : 64 - q;
           P &= ~upto_mask(q + len - 1);
