@@ -1633,6 +1633,13 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   }
   dm_select_fw(g, g->fparity);
   unsigned long long* list_n = g->fl_n + 16 * (g->fr_pass % 3);  // this pass's list length (k_frontier_bits)
+  // every kRelistPasses passes the tile list goes back into tile order
+  // (dm_launch_relist); the passes still labelling read it, so the map stream
+  // first waits for them (split passes have not joined the pass stream)
+  if (++g->relist_age >= kRelistPasses) {
+    DM_HIP(dm_join_pass_stream(g));
+    if (int rc = dm_launch_relist(g)) return rc;
+  }
   KernelTimer t;
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));

@@ -1260,12 +1260,15 @@ __global__ __launch_bounds__(256) void k_recount(Geom g, const int8_t* __restric
                                     s_edge[3][threadIdx.x];
 }
 
-// After k_recount (bulk state writes: counts only, flags clear): the
-// persistent frontier tile list from scratch, every tile with a free cell in
-// tile order, each flagged kTileListed by the thread that places it.  Ballot
-// compaction over chunks of `iters` x 256 tiles per workgroup and round, one
-// list atomic per chunk (the loop bounds are uniform within the workgroup:
-// its barriers are safe).
+// The persistent frontier tile list from scratch, every tile with a free
+// cell in tile order, each tile's kTileListed flag set or cleared to match:
+// after bulk state writes (k_recount), and every kRelistPasses passes, which
+// puts the tiles appended since in tile order again (the bit-row and tile
+// kernels read neighbouring listed tiles together: appended tiles arrive in
+// exploration order, and at C3 a list in that order doubled k_frontier_bits'
+// fetched bytes).  Ballot compaction over chunks of `iters` x 256 tiles per
+// workgroup and round, one list atomic per chunk (the loop bounds are
+// uniform within the workgroup: its barriers are safe).
 constexpr int kListIters = 16;
 __global__ __launch_bounds__(256) void k_list_tiles(int64_t NT, int32_t* __restrict__ tile_free,
                                                     int32_t* __restrict__ ftiles, unsigned long long* list_n,
@@ -1279,7 +1282,11 @@ __global__ __launch_bounds__(256) void k_list_tiles(int64_t NT, int32_t* __restr
     uint32_t mine = 0u;
     for (int i = 0; i < iters; ++i) {
       const int64_t t = c0 + (int64_t)i * blockDim.x + threadIdx.x;
-      mine |= (t < NT && (tile_free[t] & kTileFreeMask) > 0 ? 1u : 0u) << i;
+      if (t >= NT) continue;
+      const int32_t v = tile_free[t];
+      const bool f = (v & kTileFreeMask) > 0;
+      mine |= (f ? 1u : 0u) << i;
+      if (f != ((v & kTileListed) != 0)) tile_free[t] = f ? (v | kTileListed) : (v & kTileFreeMask);
     }
     for (int i = 0; i < iters; ++i) {
       const unsigned long long bal = __ballot((mine >> i) & 1u);
@@ -1301,7 +1308,6 @@ __global__ __launch_bounds__(256) void k_list_tiles(int64_t NT, int32_t* __restr
       if (f) {
         const int64_t t = c0 + (int64_t)i * blockDim.x + threadIdx.x;
         ftiles[pre + before + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)t;
-        tile_free[t] |= kTileListed;
       }
       pre += s_wn[i][0] + s_wn[i][1] + s_wn[i][2] + s_wn[i][3];
     }
@@ -1586,6 +1592,19 @@ int dm_launch_gate(hipStream_t s, unsigned long long* flag, unsigned long long* 
   return DM_OK;
 }
 
+// The persistent frontier tile list rebuilt in tile order from tile_free
+// (~256 chunks).  No frontier pass may be reading the list: the caller has
+// joined the pass stream.
+int dm_launch_relist(dm_grid* g) {
+  DM_HIP(hipMemsetAsync(g->ftiles_n, 0, sizeof(unsigned long long), g->stream));
+  const int iters = (int)std::min<int64_t>(kListIters, std::max<int64_t>(1, (g->NT + 65535) / 65536));
+  DM_LAUNCH(k_list_tiles, dim3(grid_for((g->NT + iters - 1) / iters, 256, 1024)), dim3(256), 0, g->stream,
+            g->NT, g->tile_free, g->ftiles, g->ftiles_n, iters);
+  DM_HIP(hipGetLastError());
+  g->relist_age = 0;
+  return DM_OK;
+}
+
 int dm_launch_recount(dm_grid* g) {
   const Geom ge = make_geom(g);
   // the tile list is rebuilt from position 0: passes still labelling on the
@@ -1595,12 +1614,7 @@ int dm_launch_recount(dm_grid* g) {
   DM_LAUNCH(k_recount, dim3((unsigned)g->NT), dim3(256), 0, g->stream, ge, g->state,
                      g->tile_free, g->fmask, g->fedge);
   DM_HIP(hipGetLastError());
-  // the persistent frontier tile list from the new counts (~256 chunks)
-  DM_HIP(hipMemsetAsync(g->ftiles_n, 0, sizeof(unsigned long long), g->stream));
-  const int iters = (int)std::min<int64_t>(kListIters, std::max<int64_t>(1, (g->NT + 65535) / 65536));
-  DM_LAUNCH(k_list_tiles, dim3(grid_for((g->NT + iters - 1) / iters, 256, 1024)), dim3(256), 0, g->stream,
-            g->NT, g->tile_free, g->ftiles, g->ftiles_n, iters);
-  DM_HIP(hipGetLastError());
+  if (int rc = dm_launch_relist(g)) return rc;
   g->fmask_valid = true;
   return DM_OK;
 }

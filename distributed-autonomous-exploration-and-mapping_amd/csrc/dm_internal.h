@@ -339,6 +339,7 @@ struct dm_grid {
   // on the map stream after its batch) while later batches append behind them.
   int32_t* ftiles = nullptr;               // [NT]
   unsigned long long* ftiles_n = nullptr;  // [16]: [0] the list length
+  int relist_age = 0;  // passes since the list was last put in tile order (dm_launch_relist)
   int32_t* big_tiles = nullptr;  // [NT] per list position: 1 = too many runs for a tile-wave (k_frontier_bits)
   uint64_t* fbits = nullptr;   // [NT][64] frontier bit rows of the listed tiles (k_frontier_bits)
   int32_t* border = nullptr;   // [tile][4][64] slot ids of a tile's edges (published sides only)
@@ -503,6 +504,9 @@ inline int32_t dm_integrate_chunks(const dm_grid* g, int64_t nb) {
 int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                         const float* d_ranges, const double* d_trig);
 int dm_launch_recount(dm_grid* g);
+int dm_launch_relist(dm_grid* g);
+// Passes between rebuilds of the tile list in tile order (dm_launch_relist).
+constexpr int kRelistPasses = 16;
 int dm_launch_state_from_logodds(dm_grid* g);
 int dm_launch_map_image(dm_grid* g, uint8_t* d_img);
 int dm_launch_set_state(dm_grid* g, const int8_t* d_state_in);

@@ -1,11 +1,13 @@
 """GPU: the persistent frontier tile list (dm_internal.h `ftiles`): every
-tile that has held a free cell since the last bulk state write, appended by
-the integrate apply when a tile's free count first rises above 0 (listed flag
-in `tile_free`), rebuilt by k_list_tiles after bulk writes (dm_set_state,
-dm_set_logodds, dm_reset, dm_load).  A pass's `frontier_tiles` statistic is
-its snapshot of the list length, so it must equal the number of tiles that
-ever held a free cell since the last bulk write; and tiles that lost every
-free cell stay listed without changing any result."""
+tile that has held a free cell since the last rebuild, appended by the
+integrate apply when a tile's free count first rises above 0 (listed flag in
+`tile_free`), rebuilt in tile order by k_list_tiles after bulk writes
+(dm_set_state, dm_set_logodds, dm_reset, dm_load) and every 16 passes.  A
+pass's `frontier_tiles` statistic is its snapshot of the list length, so
+within 16 passes of a bulk write it equals the number of tiles that ever held
+a free cell since; tiles that lost every free cell stay listed until the next
+rebuild without changing any result, and a rebuild drops them (flag cleared,
+so a tile that regains a free cell is appended again)."""
 import numpy as np
 import pytest
 
@@ -91,6 +93,28 @@ def test_listed_tiles_that_lose_their_free_cells(oracle_lib):
             poses = np.array([[0.3, -0.2, 0.1 * k], [3.1, 2.2, -0.4 * k]])
             far = 9.0 if k < 3 else 1.2  # later batches: short ranges, hits inside the freed region
             ranges = (np.round(rng.uniform(0.5, far, (2, N)) * 1000) / 1000).astype(np.float32)
+            m.integrate(poses, ranges, amin, inc)
+            om.integrate(poses, ranges, amin, inc)
+            if k >= 2:
+                got.append(m.frontiers_end())
+            m.frontiers_begin()
+            exp.append(om.frontiers(want_mask=False, want_labels=False)[2])
+        got += [m.frontiers_end(), m.frontiers_end()]
+        for fr, e in zip(got, exp):
+            np.testing.assert_array_equal(fr.clusters, e)
+        assert_map_equal(m, om)
+
+
+def test_periodic_rebuilds_keep_results(oracle_lib):
+    """40 pipelined passes (two periodic rebuilds, with passes in flight),
+    rays that free cells early and occupy some of them later: every pass
+    equals the oracle's frontiers of its own batch."""
+    p, batches, amin, inc = cases.world_case(73, 900, 800, 0.05, 6, 720, 40, region_frac=0.8)
+    om = oracle_lib.OracleMap(p)
+    with dm.OccupancyMapper(p) as m:
+        m.set_overlap(True)
+        got, exp = [], []
+        for k, (poses, ranges) in enumerate(batches):
             m.integrate(poses, ranges, amin, inc)
             om.integrate(poses, ranges, amin, inc)
             if k >= 2:
