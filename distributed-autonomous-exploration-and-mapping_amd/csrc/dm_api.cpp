@@ -527,9 +527,13 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     if ((rc = dev_alloc(&f.edge_slot, 2 * g->W, "edge slots"))) return fail(rc);
   }
   if ((rc = dev_alloc(&g->fl_n, 48, "frontier list lengths"))) return fail(rc);
-  if ((rc = dev_alloc(&g->ftiles, g->NT, "frontier tile list"))) return fail(rc);
-  if ((rc = dev_alloc(&g->ftiles_n, 16, "frontier tile list length"))) return fail(rc);
-  DM_HIP(hipMemset(g->ftiles_n, 0, sizeof(unsigned long long) * 16));
+  for (int i = 0; i < 2; ++i) {
+    if ((rc = dev_alloc(&g->flist[i], g->NT, "frontier tile list"))) return fail(rc);
+    if ((rc = dev_alloc(&g->flist_n[i], 16, "frontier tile list length"))) return fail(rc);
+    DM_HIP(hipMemset(g->flist_n[i], 0, sizeof(unsigned long long) * 16));
+  }
+  g->ftiles = g->flist[0];
+  g->ftiles_n = g->flist_n[0];
   DM_HIP(hipMemset(g->fl_n, 0, sizeof(unsigned long long) * 48));
   if ((rc = dev_alloc(&g->bits_flag, 16, "bit-row hand-off word"))) return fail(rc);
   DM_HIP(hipMemset(g->bits_flag, 0, sizeof(unsigned long long) * 16));
@@ -565,8 +569,8 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipHostGetDevicePointer(work hint)"));
   e = hipDeviceGetAttribute(&g->n_cu, hipDeviceAttributeMultiprocessorCount, device);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipDeviceGetAttribute(multiprocessor count)"));
-  // Stream priorities: the map chain (accumulation, frontier prep and bit
-  // rows) and the pass's labelling streams high, the integrate front-end low,
+  // Stream priorities: the map chain (accumulation, frontier bit rows) and
+  // the pass's labelling streams high, the integrate front-end low,
   // so a front-end enqueued early fills what the map chain leaves idle instead
   // of competing with the accumulation for its CUs (round-2/3 A/B of every
   // combination and of CU-masked streams: DESIGN.md §3.3).
@@ -586,7 +590,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   // waits on a readback slot's event and then reads mapped host memory:
   // default fences.
   for (hipEvent_t* ev : {&g->ev_fe, &g->ev_bits[0], &g->ev_bits[1], &g->iw[0].ev_free, &g->iw[1].ev_free,
-                         &g->ev_bigfork, &g->ev_big}) {
+                         &g->ev_bigfork, &g->ev_big, &g->flist_ev[0], &g->flist_ev[1]}) {
     e = hipEventCreateWithFlags(ev, hipEventDisableTiming | hipEventDisableSystemFence);
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
   }
@@ -610,7 +614,7 @@ int dm_destroy(dm_grid* g) {
   (void)dm_sync_all(g);
   for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
   for (hipEvent_t ev : {g->ev_fe, g->ev_bits[0], g->ev_bits[1], g->iw[0].ev_free, g->iw[1].ev_free,
-                        g->ev_bigfork, g->ev_big})
+                        g->ev_bigfork, g->ev_big, g->flist_ev[0], g->flist_ev[1]})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& r : g->rb) {
     if (r.ev) (void)hipEventDestroy(r.ev);
@@ -626,7 +630,8 @@ int dm_destroy(dm_grid* g) {
     dev_free(f.cnt); dev_free(f.fsh); dev_free(f.big_tiles); dev_free(f.fbits);
     dev_free(f.edge_slot); dev_free(f.slot_parent);
   }
-  dev_free(g->fl_n); dev_free(g->bits_flag); dev_free(g->ftiles); dev_free(g->ftiles_n);
+  dev_free(g->fl_n); dev_free(g->bits_flag);
+  for (int i = 0; i < 2; ++i) { dev_free(g->flist[i]); dev_free(g->flist_n[i]); }
   for (int b = 0; b < 2; ++b) { dev_free(g->goal_k[b]); dev_free(g->goal_i[b]); }
   dev_free(g->goal_io); dev_free(g->goal_idx);
   for (auto& w : g->iw) {

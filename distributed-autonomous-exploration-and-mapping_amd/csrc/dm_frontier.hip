@@ -49,7 +49,7 @@ constexpr int kMaxRoots = 1024;       // 8-connected components in a 64x64 tile
 struct FGeom {
   int32_t W, R, row0, TX, TY;
   int32_t has_before, has_after;
-  int32_t pad_ = 0;  // no implicit padding: equal geometries are equal bytes (dm_batch.h cache keys)
+  int32_t pad_ = 0;  // no implicit padding
   int64_t NT;
   int32_t want_mask, want_labels;
   int64_t H;
@@ -1619,7 +1619,7 @@ int dm_launch_bucket_sort(dm_grid* g, hipStream_t stream, long long* clusters, c
 int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool split, hipStream_t* end_stream) {
   const FGeom fg = make_fgeom(g, want_mask, want_labels);
   const int64_t cells = g->R * g->W;
-  // the prep and the bit rows run on g->stream after everything shared with
+  // the bit rows run on g->stream after everything shared with
   // the pass stream (labelling of earlier passes) -- except for split passes,
   // which keep that order on the pass stream itself
   if (!split) DM_HIP(dm_join_pass_stream(g));
@@ -1633,13 +1633,10 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   }
   dm_select_fw(g, g->fparity);
   unsigned long long* list_n = g->fl_n + 16 * (g->fr_pass % 3);  // this pass's list length (k_frontier_bits)
-  // every kRelistPasses passes the tile list goes back into tile order
-  // (dm_launch_relist); the passes still labelling read it, so the map stream
-  // first waits for them (split passes have not joined the pass stream)
-  if (++g->relist_age >= kRelistPasses) {
-    DM_HIP(dm_join_pass_stream(g));
-    if (int rc = dm_launch_relist(g)) return rc;
-  }
+  // every kRelistPasses passes the tile list goes back into tile order, into
+  // the other list (dm_launch_relist: the passes still labelling keep theirs)
+  if (++g->relist_age >= kRelistPasses)
+    if (int rc = dm_launch_relist(g, true)) return rc;
   KernelTimer t;
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));
   if (want_labels) DM_HIP(hipMemsetAsync(g->cell_slot, 0xFF, sizeof(int32_t) * (size_t)cells, g->stream));

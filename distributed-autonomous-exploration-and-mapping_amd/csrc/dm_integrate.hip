@@ -1593,9 +1593,23 @@ int dm_launch_gate(hipStream_t s, unsigned long long* flag, unsigned long long* 
 }
 
 // The persistent frontier tile list rebuilt in tile order from tile_free
-// (~256 chunks).  No frontier pass may be reading the list: the caller has
-// joined the pass stream.
-int dm_launch_relist(dm_grid* g) {
+// (~256 chunks).  swap: into the other list, after the passes that read it
+// (the pass stream's position when it was left: 16 passes ago, done unless
+// passes are enqueued faster than they run), then switch; the passes in
+// flight keep the current list, which nothing appends to any more.
+int dm_launch_relist(dm_grid* g, bool swap) {
+  if (swap) {
+    const int x = 1 - g->flist_cur;
+    if (g->flist_ev_set[x] && hipEventQuery(g->flist_ev[x]) != hipSuccess)
+      DM_HIP(hipStreamWaitEvent(g->stream, g->flist_ev[x], 0));
+    if (g->pass_stream) {  // passes reading the list being left run there (or on `stream`: ordered)
+      DM_HIP(hipEventRecord(g->flist_ev[g->flist_cur], g->pass_stream));
+      g->flist_ev_set[g->flist_cur] = true;
+    }
+    g->flist_cur = x;
+    g->ftiles = g->flist[x];
+    g->ftiles_n = g->flist_n[x];
+  }
   DM_HIP(hipMemsetAsync(g->ftiles_n, 0, sizeof(unsigned long long), g->stream));
   const int iters = (int)std::min<int64_t>(kListIters, std::max<int64_t>(1, (g->NT + 65535) / 65536));
   DM_LAUNCH(k_list_tiles, dim3(grid_for((g->NT + iters - 1) / iters, 256, 1024)), dim3(256), 0, g->stream,
@@ -1614,7 +1628,7 @@ int dm_launch_recount(dm_grid* g) {
   DM_LAUNCH(k_recount, dim3((unsigned)g->NT), dim3(256), 0, g->stream, ge, g->state,
                      g->tile_free, g->fmask, g->fedge);
   DM_HIP(hipGetLastError());
-  if (int rc = dm_launch_relist(g)) return rc;
+  if (int rc = dm_launch_relist(g, false)) return rc;
   g->fmask_valid = true;
   return DM_OK;
 }

@@ -291,7 +291,7 @@ struct dm_grid {
   int32_t last_S = 0, last_N = 0;
 
   // frontier workspace
-  // What a pass's prep and bit kernels write on `stream` while the previous
+  // What a pass's bit-row kernel writes on `stream` while the previous
   // pass's labelling may still run on pass_stream is double-buffered by pass
   // parity (fparity): counters, shards, list, frontier bit rows, edge slots,
   // slot parents.  The current set's arrays are also reachable through the
@@ -315,8 +315,8 @@ struct dm_grid {
   // a ring of three on separate lines: pass n uses fl_n[16 * (n % 3)]
   unsigned long long* fl_n = nullptr;
   // pass_stream (dm_set_overlap + dm_frontiers_begin): the labelling half of
-  // a pass (tile kernels, resolve, sort) runs there, after the prep and the
-  // bit-row kernel on `stream` (which alone read the map), so the next
+  // a pass (tile kernels, resolve, sort) runs there, after the bit-row
+  // kernel on `stream` (which alone reads the map), so the next
   // batch's map update overlaps it.  bits_flag / bits_seq: the bit rows'
   // hand-off (k_seq_signal on `stream`, k_seq_gate on pass_stream).
   hipStream_t pass_stream = nullptr;
@@ -337,9 +337,19 @@ struct dm_grid {
   // bulk writes (dm_launch_recount: k_list_tiles).  Append-only between
   // rebuilds, so a pass reads the first *ftiles_n entries (its snapshot, taken
   // on the map stream after its batch) while later batches append behind them.
-  int32_t* ftiles = nullptr;               // [NT]
-  unsigned long long* ftiles_n = nullptr;  // [16]: [0] the list length
-  int relist_age = 0;  // passes since the list was last put in tile order (dm_launch_relist)
+  int32_t* ftiles = nullptr;               // [NT] the current list (one of flist)
+  unsigned long long* ftiles_n = nullptr;  // [16]: [0] its length
+  // Two lists: the periodic rebuild in tile order (dm_launch_relist) writes
+  // the other one and switches, so passes still labelling go on reading the
+  // old one (nothing appends to it after the switch) and the map stream never
+  // waits for them; flist_ev[i]: the pass stream's position when list i was
+  // left, which a rebuild into list i waits for (long done 16 passes later)
+  int32_t* flist[2] = {nullptr, nullptr};
+  unsigned long long* flist_n[2] = {nullptr, nullptr};
+  hipEvent_t flist_ev[2] = {nullptr, nullptr};
+  bool flist_ev_set[2] = {false, false};
+  int flist_cur = 0;
+  int relist_age = 0;  // passes since the list was last put in tile order
   int32_t* big_tiles = nullptr;  // [NT] per list position: 1 = too many runs for a tile-wave (k_frontier_bits)
   uint64_t* fbits = nullptr;   // [NT][64] frontier bit rows of the listed tiles (k_frontier_bits)
   int32_t* border = nullptr;   // [tile][4][64] slot ids of a tile's edges (published sides only)
@@ -504,7 +514,9 @@ inline int32_t dm_integrate_chunks(const dm_grid* g, int64_t nb) {
 int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                         const float* d_ranges, const double* d_trig);
 int dm_launch_recount(dm_grid* g);
-int dm_launch_relist(dm_grid* g);
+// swap: rebuild into the other list and switch (passes may be in flight);
+// otherwise into the current one (every stream joined: bulk writes)
+int dm_launch_relist(dm_grid* g, bool swap);
 // Passes between rebuilds of the tile list in tile order (dm_launch_relist).
 constexpr int kRelistPasses = 16;
 int dm_launch_state_from_logodds(dm_grid* g);
