@@ -1633,9 +1633,10 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   }
   dm_select_fw(g, g->fparity);
   unsigned long long* list_n = g->fl_n + 16 * (g->fr_pass % 3);  // this pass's list length (k_frontier_bits)
-  // every kRelistPasses passes the tile list goes back into tile order, into
-  // the other list (dm_launch_relist: the passes still labelling keep theirs)
-  if (++g->relist_age >= kRelistPasses)
+  // every relist_period passes (1, 2, 4, ... 16) the tile list goes back into
+  // tile order, into the other list (dm_launch_relist: the passes still
+  // labelling keep theirs)
+  if (++g->relist_age >= g->relist_period)
     if (int rc = dm_launch_relist(g, true)) return rc;
   KernelTimer t;
   if (want_mask) DM_HIP(hipMemsetAsync(g->mask, 0, (size_t)cells, g->stream));

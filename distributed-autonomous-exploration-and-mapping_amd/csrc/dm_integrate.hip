@@ -1616,6 +1616,8 @@ int dm_launch_relist(dm_grid* g, bool swap) {
             g->NT, g->tile_free, g->ftiles, g->ftiles_n, iters);
   DM_HIP(hipGetLastError());
   g->relist_age = 0;
+  // from a fresh list (bulk writes) the period doubles up to kRelistPasses
+  g->relist_period = swap ? std::min(2 * g->relist_period, kRelistPasses) : 1;
   return DM_OK;
 }
 

@@ -349,7 +349,9 @@ struct dm_grid {
   hipEvent_t flist_ev[2] = {nullptr, nullptr};
   bool flist_ev_set[2] = {false, false};
   int flist_cur = 0;
-  int relist_age = 0;  // passes since the list was last put in tile order
+  int relist_age = 0;     // passes since the list was last put in tile order
+  int relist_period = 1;  // passes between those rebuilds: 1, 2, 4, ... up to kRelistPasses
+                          // (a fresh map's list grows fastest in its first passes)
   int32_t* big_tiles = nullptr;  // [NT] per list position: 1 = too many runs for a tile-wave (k_frontier_bits)
   uint64_t* fbits = nullptr;   // [NT][64] frontier bit rows of the listed tiles (k_frontier_bits)
   int32_t* border = nullptr;   // [tile][4][64] slot ids of a tile's edges (published sides only)
@@ -517,7 +519,8 @@ int dm_launch_recount(dm_grid* g);
 // swap: rebuild into the other list and switch (passes may be in flight);
 // otherwise into the current one (every stream joined: bulk writes)
 int dm_launch_relist(dm_grid* g, bool swap);
-// Passes between rebuilds of the tile list in tile order (dm_launch_relist).
+// Passes between rebuilds of the tile list in tile order (dm_launch_relist),
+// once the doubling period from a fresh list reaches it.
 constexpr int kRelistPasses = 16;
 int dm_launch_state_from_logodds(dm_grid* g);
 int dm_launch_map_image(dm_grid* g, uint8_t* d_img);

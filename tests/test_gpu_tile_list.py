@@ -2,12 +2,13 @@
 tile that has held a free cell since the last rebuild, appended by the
 integrate apply when a tile's free count first rises above 0 (listed flag in
 `tile_free`), rebuilt in tile order by k_list_tiles after bulk writes
-(dm_set_state, dm_set_logodds, dm_reset, dm_load) and every 16 passes.  A
-pass's `frontier_tiles` statistic is its snapshot of the list length, so
-within 16 passes of a bulk write it equals the number of tiles that ever held
-a free cell since; tiles that lost every free cell stay listed until the next
-rebuild without changing any result, and a rebuild drops them (flag cleared,
-so a tile that regains a free cell is appended again)."""
+(dm_set_state, dm_set_logodds, dm_reset, dm_load) and periodically (after 1,
+2, 4, 8 passes, then every 16).  A pass's `frontier_tiles` statistic is its
+snapshot of the list length: at least the tiles holding a free cell, at most
+the tiles that held one since the last bulk write; tiles that lost every free
+cell stay listed until the next rebuild without changing any result, and a
+rebuild drops them (flag cleared, so a tile that regains a free cell is
+appended again)."""
 import numpy as np
 import pytest
 
@@ -36,7 +37,8 @@ def test_list_grows_with_every_tile_that_held_a_free_cell(oracle_lib):
             ever |= _tiles_with_free(om.state)
             fr = m.frontiers()
             np.testing.assert_array_equal(fr.clusters, om.frontiers(want_mask=False, want_labels=False)[2])
-            assert m.last_stats()["frontier_tiles"] == int(ever.sum())
+            n = m.last_stats()["frontier_tiles"]
+            assert int(_tiles_with_free(om.state).sum()) <= n <= int(ever.sum())
         assert_map_equal(m, om)
 
 
