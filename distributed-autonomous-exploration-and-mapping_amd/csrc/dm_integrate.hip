@@ -1546,14 +1546,16 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   // and ~12.8 k that exit at once, whose dispatch held the kernel's end and
   // the front-end streams' first workgroups ~6 us longer in the pipelined
   // step (profiles/r04_accum_timeline.log); the last finished call's count
-  // (+25 % + 256) sizes it instead
+  // (+1/16 + 64: calls of one workload differ by a few percent; a grid one
+  // short of the items only gives a few workgroups a second item) sizes it
+  // instead (+25 % + 256 measured 1-3 % slower, profiles/r04_accum_grid_slack_ab.log)
   const volatile unsigned long long* hint = g->h_hint;
   const int64_t cap = g->hitem_cap + g->act_cap;
 #ifndef DM_ACCUM_HINT
 #define DM_ACCUM_HINT 1  // 0: capacity grids (the round-3 launch, for A/B builds)
 #endif
   const int64_t hw = DM_ACCUM_HINT ? (int64_t)hint[0] : 0, hi = DM_ACCUM_HINT ? (int64_t)hint[1] : 0;
-  const int64_t accum_wgs = hw > 0 ? std::min(cap, dm_quantize_up(hw + hw / 4 + 256)) : cap;
+  const int64_t accum_wgs = hw > 0 ? std::min(cap, dm_quantize_up(hw + hw / 16 + 64)) : cap;
   DM_LAUNCH(k_tile_accum, dim3(grid_for(accum_wgs, 1, dm_grid::kAccumGrid)),
                      dim3(kQuarter), 0,
                      g->stream, ge, make_apply(g), w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS,
@@ -1569,7 +1571,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
     return DM_OK;
   }
   dm_timer_begin(g, "fmask", &t);
-  const int64_t fmask_items = hi > 0 ? std::min(cap, dm_quantize_up(hi + hi / 4 + 256)) : cap;
+  const int64_t fmask_items = hi > 0 ? std::min(cap, dm_quantize_up(hi + hi / 16 + 64)) : cap;
   DM_LAUNCH(k_fmask_items, dim3(grid_for(fmask_items, 4, 8192)), dim3(256), 0, g->stream,
                      ge, w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS, (int)CNT_SITEMS, w.pieces, w.cnt,
                      g->state, g->fmask, g->fedge,
