@@ -177,42 +177,32 @@ def main():
         H_total = G * world_size
     half_w = G * res / 2.0
     oy_global = -H_total * res / 2.0
-    # one world over the whole map (every rank builds the same one)
-    world = synth.make_world(args.seed * 1000, -half_w, oy_global, half_w, -oy_global)
     from dm.sharded import band_rows as _band_rows
     b_row0, b_rows = _band_rows(H_total, world_size, rank) if world_size > 1 else (0, H_total)
-
-    def band_stream(q):
-        """Rank q's robots: random-walking anywhere in q's band."""
-        y0 = oy_global + q * G * res
-        return synth.ScanStream(world, args.robots, args.beams, args.seed * 1000 + 500 + q,
-                                region=(-half_w + 1.0, y0 + 1.0, half_w - 1.0, y0 + G * res - 1.0))
-
     # Scans near a band edge also reach the neighbouring band: each rank
     # integrates its own robots' scans plus the neighbours' scans whose
     # max-range disk reaches its band (host-side replication of the scan
     # stream, SURVEY.md §8(e)); libdm clips every ray to the band, so each
     # cell update is counted by exactly one rank.  C4: every rank replays the
     # same 32-robot stream and keeps the scans that reach its band.
-    reach = 12.0 + 2 * res
-    ylo = oy_global + b_row0 * res - reach
-    yhi = oy_global + (b_row0 + b_rows) * res + reach
-    if c4:
-        streams = {-1: synth.ScanStream(world, args.robots, args.beams, args.seed * 1000 + 500,
-                                        region=(-half_w + 1.0, oy_global + 1.0, half_w - 1.0,
-                                                -oy_global - 1.0))}
-    else:
-        streams = {q: band_stream(q) for q in (rank - 1, rank, rank + 1) if 0 <= q < world_size}
     t_gen = time.perf_counter()
-    pool = []
-    for _ in range(args.pool):
-        poses, ranges = [], []
-        for q, st in streams.items():
+    if c4:
+        # one world over the whole map (every rank builds the same one)
+        world = synth.make_world(args.seed * 1000, -half_w, oy_global, half_w, -oy_global)
+        reach = 12.0 + 2 * res
+        ylo = oy_global + b_row0 * res - reach
+        yhi = oy_global + (b_row0 + b_rows) * res + reach
+        st = synth.ScanStream(world, args.robots, args.beams, args.seed * 1000 + 500,
+                              region=(-half_w + 1.0, oy_global + 1.0, half_w - 1.0, -oy_global - 1.0))
+        pool = []
+        for _ in range(args.pool):
             p_, r_ = st.next_batch()
-            keep = np.ones(len(p_), bool) if q == rank else (p_[:, 1] >= ylo) & (p_[:, 1] <= yhi)
-            poses.append(p_[keep])
-            ranges.append(r_[keep])
-        pool.append((np.concatenate(poses), np.concatenate(ranges)))
+            keep = (p_[:, 1] >= ylo) & (p_[:, 1] <= yhi)
+            pool.append((p_[keep], r_[keep]))
+    else:
+        # rank r's robots random-walk anywhere in r's band (synth.c3_pool:
+        # the same batches the GPU test of the timed configuration replays)
+        world, _, pool = synth.c3_pool(args.seed, G, args.robots, args.beams, args.pool, world_size, rank, res)
     t_gen = time.perf_counter() - t_gen
     amin = float(synth.LD06_ANGLE_MIN)
     inc = float(synth.ld06_angle_increment(args.beams))
@@ -481,6 +471,12 @@ def main():
             "clusters": fr_clusters,
             "kernel_avg_ms": avg,
             "roofline": {
+                # bytes the DRAM actually moved (PMC) lead: the model's 8 B per
+                # update stay in LDS, so `frac` (the contract's algorithmic
+                # fraction) credits bytes that never reach HBM
+                "frac_traffic": (traffic / (t_accum_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS
+                                 if traffic and t_accum_ms > 0 else None),
+                "traffic": traffic,
                 "kernel": "tile_accum",
                 "dominant_kernel": dominant,
                 "bound": "hbm",
@@ -488,12 +484,7 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
-                "traffic": traffic,
                 "traffic_source": traffic_src,
-                # the same launch against the bytes it actually moved (PMC,
-                # per-shape calibrated factors): what the DRAM really did
-                "frac_traffic": (traffic / (t_accum_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS
-                                 if traffic and t_accum_ms > 0 else None),
                 "avg_launch_ms": t_accum_ms,
                 "algorithmic_bytes_per_launch": bytes_accum,
                 "bytes_model": "8*U + 25*T per call (SURVEY.md §8(d) per-unit figures)",
@@ -580,17 +571,16 @@ def frontier_roofline(avg, cells, F, K, tiles_visited, workload, wall_s=None):
     read per frontier cell) + 48*K (cluster records); the kernels read only
     the tiles holding a free cell, so `frac` is that model
     over the tiles the pass actually lists (4096 state bytes + 260 halo bytes
-    + a 4096-byte mask each: `visited_bytes`), `frac_full_map` the whole-map
-    model (it charges bytes a sparse pass never touches), and
-    `frac_traffic` the PMC-measured bytes."""
+    + a 4096-byte mask each: `visited_bytes`) and `frac_traffic` the
+    PMC-measured bytes (listed first: what the DRAM really moved).  No
+    whole-map fraction: a pass reads only the listed tiles."""
     t_ms = frontier_device_ms(avg)
-    B = 2.0 * cells + 16.0 * F + 48.0 * K
-    ach_full = B / (t_ms * 1e-3) / 1e9 if t_ms > 0 else None
-    out = {"bound": "hbm", "bytes_model": "(4096 + 260 + 4096)*tiles_visited + 16*F + 48*K per pass "
+    # frac_traffic (PMC bytes moved) is filled in first below when measured
+    out = {"frac_traffic": None, "traffic": None,
+           "bound": "hbm", "bytes_model": "(4096 + 260 + 4096)*tiles_visited + 16*F + 48*K per pass "
                                           "(SURVEY.md §8(d)'s 2*W*H + 16*F + 48*K over the listed tiles)",
-           "full_map_bytes": B, "frontier_cells": F, "clusters": K, "device_ms": t_ms,
+           "frontier_cells": F, "clusters": K, "device_ms": t_ms,
            "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-           "frac_full_map": ach_full / HBM_PEAK_GBPS if ach_full else None,
            "kernels_ms": {k: avg[k] for k in FRONTIER_KERNELS if k in avg}}
     if wall_s:
         out["wall_ms"] = wall_s * 1e3
@@ -599,7 +589,6 @@ def frontier_roofline(avg, cells, F, K, tiles_visited, workload, wall_s=None):
     out.update({"tiles_visited": tiles_visited, "algorithmic_bytes": vb, "achieved": ach,
                 "frac": ach / HBM_PEAK_GBPS if ach else None})
     w, src = pmc_summary(workload)
-    out["traffic"] = None
     out["traffic_source"] = src
     if w is not None:
         ks = w.get("kernels", {})

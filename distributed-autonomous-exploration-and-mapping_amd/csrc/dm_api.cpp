@@ -1068,6 +1068,10 @@ int dm_merge_bands_begin(dm_grid* g, const void* d_gathered, int32_t nranks, int
   if (ms != g->stream) {
     g->p_tail = r.ev;
     g->p_pending = true;
+    // no band pass's completion implies this merge's: only an explicit join
+    // (dm_join_pass_stream) clears it, never wait_oldest of a kind-1 pass
+    // (the merge reads the shared sort workspace a later pass would reuse)
+    g->p_tail_pass = UINT64_MAX;
   }
   r.kind = 2;
   r.merge_n = n;

@@ -61,6 +61,14 @@ def band_rows(height: int, world_size: int, rank: int):
     return row0, rows
 
 
+def group_ranks(dist, group=None) -> list[int]:
+    """Global ranks of `group` (None: the default group) in group-rank order:
+    the member list a second communicator over the same processes needs."""
+    if group is None or group is dist.group.WORLD:
+        return list(range(dist.get_world_size()))
+    return [int(r) for r in dist.get_process_group_ranks(group)]
+
+
 def band_params(params: DmParams, world_size: int, rank: int) -> DmParams:
     bp = DmParams.from_buffer_copy(params)
     row0, rows = band_rows(int(params.height), world_size, rank)
@@ -159,15 +167,19 @@ class ShardedMapper:
     rank `rank`'s part.  With world_size == 1 it is a plain OccupancyMapper."""
 
     def __init__(self, params: DmParams, rank: int = 0, world_size: int = 1, device: int = 0,
-                 group=None, band=None, timeout: float = 300.0):
+                 group=None, band=None, timeout: float = 300.0, force_exchange: bool = False):
         """`timeout`: seconds any collective (or the device work queued behind
-        one) may take before this rank gives up with DM_ERR_COLLECTIVE."""
+        one) may take before this rank gives up with DM_ERR_COLLECTIVE.
+        `force_exchange`: with world_size 1, run the multi-rank exchange
+        anyway (halo gather, export record, records gather, device merge)
+        over `group` (a 1-rank process group): the RCCL path on one GPU."""
         self.params = DmParams.from_buffer_copy(params)
         self.rank, self.world_size, self.group = rank, world_size, group
+        self._exchange = world_size > 1 or bool(force_exchange)
         self.timeout = float(timeout)
         self.failed = None  # sticky DM_ERR_COLLECTIVE message
         self.min_size = int(params.min_frontier_size)
-        if world_size == 1:
+        if not self._exchange:
             bp = DmParams.from_buffer_copy(params)
         else:
             bp = band_params(params, world_size, rank)
@@ -181,7 +193,7 @@ class ShardedMapper:
             self.max_in_flight = int(load_library().dm_max_passes_in_flight())
         except Exception:  # a non-libdm band (CPU tests): libdm's default ring
             self.max_in_flight = 2
-        if world_size > 1:
+        if self._exchange:
             import torch.distributed as dist
 
             self._dist = dist
@@ -208,8 +220,11 @@ class ShardedMapper:
                 # communicator: a records gather that waits for a pass's
                 # labelling then never holds up the next pass's halo gather
                 # on the map stream (one communicator runs its collectives
-                # in issue order)
-                self.rec_group = dist.new_group(list(range(world_size)))
+                # in issue order).  Built over the mapper's own group's
+                # ranks (a subgroup's ranks are not 0..P-1 globally);
+                # new_group is collective over the default group, so every
+                # process of it constructs its mappers in the same order.
+                self.rec_group = dist.new_group(group_ranks(dist, group))
                 self._xstreams = {}
                 # records per band export: sized for the band up front (a
                 # cluster per tile: C5's 4096-beam fans reach 0.81), then to
@@ -291,7 +306,7 @@ class ShardedMapper:
         ranges = np.asarray(ranges, np.float32)
         if ranges.ndim != 2:
             ranges = ranges.reshape(poses.shape[0], -1)
-        if self.world_size > 1:
+        if self._exchange:
             keep = self.scan_mask(poses)
             poses, ranges = poses[keep], ranges[keep]
         return self.band.integrate(poses, ranges, angle_min, angle_increment)
@@ -417,7 +432,7 @@ class ShardedMapper:
         """Frontiers of the map as it is now (synchronous; passes started with
         frontiers_begin() may still be in flight)."""
         self._check()
-        if self.world_size == 1:
+        if not self._exchange:
             return self.band.frontiers(want_mask=want_mask, want_labels=want_labels)
         if self._dev_path and not (want_mask or want_labels):
             return self._frontiers_device()
@@ -440,10 +455,10 @@ class ShardedMapper:
         if len(self._pending) >= self.max_in_flight:
             raise RuntimeError(f"{len(self._pending)} frontiers_begin() passes are in flight: "
                                "call frontiers_end() first")
-        if self.world_size == 1 and hasattr(self.band, "frontiers_begin"):
+        if not self._exchange and hasattr(self.band, "frontiers_begin"):
             self.band.frontiers_begin()
             self._pending.append(("band", None))
-        elif self.world_size > 1 and self._dev_path:
+        elif self._exchange and self._dev_path:
             gexp, xs = self._device_enqueue()
             with self._torch.cuda.stream(xs):  # libdm merges on the exchange stream
                 self.band.merge_bands_begin(gexp.data_ptr(), self.world_size, self.rec_cap, self.min_size)

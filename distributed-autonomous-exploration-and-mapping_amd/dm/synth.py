@@ -286,3 +286,41 @@ def ld06_points(world: World, x: float, y: float, yaw: float, rng: np.random.Gen
     pts["distance_mm"] = np.where(ok, np.round(d * 1000.0), 0).astype(np.uint16)
     pts["intensity"] = np.where(ok, rng.integers(100, 255, n_points), 0).astype(np.uint8)
     return pts
+
+
+def c3_pool(seed: int, G: int, robots: int, beams: int, n: int, world_size: int = 1, rank: int = 0,
+            res: float = 0.05):
+    """The bench line's C3 batches (bench.py): rank
+    `rank` of `world_size` owns a G-row band of a G x G*world_size map; each
+    band has `robots` robots random-walking anywhere in it, in one world over
+    the whole map; a rank integrates its own robots' scans plus the
+    neighbouring bands' scans whose max-range disk reaches its band.
+    Returns (world, (origin_x, origin_y), pool): pool is n (poses [S,3],
+    ranges [S,beams]) batches.  Tests replay exactly what bench.py times."""
+    from .sharded import band_rows
+
+    H_total = G * world_size
+    half_w = G * res / 2.0
+    oy_global = -H_total * res / 2.0
+    world = make_world(seed * 1000, -half_w, oy_global, half_w, -oy_global)
+    b_row0, b_rows = band_rows(H_total, world_size, rank) if world_size > 1 else (0, H_total)
+
+    def band_stream(q):
+        y0 = oy_global + q * G * res
+        return ScanStream(world, robots, beams, seed * 1000 + 500 + q,
+                          region=(-half_w + 1.0, y0 + 1.0, half_w - 1.0, y0 + G * res - 1.0))
+
+    reach = 12.0 + 2 * res
+    ylo = oy_global + b_row0 * res - reach
+    yhi = oy_global + (b_row0 + b_rows) * res + reach
+    streams = {q: band_stream(q) for q in (rank - 1, rank, rank + 1) if 0 <= q < world_size}
+    pool = []
+    for _ in range(n):
+        poses, ranges = [], []
+        for q, st in streams.items():
+            p_, r_ = st.next_batch()
+            keep = np.ones(len(p_), bool) if q == rank else (p_[:, 1] >= ylo) & (p_[:, 1] <= yhi)
+            poses.append(p_[keep])
+            ranges.append(r_[keep])
+        pool.append((np.concatenate(poses), np.concatenate(ranges)))
+    return world, (-half_w, oy_global), pool

@@ -12,7 +12,7 @@ print("tile_accum frac", r.get("frac"), "avg ms", r.get("avg_launch_ms"), "traff
 if r.get("atomics"):
     print("atomics frac", r["atomics"]["frac"])
 fr = r.get("frontier") or {}
-print("frontier device ms", fr.get("device_ms"), "frac", fr.get("frac"), "frac_full_map", fr.get("frac_full_map"), "frac_traffic", fr.get("frac_traffic"))
+print("frontier device ms", fr.get("device_ms"), "frac", fr.get("frac"), "frac_traffic", fr.get("frac_traffic"))
 print("kernels", {k: round(v * 1e3, 1) for k, v in d.get("kernel_avg_ms", {}).items()})
 ex = d.get("frontier_explored")
 if ex:

@@ -77,6 +77,21 @@ for s in "$@"; do
     c5:*)
       timeout -k 10 600 python -u bench.py --config C5 --sweep ${s#c5:} --cpu-seconds 0 > $OUT/bench_c5.log 2>&1
       rc=$?; echo "c5 rc=$rc"; tail -1 $OUT/bench_c5.log | cut -c1-300; ok $rc || exit $rc ;;
+    driver)
+      # the driver's exact command three times (step traces), a 200-step run,
+      # and a kernel trace of the driver's command (per-step kernels after reset)
+      for i in 1 2 3; do
+        timeout -k 10 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 --step-trace $OUT/drv_trace_$i.json \
+          > $OUT/drv_$i.log 2>&1
+        rc=$?; echo "driver run $i rc=$rc"; ok $rc || exit $rc
+      done
+      timeout -k 10 400 python -u bench.py --gpus 1 --steps 200 --warmup 5 --cpu-seconds 0 \
+        --step-trace $OUT/drv_trace_200.json > $OUT/drv_200.log 2>&1
+      rc=$?; echo "200-step rc=$rc"; ok $rc || exit $rc
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace -d $OUT/drvprof -o run \
+        --output-format csv -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 \
+        --no-explored --no-host-inputs > $OUT/drvprof.log 2>&1)
+      rc=$?; echo "drvprof rc=$rc"; ok $rc || exit $rc ;;
     cfg:*)
       c=${s#cfg:}
       timeout -k 10 400 python -u bench.py --config $c --cpu-seconds 10 > $OUT/bench_$c.log 2>&1
