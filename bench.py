@@ -285,23 +285,26 @@ def main():
 
     if pipelined:
         mapper.set_overlap(True)
-    run_steps(0, args.warmup)
 
     def barrier():
         if world_size > 1:
             dist.barrier()
 
-    barrier()
-    torch.cuda.synchronize()
-    # no cyclic-GC pass inside the timed steps (the objects of warm-up and
-    # setup are frozen first): a collection is a host stall of 0.1+ ms that
-    # the pipelined step cannot hide (as timeit does; reference counting still
-    # frees everything the steps create)
+    # no cyclic-GC pass inside the timed steps (the setup's objects are frozen
+    # first): a collection is a host stall of 0.1+ ms that the pipelined step
+    # cannot hide (as timeit does; reference counting still frees everything
+    # the steps create).  Done BEFORE the warm-up: a collection between the
+    # warm-up and the timed steps (~65 ms with torch loaded) left the GPU idle
+    # and the host's caches cold, and the first timed step took 175-200 us
+    # instead of ~100 (profiles/r05_driver_cmd_*)
     import gc
 
     gc.collect()
     gc.freeze()
     gc.disable()
+    run_steps(0, args.warmup)
+    barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     marks = []
     fr = run_steps(args.warmup, args.steps, marks=marks)

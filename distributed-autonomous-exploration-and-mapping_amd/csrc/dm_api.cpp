@@ -574,16 +574,26 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   // so a front-end enqueued early fills what the map chain leaves idle instead
   // of competing with the accumulation for its CUs (round-2/3 A/B of every
   // combination and of CU-masked streams: DESIGN.md §3.3).
+  // (DM_PRIO_GRID / _FE / _PASS: 1 high, 0 low -- A/B builds only)
+#ifndef DM_PRIO_GRID
+#define DM_PRIO_GRID 1
+#endif
+#ifndef DM_PRIO_FE
+#define DM_PRIO_FE 0
+#endif
+#ifndef DM_PRIO_PASS
+#define DM_PRIO_PASS 1
+#endif
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  e = hipStreamCreateWithPriority(&g->stream, hipStreamNonBlocking, prio_hi);
+  e = hipStreamCreateWithPriority(&g->stream, hipStreamNonBlocking, DM_PRIO_GRID ? prio_hi : prio_lo);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate"));
   g->own_stream = true;
-  e = hipStreamCreateWithPriority(&g->fe_stream, hipStreamNonBlocking, prio_lo);
+  e = hipStreamCreateWithPriority(&g->fe_stream, hipStreamNonBlocking, DM_PRIO_FE ? prio_hi : prio_lo);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(front-end)"));
-  e = hipStreamCreateWithPriority(&g->pass_stream, hipStreamNonBlocking, prio_hi);
+  e = hipStreamCreateWithPriority(&g->pass_stream, hipStreamNonBlocking, DM_PRIO_PASS ? prio_hi : prio_lo);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(pass)"));
-  e = hipStreamCreateWithPriority(&g->big_stream, hipStreamNonBlocking, prio_hi);
+  e = hipStreamCreateWithPriority(&g->big_stream, hipStreamNonBlocking, DM_PRIO_PASS ? prio_hi : prio_lo);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(big)"));
   // ev_fe / ev_free only order the two streams on the device: no system-
   // scope fence (no host-visible cache writeback at every step).  The host
@@ -995,7 +1005,7 @@ int claim_slot(dm_grid* g, int* slot) {
 int wait_oldest(dm_grid* g, int kind, const char* what) {
   if (!g->rb_count || g->rb[g->rb_head].kind != kind)
     return dm_set_error(DM_ERR_INVALID_ARG, "the oldest pass in flight is not a %s pass", what);
-  DM_HIP(hipEventSynchronize(g->rb[g->rb_head].ev));
+  DM_HIP(dm_event_wait(g->rb[g->rb_head].ev));
   if (kind == 1) {  // passes end in order: this one and every earlier one are done
     const uint64_t pass = g->rb[g->rb_head].pass;
     for (auto& f : g->fw)

@@ -646,29 +646,36 @@ __device__ inline int32_t walk_piece(uint32_t* tl, const PackedPiece& mine, bool
   return walk_tp(tl, tp, valid ? tp.len : 0, lane);
 }
 
+#ifndef DM_SPLIT_WALK
+#define DM_SPLIT_WALK 1  // 0: one lane per piece (the round-4 walk, for A/B builds)
+#endif
+
 // Light tiles: their pieces cross the tile from different directions and
-// rarely share cells, so each lane walks from its piece's first cell, with
-// no stagger and no wrap.  A lane whose piece has ended adds into its own
-// spare word past the tile (tl[kTileWords + lane], never read) instead of
-// masking the step: no exec-mask branch per step, no pile-up on one word.
-// Returns the piece's length (its cell updates).
-__device__ inline int32_t walk_tp_plain(uint32_t* tl, const TilePiece& tp, int32_t len, int lane) {
-  int32_t wl = len;
+// rarely share cells, so each lane walks from its first cell, with no
+// stagger and no wrap.  A lane whose part has ended adds into its own spare
+// word past the tile (tl[kTileWords + lane], never read) instead of masking
+// the step: no exec-mask branch per step, no pile-up on one word.
+// With fewer pieces than lanes: each piece is split over
+// f = lanes / c lanes (dm_split_part), lane `part` of them walking cells
+// [j0, j0 + n) from the closed-form cell j0 (PieceCursor::init_at).  The
+// wave's trip count is its longest part instead of its longest piece: C3's
+// light items (95 pieces on average) 45 -> 31 steps on the critical path.
+// The part that ends the piece adds the hit (SPEC a6).
+__device__ inline int32_t walk_tp_split(uint32_t* tl, const TilePiece& tp, int32_t len, int32_t f, int32_t part,
+                                        float rf, int lane) {
+  const SplitPart sp = dm_split_part(len, f, part, rf);
+  int32_t wl = sp.n;
   for (int o = 32; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o));
   const int32_t spare = kTileWords + lane;
   PieceCursor cur;
-  cur.init(tp);
+  if (f == 1) cur.init(tp);
+  else cur.init_at(tp, sp.j0, __builtin_amdgcn_rcpf((float)tp.two_n));
   for (int32_t st = 0; st < wl; ++st) {
-    atomicAdd(&tl[st < len ? cur.addr : spare], 1u);
+    atomicAdd(&tl[st < sp.n ? cur.addr : spare], 1u);
     cur.step(tp);
   }
-  if (len > 0 && tp.addr_end >= 0) atomicAdd(&tl[tp.addr_end], 0xFFFFu);
-  return len;
-}
-
-__device__ inline int32_t walk_piece_plain(uint32_t* tl, const PackedPiece& mine, bool valid, int lane) {
-  const TilePiece tp = dm_unpack_piece(mine.x, mine.y, mine.z, mine.w);
-  return walk_tp_plain(tl, tp, valid ? tp.len : 0, lane);
+  if (sp.n > 0 && sp.j0 + sp.n == len && tp.addr_end >= 0) atomicAdd(&tl[tp.addr_end], 0xFFFFu);
+  return sp.n;
 }
 
 // Sparse items: the same walk into a byte-packed count tile (pitch 64, one
@@ -686,25 +693,30 @@ __device__ inline int32_t to_pitch64(int32_t a) {  // pitch-65 address or step -
   return a >= 0 ? a - a / kLdsPitch : -((-a) - (-a) / kLdsPitch);
 }
 
-__device__ inline int32_t walk_piece_bytes(uint32_t* tq, const PackedPiece& mine, bool valid) {
+// Split as walk_tp_split: a sparse tile's c <= 15 pieces over the wave's 64
+// lanes, f = 64 / c >= 4 lanes per piece (lane `part` of them).
+__device__ inline int32_t walk_piece_bytes(uint32_t* tq, const PackedPiece& mine, bool valid, int32_t f,
+                                           int32_t part, float rf) {
   TilePiece tp = dm_unpack_piece(mine.x, mine.y, mine.z, mine.w);
   const int32_t len = valid ? tp.len : 0;
-  int32_t wl = len;
+  const SplitPart sp = dm_split_part(len, f, part, rf);
+  int32_t wl = sp.n;
   for (int o = 32; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o));
   tp.addr0 = to_pitch64(tp.addr0);
   tp.da = to_pitch64(tp.da);
   tp.db = to_pitch64(tp.db);
   PieceCursor cur;
-  cur.init(tp);
+  if (f == 1) cur.init(tp);
+  else cur.init_at(tp, sp.j0, __builtin_amdgcn_rcpf((float)tp.two_n));
   for (int32_t st = 0; st < wl; ++st) {
-    if (st < len) atomicAdd(&tq[cur.addr >> 2], 1u << (8 * (cur.addr & 3)));
+    if (st < sp.n) atomicAdd(&tq[cur.addr >> 2], 1u << (8 * (cur.addr & 3)));
     cur.step(tp);
   }
-  if (len > 0 && tp.addr_end >= 0) {
+  if (sp.n > 0 && sp.j0 + sp.n == len && tp.addr_end >= 0) {
     const int32_t e = to_pitch64(tp.addr_end);
     atomicAdd(&tq[e >> 2], 0x0Fu << (8 * (e & 3)));
   }
-  return len;
+  return sp.n;
 }
 
 __device__ inline PackedPiece no_piece() {
@@ -837,7 +849,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok,
     const int32_t* __restrict__ heavy_list, int32_t* heavy_done, int32_t* tlist, unsigned long long* tlist_n,
     unsigned long long* hint, const unsigned long long* __restrict__ halt) {
-  __shared__ uint32_t tl[kTileWords + 64];  // + one spare word per lane (walk_piece_plain)
+  __shared__ uint32_t tl[kTileWords + 64];  // + one spare word per lane (walk_tp_split)
   __shared__ int32_t s_T, s_free, s_last;
   __shared__ uint32_t s_U;
   const int tid = threadIdx.x, lane = lane_id();
@@ -891,12 +903,22 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
   PackedPiece mine;
   CellRows<4> cells;
   int32_t tfree;
+  // a light item's split factor (walk_tp_split; 1 for heavy / medium items)
+  auto split_of = [&](const int4& d) -> int32_t {
+    const int32_t c = __builtin_amdgcn_readfirstlane(d.z);
+    const int32_t heavy = __builtin_amdgcn_readfirstlane(d.w);
+    return DM_SPLIT_WALK && heavy < 0 ? dm_split_factor(c, kQuarter) : 1;
+  };
+  // this thread's piece of item d (piece tid / f of a split light item)
+  auto piece_of = [&](int32_t f) -> int32_t {
+    return f == 1 ? tid : dm_udiv_small(tid, f, __builtin_amdgcn_rcpf((float)f));
+  };
   auto load_pieces = [&](const int4& d) -> PackedPiece {
     const int32_t c0 = __builtin_amdgcn_readfirstlane(d.y);
     const int32_t c = __builtin_amdgcn_readfirstlane(d.z);
     // lanes past the item's pieces re-read its last one (past the list's end:
     // piece 0); unconditional, so the loop carries no phi of the old pieces
-    return pieces[c0 + min(tid, max(c - 1, 0))];
+    return pieces[c0 + min(piece_of(split_of(d)), max(c - 1, 0))];
   };
   mine = load_pieces(info);
   // DM_EARLY_PIECES: the next item's pieces are issued right after this
@@ -995,7 +1017,10 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
       cells.prefetch(g, tx0, ty0, tid >> 4, 16, cx, L, state, vec_ok);
       int32_t u;  // this thread's cell updates (one per step)
       if (c <= kChunk) {
-        u = walk_piece_plain(tl, mine, tid < c, lane);
+        const int32_t f = split_of(info);
+        const int32_t pi = piece_of(f);
+        const TilePiece tp = dm_unpack_piece(mine.x, mine.y, mine.z, mine.w);
+        u = walk_tp_split(tl, tp, pi < c ? tp.len : 0, f, tid - pi * f, __builtin_amdgcn_rcpf((float)f), lane);
       } else {  // medium: near a sensor, the staggered walk
         u = walk_piece(tl, mine, tid < c, lane);
         for (int32_t r0 = kChunk; r0 < c; r0 += kChunk) {
@@ -1066,9 +1091,13 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     const int32_t tile = d.x, c0 = d.y, c = d.z;
     if (lane == 0 && wv == 0) tl_word += 1ull << 16;
     const int32_t tx0 = (tile % g.r.TX) * DM_TS, ty0 = (tile / g.r.TX) * DM_TS;
-    const PackedPiece sp = lane < c ? pieces[c0 + lane] : no_piece();
+    // f = 64 / c lanes per piece (walk_piece_bytes' split)
+    const int32_t fs = DM_SPLIT_WALK ? dm_split_factor(c, 64) : 1;
+    const float rfs = __builtin_amdgcn_rcpf((float)fs);
+    const int32_t spi = fs == 1 ? lane : dm_udiv_small(lane, fs, rfs);
+    const PackedPiece sp = spi < c ? pieces[c0 + spi] : no_piece();
     const int32_t sfree = tile_free[tile];
-    int32_t u = walk_piece_bytes(tq, sp, lane < c);
+    int32_t u = walk_piece_bytes(tq, sp, spi < c, fs, lane - spi * fs, rfs);
     const bool inside = tx0 + DM_TS <= g.r.W && ty0 + DM_TS <= g.r.R;  // uniform in the wave
     uint32_t wU = 0u;
     if (inside) {

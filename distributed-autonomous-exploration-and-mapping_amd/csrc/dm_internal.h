@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -489,6 +490,25 @@ inline void dm_select_fw(dm_grid* g, int s) {
   g->fbits = f.fbits;
   g->edge_slot = f.edge_slot;
   g->slot_parent = f.slot_parent;
+}
+
+// Host wait for an event the pipelined caller expects within tens of
+// microseconds (a readback slot's pass): poll it instead of
+// hipEventSynchronize, which after a short active wait sleeps on an
+// interrupt and wakes up tens of microseconds late (the bench's step
+// cadence showed +20-80 us spikes on ~10 % of the steps).  After kSpinNs of
+// polling it blocks as before.
+inline hipError_t dm_event_wait(hipEvent_t ev) {
+  constexpr long long kSpinNs = 20000000;  // 20 ms
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned it = 0;; ++it) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e != hipErrorNotReady) return e;
+    if ((it & 63u) == 63u &&
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() > kSpinNs)
+      return hipEventSynchronize(ev);
+    __builtin_ia32_pause();
+  }
 }
 
 // Order `stream` after the pass_stream work enqueued so far (the frontier

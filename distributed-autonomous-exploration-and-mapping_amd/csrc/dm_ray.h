@@ -315,9 +315,39 @@ DM_HD inline TilePiece dm_unpack_piece(uint32_t x, uint32_t y, uint32_t z, uint3
 struct PieceCursor {
   int32_t addr, rem;
   DM_HD void init(const TilePiece& tp) { addr = tp.addr0; rem = tp.rem0; }
+  // at cell j (0 <= j < 64) of the piece: the closed form once (dm_piece_addr)
+  DM_HD void init_at(const TilePiece& tp, int32_t j, float rtwo_n) {
+    const int32_t num = tp.rem0 + j * tp.two_adb;
+    const int32_t dq = dm_udiv_small(num, tp.two_n, rtwo_n);
+    addr = tp.addr0 + j * tp.da + dq * tp.db;
+    rem = num - dq * tp.two_n;
+  }
   DM_HD void step(const TilePiece& tp) {
     addr += tp.da;
     rem += tp.two_adb;
     if (rem >= tp.two_n) { rem -= tp.two_n; addr += tp.db; }
   }
 };
+
+// Split walks (k_tile_accum): an item of c pieces on `lanes` lanes gives
+// each piece f = lanes / c lanes (f >= 1); lane t takes part t % f of piece
+// t / f, cells [j0, j0 + n) with parts of ceil(len / f) cells.  A piece's
+// parts cover its cells exactly once, so the counts do not change; the
+// walk's trip count (the longest part on the wave) shrinks by up to f.
+struct SplitPart {
+  int32_t j0, n;
+};
+DM_HD inline int32_t dm_split_factor(int32_t c, int32_t lanes) { return c > 0 && c <= lanes ? lanes / c : 1; }
+DM_HD inline SplitPart dm_split_part(int32_t len, int32_t f, int32_t part, float rf) {
+  SplitPart s;
+  if (f == 1) {
+    s.j0 = 0;
+    s.n = len;
+    return s;
+  }
+  const int32_t plen = dm_udiv_small(len + f - 1, f, rf);  // ceil(len / f), len <= 64
+  s.j0 = part * plen;
+  const int32_t left = len - s.j0;
+  s.n = left < 0 ? 0 : (left < plen ? left : plen);
+  return s;
+}

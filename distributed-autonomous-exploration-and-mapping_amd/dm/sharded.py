@@ -276,11 +276,17 @@ class ShardedMapper:
         """Wait (host side, at most self.timeout) for a CUDA/HIP event recorded
         after collectives, so no later blocking synchronisation can wait on a
         collective a dead peer never joins."""
-        deadline = time.monotonic() + self.timeout
+        t0 = time.monotonic()
+        deadline = t0 + self.timeout
         while not ev.query():
-            if time.monotonic() > deadline:
+            now = time.monotonic()
+            if now > deadline:
                 self._fail(f"{what}: device exchange did not complete within {self.timeout:g} s")
-            time.sleep(2e-5)
+            # poll without sleeping for the first 2 ms: a pipelined pass ends
+            # tens of microseconds after the host starts waiting, and a sleep
+            # of 20 us oversleeps by ~50 us (the kernel's timer slack)
+            if now - t0 > 2e-3:
+                time.sleep(2e-5)
 
     def _drain(self, what: str, stream=None):
         import torch

@@ -77,6 +77,26 @@ extern "C" int emu_integrate(int32_t W, int32_t R, int32_t row0, double ox, doub
       PieceCursor cur;
       cur.init(tp);
       if (tp.len < 1 || tp.len > DM_TS) return -101;
+      // k_tile_accum's split walks (walk_tp_split / walk_piece_bytes): the
+      // parts of a piece over f lanes cover its cells once, each part's
+      // cursor starting at the closed-form cell j0
+      for (int32_t f : {2, 3, 4, 5, 7, 16, 21, 64, 128, 256}) {
+        int32_t covered = 0;
+        for (int32_t part = 0; part < f; ++part) {
+          const SplitPart spp = dm_split_part(tp.len, f, part, 1.0f / (float)f);
+          if (spp.n < 0 || (spp.n > 0 && (spp.j0 != covered || spp.j0 + spp.n > tp.len))) return -106;
+          covered += spp.n;
+          if (spp.n == 0) continue;
+          PieceCursor pc;
+          pc.init_at(tp, spp.j0, rtwo_n);
+          if (pc.addr != dm_piece_addr(tp, spp.j0, rtwo_n)) return -107;
+          for (int32_t i = 1; i < spp.n; ++i) {
+            pc.step(tp);
+            if (pc.addr != dm_piece_addr(tp, spp.j0 + i, rtwo_n)) return -107;
+          }
+        }
+        if (covered != tp.len) return -106;
+      }
       for (int st = 0; st < tp.len; ++st, cur.step(tp)) {
         const int32_t k = segs[s].k0 + st;
         int32_t x, yl;

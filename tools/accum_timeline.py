@@ -18,7 +18,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "distributed-autonomous-exploration-and-mapping_amd")
-os.environ["DM_LIB"] = os.path.join(PKG, "dm", "libdm_phase.so")
+os.environ.setdefault("DM_LIB", os.path.join(PKG, "dm", "libdm_phase.so"))
 sys.path.insert(0, PKG)
 
 import numpy as np  # noqa: E402
