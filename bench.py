@@ -396,6 +396,9 @@ def main():
             band.integrate_async(poses_k, pinned[k % len(pool)].data_ptr(), poses_k.shape[0], N, amin, inc)
 
         band.reset()
+        gc.collect()  # as for `value`: no collection inside (or right before) the timed steps
+        gc.freeze()
+        gc.disable()
         run_steps(0, args.warmup, integrate_host)
         barrier()
         torch.cuda.synchronize()
@@ -405,6 +408,8 @@ def main():
         torch.cuda.synchronize()
         barrier()
         el_h = time.perf_counter() - t0
+        gc.enable()
+        gc.unfreeze()
         if world_size > 1:
             t = torch.tensor([el_h], dtype=torch.float64, device=cdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)

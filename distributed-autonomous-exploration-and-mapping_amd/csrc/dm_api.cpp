@@ -501,6 +501,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   if ((rc = dev_alloc(&g->tile_free, g->NT, "tile free counts"))) return fail(rc);
   if ((rc = dev_alloc(&g->fmask, g->NT * DM_TILE * 16, "tile free / unknown bit rows"))) return fail(rc);
   if ((rc = dev_alloc(&g->fedge, g->NT * 4, "tile unknown edge words"))) return fail(rc);
+  if ((rc = dev_alloc(&g->tile_seen, g->NT, "tile seen flags"))) return fail(rc);
   // The five run-time switches (read once, here): DM_SPARSE_PIECES (0: no
   // sparse work items), DM_FMASK=on|off (fmask maintenance forced either way),
   // DM_FRONTIER_KERNEL=wave|wg (one frontier tile kernel for every pass),
@@ -649,7 +650,7 @@ int dm_destroy(dm_grid* g) {
     dev_free(w.heavy_done); dev_free(w.tile_count); dev_free(w.tile_cur); dev_free(w.cnt); dev_free(w.sh);
     dev_free(w.pose4); dev_free(w.ranges);
   }
-  dev_free(g->L); dev_free(g->state); dev_free(g->fmask); dev_free(g->fedge);
+  dev_free(g->L); dev_free(g->state); dev_free(g->fmask); dev_free(g->fedge); dev_free(g->tile_seen);
   dev_free(g->tile_free); dev_free(g->beams); dev_free(g->blk_hist); dev_free(g->blk_n);
   dev_free(g->trig);
   dev_free(g->bs_key); dev_free(g->bs_key2); dev_free(g->bs_idx); dev_free(g->bs_idx2);

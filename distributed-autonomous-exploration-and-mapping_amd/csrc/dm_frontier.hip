@@ -230,6 +230,8 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
     DM_PH_COUNT(dm_phase_acc_frontier, 17, nruns);
     DM_PH_COUNT(dm_phase_acc_frontier, 18, 1);
     // ---- 3. union with overlapping runs of the row above ---------------------
+    // (all rows at once: uniting row blocks level by level, 6 barriers, so
+    // that finds stay short, measured 1.5x slower at C5)
     for (int r = tid; r < nruns; r += kFT) {
       const int y = r_y[r];
       if (y == 0) continue;
@@ -541,23 +543,40 @@ __device__ inline uint32_t unknown_at(const FGeom& g, const int8_t* __restrict__
 // are coalesced: load q, lane l reads the 16-B chunk l % 4 of row 16q + l / 4
 // (16 rows x 64 B per wave instruction), then each lane gathers its row's four
 // chunks with shuffles.
+#ifndef DM_SEEN_HALO
+#define DM_SEEN_HALO 1  // 0: every halo cell loaded (A/B builds)
+#endif
+// unseen (wave-uniform): bit 0 left, 1 right, 2 above, 3 below, 4 above-left,
+// 5 above-right, 6 below-left, 7 below-right neighbour tile exists in this
+// band and is still all unknown (tile_seen 0): its facing cells are unknown
+// without a load (columns past the map's edge excepted).
 __device__ inline void tile_rows(const FGeom& g, const int8_t* __restrict__ state, const int8_t* __restrict__ halo,
-                                 int32_t tx0, int32_t ty0, int lane, uint64_t& U, uint64_t& Fr, uint32_t& uL,
-                                 uint32_t& uR, uint64_t& Ue, uint32_t& eL, uint32_t& eR) {
+                                 int32_t tx0, int32_t ty0, int lane, uint32_t unseen, uint64_t& U, uint64_t& Fr,
+                                 uint32_t& uL, uint32_t& uR, uint64_t& Ue, uint32_t& eL, uint32_t& eR) {
   uint32_t wq[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) wq[q] = chunk_bits(g, state, halo, tx0, ty0 + 16 * q + (lane >> 2), lane & 3);
   // rows -1 (lanes 0-3) and 64 (lanes 4-7), unknown bits only
-  const uint32_t we = lane < 8 ? chunk_bits(g, state, halo, tx0, lane < 4 ? ty0 - 1 : ty0 + DM_TS, lane & 3) : 0u;
+  uint32_t we = 0u;
+  if (lane < 8) {
+    if ((unseen >> (lane < 4 ? 2 : 3)) & 1u) {
+      const int32_t x0 = tx0 + 16 * (lane & 3);  // the in-map columns of the chunk
+      we = x0 >= g.W ? 0u : (x0 + 16 <= g.W ? 0xFFFFu : (1u << (g.W - x0)) - 1u);
+    } else {
+      we = chunk_bits(g, state, halo, tx0, lane < 4 ? ty0 - 1 : ty0 + DM_TS, lane & 3);
+    }
+  }
   // column halos of this lane's row; lanes 0 / 63 also the corners
-  uL = unknown_at(g, state, halo, tx0 - 1, ty0 + lane);
-  uR = unknown_at(g, state, halo, tx0 + DM_TS, ty0 + lane);
+  // (rows past the band's end take the halo row / nothing, as loaded)
+  const bool in_band = ty0 + lane < g.R;
+  uL = ((unseen & 1u) && in_band) ? 1u : unknown_at(g, state, halo, tx0 - 1, ty0 + lane);
+  uR = ((unseen & 2u) && in_band) ? 1u : unknown_at(g, state, halo, tx0 + DM_TS, ty0 + lane);
   eL = 0u;
   eR = 0u;
   if (lane == 0 || lane == 63) {
     const int32_t ey = lane == 0 ? ty0 - 1 : ty0 + DM_TS;
-    eL = unknown_at(g, state, halo, tx0 - 1, ey);
-    eR = unknown_at(g, state, halo, tx0 + DM_TS, ey);
+    eL = ((unseen >> (lane == 0 ? 4 : 6)) & 1u) ? 1u : unknown_at(g, state, halo, tx0 - 1, ey);
+    eR = ((unseen >> (lane == 0 ? 5 : 7)) & 1u) ? 1u : unknown_at(g, state, halo, tx0 + DM_TS, ey);
   }
   U = 0ull;
   Fr = 0ull;
@@ -634,7 +653,7 @@ __device__ inline uint64_t nib_row(uint4 v, int shift) {
 // halo rows instead.  Also copies the list length into the pass's counters.
 __global__ __launch_bounds__(kFW * 64) void k_frontier_bits(
     FGeom g, const int8_t* __restrict__ state, const int8_t* __restrict__ halo, const uint8_t* __restrict__ fmask,
-    const uint64_t* __restrict__ fedge, const int32_t* __restrict__ ftiles,
+    const uint64_t* __restrict__ fedge, const uint8_t* __restrict__ tile_seen, const int32_t* __restrict__ ftiles,
     const unsigned long long* __restrict__ ftiles_n, unsigned long long* list_n, uint64_t* __restrict__ fbits,
     unsigned long long* cnt, int use_fmask, int32_t* __restrict__ big_flag, unsigned long long* fsh,
     int32_t* __restrict__ edge_slot, int64_t n_edge, int32_t* __restrict__ slot_parent,
@@ -669,7 +688,9 @@ __global__ __launch_bounds__(kFW * 64) void k_frontier_bits(
     for (int64_t i = i0; i < g.slot_cap; i += stride) slot_parent[i] = (int32_t)i;
   }
   // four consecutive listed tiles per workgroup: horizontal neighbours share
-  // the 128-byte lines of their rows and halo columns
+  // the 128-byte lines of their rows and halo columns.  (Consecutive chunks
+  // on one XCD, for its L2, cut C3's bytes 28 -> 20 MB per launch but made
+  // this kernel and the step slower: DESIGN.md §3.2)
   for (int64_t jj = (int64_t)blockIdx.x * kFW + w; jj < nft; jj += (int64_t)gridDim.x * kFW) {
     const int32_t tile = __builtin_amdgcn_readfirstlane(ftiles[jj]);
     const int32_t tx = tile % g.TX, ty = tile / g.TX;
@@ -677,7 +698,21 @@ __global__ __launch_bounds__(kFW * 64) void k_frontier_bits(
     uint64_t U, Fr, Ue;
     uint32_t uL, uR, eL, eR;
     if (!use_fmask || (ty == 0 && g.has_before) || (ty == g.TY - 1 && g.has_after)) {
-      tile_rows(g, state, halo, tx0, ty0, lane, U, Fr, uL, uR, Ue, eL, eR);
+      // neighbour tiles of this band that are still all unknown (uniform loads)
+      uint32_t unseen = 0u;
+      if (DM_SEEN_HALO) {
+        const bool l = tx > 0, r = tx + 1 < g.TX, u = ty > 0, d = ty + 1 < g.TY;
+        const int64_t t = tile;
+        if (l && !tile_seen[t - 1]) unseen |= 1u;
+        if (r && !tile_seen[t + 1]) unseen |= 2u;
+        if (u && !tile_seen[t - g.TX]) unseen |= 4u;
+        if (d && !tile_seen[t + g.TX]) unseen |= 8u;
+        if (u && l && !tile_seen[t - g.TX - 1]) unseen |= 16u;
+        if (u && r && !tile_seen[t - g.TX + 1]) unseen |= 32u;
+        if (d && l && !tile_seen[t + g.TX - 1]) unseen |= 64u;
+        if (d && r && !tile_seen[t + g.TX + 1]) unseen |= 128u;
+      }
+      tile_rows(g, state, halo, tx0, ty0, lane, unseen, U, Fr, uL, uR, Ue, eL, eR);
     } else {
       // fmask: [tile][row][16] nibble bytes (free | unknown << 4)
       const uint8_t* rec = fmask + (int64_t)tile * (DM_TS * 16);
@@ -1678,7 +1713,7 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
                       g->ftf_hint <= kDenseMaxTiles);
   dm_timer_begin(g, "frontier_bits", &t);
   DM_LAUNCH(k_frontier_bits, dim3(bits_grid), dim3(kFW * 64), 0, g->stream, fg, g->state, g->halo, g->fmask,
-            g->fedge, g->ftiles, g->ftiles_n, list_n, g->fbits, g->cnt, g->fmask_on ? 1 : 0,
+            g->fedge, g->tile_seen, g->ftiles, g->ftiles_n, list_n, g->fbits, g->cnt, g->fmask_on ? 1 : 0,
             dense ? nullptr : g->big_tiles, g->fsh, g->edge_slot, 2 * g->W, g->slot_parent, g->fe_flag + kHaltWord,
             g->bits_flag + kStampWord);
   dm_timer_end(g, &t);
@@ -1728,6 +1763,8 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
     // one workgroup per listed tile of the last collected pass (+25 %; the
     // kernel grid-strides): thousands of empty workgroups would only keep
     // the dispatcher from the other streams' kernels
+    // (caps of 256-1024 workgroups, to leave the map update more slots,
+    // measured slower: DESIGN.md §3.3.2)
     const int dense_grid = grid_for(std::min<int64_t>(g->NT, g->ftile_hint > 0 ? want_waves : g->NT), 1, 8192);
     DM_LAUNCH(k_frontier_tile_big, dim3(dense_grid), dim3(kFT), 0, ps, fg, g->fbits, nullptr, g->ftiles, list_n,
               g->border, g->rel, g->slot_label, g->slot_parent, g->slot_own, g->slot_acc, g->mask,

@@ -423,6 +423,40 @@ __device__ inline float apply_one(const ApplyArgs& p, float L, uint32_t h, uint3
   return __builtin_amdgcn_fmed3f(L, p.l_min, p.l_max);
 }
 
+// Mask-free forms for the dense apply (CellRows::apply).  gfx950 wants two
+// wait states between a VALU compare that writes a lane mask and the
+// v_cndmask reading it, and the compiler turned the per-cell selects into
+// exec-masked branches (3 scalar instructions + hazard s_nops per cell):
+// the selects below are v_bfi_b32 on masks built by integer arithmetic.
+#ifndef DM_APPLY_BFI
+#define DM_APPLY_BFI 1  // 0: the compare / select form (A/B builds)
+#endif
+// x != 0 ? 0xFFFFFFFF : 0
+__device__ inline uint32_t nz_mask(uint32_t x) {
+  uint32_t r;
+  asm("v_min_u32_e32 %0, 1, %1\n\tv_sub_u32_e32 %0, 0, %0" : "=&v"(r) : "v"(x));
+  return r;
+}
+// (m & a) | (~m & b)
+__device__ inline uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+// SPEC a7 from sign bits of exact differences (L finite, thresholds without
+// signed zeros: make_apply): L >= occ_t <=> L - occ_t >= +0 (a difference of
+// two different floats is never zero, and rounds to -0 at worst when
+// flushed: negative either way), L <= free_t <=> free_t - L >= +0, L == 0
+// <=> |bits| == 0.  Returns the state as an int (-1 / 0 / 100).
+__device__ inline uint32_t state_bits(const ApplyArgs& p, float L) {
+  const int32_t sge = (int32_t)__float_as_uint(L - p.occ_t) >> 31;   // -1: L < occ_t
+  const int32_t sle = (int32_t)__float_as_uint(p.free_t - L) >> 31;  // -1: L > free_t
+  const int32_t mz = (int32_t)((__float_as_uint(L) & 0x7FFFFFFFu) - 1u) >> 31;  // -1: L == 0
+  uint32_t s = bfi((uint32_t)sle, 0xFFFFFFFFu, 0u);   // L > free_t ? -1 : 0
+  s = bfi((uint32_t)sge, s, 100u);                    // L >= occ_t ? 100 : s
+  return s | (uint32_t)mz;                            // L == 0 ? -1
+}
+
 // Bits 0..3: which of the 4 bytes of w are 0 (free); bits 4..7: which are
 // 0xFF (unknown) — a state word's fmask byte.
 __device__ inline uint8_t state_nibbles(uint32_t w) {
@@ -572,7 +606,27 @@ struct CellRows {
 #pragma unroll
         for (int e = 0; e < 4; ++e) dU += tx0 + cx + e < g.r.W ? h4[e] + m4[e] : 0u;
       }
-      if (vec) {
+      if (vec && DM_APPLY_BFI) {
+        // branch- and compare-free per cell: untouched cells keep their values
+        const float lv[4] = {l[rr].x, l[rr].y, l[rr].z, l[rr].w};
+        const uint32_t sw = *reinterpret_cast<const uint32_t*>(&s[rr]);
+        uint32_t nlb[4], nsw = 0u, msk = 0u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t mh = nz_mask(h4[e] | m4[e]);
+          const float nl = apply_one(p, lv[e], h4[e], m4[e]);
+          nlb[e] = bfi(mh, __float_as_uint(nl), __float_as_uint(lv[e]));
+          nsw |= (state_bits(p, nl) & 0xFFu) << (8 * e);
+          msk |= (mh & 0xFFu) << (8 * e);
+          dT += (int32_t)(mh & 1u);
+        }
+        const uint32_t ns = bfi(msk, nsw, sw);
+        dFree += zero_bytes(ns) - zero_bytes(sw);
+        *reinterpret_cast<float4*>(L + base) =
+            make_float4(__uint_as_float(nlb[0]), __uint_as_float(nlb[1]), __uint_as_float(nlb[2]),
+                        __uint_as_float(nlb[3]));
+        *reinterpret_cast<uint32_t*>(state + base) = ns;
+      } else if (vec) {
         // branch-free per cell: untouched cells keep their values
         float lv[4] = {l[rr].x, l[rr].y, l[rr].z, l[rr].w};
         int8_t sv[4] = {(int8_t)s[rr].x, (int8_t)s[rr].y, (int8_t)s[rr].z, (int8_t)s[rr].w};
@@ -848,7 +902,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
     uint32_t* __restrict__ slabs, float* __restrict__ L, int8_t* __restrict__ state,
     const unsigned long long* __restrict__ cnt, unsigned long long* ish, int vec_ok,
     const int32_t* __restrict__ heavy_list, int32_t* heavy_done, int32_t* tlist, unsigned long long* tlist_n,
-    unsigned long long* hint, const unsigned long long* __restrict__ halt) {
+    unsigned long long* hint, const unsigned long long* __restrict__ halt, uint8_t* __restrict__ tile_seen) {
   __shared__ uint32_t tl[kTileWords + 64];  // + one spare word per lane (walk_tp_split)
   __shared__ int32_t s_T, s_free, s_last;
   __shared__ uint32_t s_U;
@@ -1004,6 +1058,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
         if (tid == 0) {
           finish_tile(g, tile, s_T, s_free, s_U, true, tile_count, tile_free, old_free, tlist, tlist_n, ish);
           heavy_done[h] = 0;  // ready for the next call
+          tile_seen[tile] = 1;
         }
 #ifdef DM_PHASE_TIMING
         tl_word += (unsigned long long)(wall_clock64() - tf0) << 32;
@@ -1055,6 +1110,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
       s_accU += (unsigned long long)s_U;
       if (s_free) tile_free[tile] = free_update(tfree, s_free, tile, tlist, tlist_n);
       tile_count[tile] = 0;  // ready for the next call
+      tile_seen[tile] = 1;
     }
     // the next item: its pieces go out now (or went out after the walk),
     // ahead of its walk
@@ -1177,6 +1233,7 @@ __global__ __launch_bounds__(kQuarter, kAccumPerCu) void k_tile_accum(
       atomicAdd(&s_accU, (unsigned long long)U);
       if (df) tile_free[tile] = free_update(sfree, df, tile, tlist, tlist_n);
       tile_count[tile] = 0;  // ready for the next call
+      tile_seen[tile] = 1;
       s_wT[wv] = 0;
       s_wfree[wv] = 0;
       s_wU[wv] = 0u;
@@ -1256,20 +1313,21 @@ __device__ inline uint8_t fmask_byte(uint64_t fm, uint64_t um, int j) {
 // is cell (e & 63, e >> 6): a wave is one row.
 __global__ __launch_bounds__(256) void k_recount(Geom g, const int8_t* __restrict__ state,
                                                  int32_t* __restrict__ tile_free, uint8_t* __restrict__ fmask,
-                                                 uint64_t* __restrict__ fedge) {
+                                                 uint64_t* __restrict__ fedge, uint8_t* __restrict__ tile_seen) {
   const int64_t tile = blockIdx.x;
   const int32_t tx0 = (int32_t)(tile % g.r.TX) * DM_TS, ty0 = (int32_t)(tile / g.r.TX) * DM_TS;
-  __shared__ int32_t acc;
+  __shared__ int32_t acc, seen;
   __shared__ uint64_t s_edge[4][4];  // per wave: unknown column 0, column 63, row 0, row 63
-  if (threadIdx.x == 0) acc = 0;
+  if (threadIdx.x == 0) { acc = 0; seen = 0; }
   __syncthreads();
-  int32_t c = 0;
+  int32_t c = 0, known = 0;
   uint64_t ew[4] = {0ull, 0ull, 0ull, 0ull};
   uint8_t* tm = fmask + tile * (DM_TS * 16);
   for (int e = threadIdx.x; e < DM_TS * DM_TS; e += 256) {
     const int32_t x = tx0 + (e & 63), y = ty0 + (e >> 6);
     const int8_t b = (x < g.r.W && y < g.r.R) ? state[(int64_t)y * g.r.W + x] : (int8_t)1;
     c += b == 0;
+    known |= (x < g.r.W && y < g.r.R && b != -1) ? 1 : 0;
     const uint64_t fm = __ballot(b == 0);
     const uint64_t um = __ballot(b == -1);
     const int l = e & 63, r = e >> 6;  // a wave is one row
@@ -1280,10 +1338,14 @@ __global__ __launch_bounds__(256) void k_recount(Geom g, const int8_t* __restric
     if (r == DM_TS - 1) ew[3] = um;
   }
   if (c) atomicAdd(&acc, c);
+  if (known) seen = 1;
   const int l4 = __lane_id();
   if (l4 < 4) s_edge[threadIdx.x >> 6][l4] = l4 == 0 ? ew[0] : l4 == 1 ? ew[1] : l4 == 2 ? ew[2] : ew[3];
   __syncthreads();
-  if (threadIdx.x == 0) tile_free[tile] = acc;
+  if (threadIdx.x == 0) {
+    tile_free[tile] = acc;
+    tile_seen[tile] = (uint8_t)seen;
+  }
   if (threadIdx.x < 4)
     fedge[tile * 4 + threadIdx.x] = s_edge[0][threadIdx.x] | s_edge[1][threadIdx.x] | s_edge[2][threadIdx.x] |
                                     s_edge[3][threadIdx.x];
@@ -1484,8 +1546,9 @@ ApplyArgs make_apply(const dm_grid* g) {
   // same result for a bound of -0 or +0 (L is never -0), v_med3 only for +0
   a.l_min = g->p.l_min == 0.0f ? 0.0f : g->p.l_min;
   a.l_max = g->p.l_max == 0.0f ? 0.0f : g->p.l_max;
-  a.occ_t = g->p.occ_thresh;
-  a.free_t = g->p.free_thresh;
+  // thresholds without signed zeros either (state_bits: sign-bit compares)
+  a.occ_t = g->p.occ_thresh == 0.0f ? 0.0f : g->p.occ_thresh;
+  a.free_t = g->p.free_thresh == 0.0f ? 0.0f : g->p.free_thresh;
   return a;
 }
 
@@ -1589,7 +1652,8 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
                      dim3(kQuarter), 0,
                      g->stream, ge, make_apply(g), w.hitems, (int)CNT_ITEMS, w.litems, (int)CNT_LITEMS,
                      (int)CNT_SITEMS, w.pieces, w.tile_count, g->tile_free, w.slabs, g->L, g->state, w.cnt, w.sh, vec_ok,
-                     w.heavy_list, w.heavy_done, g->ftiles, g->ftiles_n, g->d_hint, g->fe_flag + kHaltWord);
+                     w.heavy_list, w.heavy_done, g->ftiles, g->ftiles_n, g->d_hint, g->fe_flag + kHaltWord,
+                     g->tile_seen);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (g->overlap) w.free_owed = true;
@@ -1659,7 +1723,7 @@ int dm_launch_recount(dm_grid* g) {
   // fmask switch-on inside dm_enqueue_frontiers may not have)
   DM_HIP(dm_join_pass_stream(g));
   DM_LAUNCH(k_recount, dim3((unsigned)g->NT), dim3(256), 0, g->stream, ge, g->state,
-                     g->tile_free, g->fmask, g->fedge);
+                     g->tile_free, g->fmask, g->fedge, g->tile_seen);
   DM_HIP(hipGetLastError());
   if (int rc = dm_launch_relist(g, false)) return rc;
   g->fmask_valid = true;

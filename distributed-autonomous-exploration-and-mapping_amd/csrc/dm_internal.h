@@ -232,6 +232,13 @@ struct dm_grid {
   // same kernels: a pass reads its neighbours' edges from these 32 B instead
   // of from their 1 KB records (one byte of every 16 B row: all 8 lines)
   uint64_t* fedge = nullptr;
+  // tile_seen: 0 while every cell of the tile is still unknown (since the
+  // last bulk write: k_recount sets it from the state), 1 once an
+  // integrate item applied the tile (k_tile_accum).  The frontier bit rows
+  // take an unseen neighbour's facing cells as unknown without reading them:
+  // the explored region's borders face unseen tiles, whose halo column would
+  // otherwise cost a 64-byte line per row.
+  uint8_t* tile_seen = nullptr;
   bool fmask_on = false, fmask_valid = false;
   int fmask_mode = 0;  // DM_FMASK=auto|on|off (read at dm_create; tests / A/B): 0 auto, 1 on, 2 off
   unsigned long long* cnt = nullptr;    // CNT_N device counters (frontier fields)
