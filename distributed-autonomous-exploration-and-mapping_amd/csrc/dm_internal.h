@@ -237,7 +237,7 @@ struct dm_grid {
   // integrate item applied the tile (k_tile_accum).  The frontier bit rows
   // take an unseen neighbour's facing cells as unknown without reading them:
   // the explored region's borders face unseen tiles, whose halo column would
-  // otherwise cost a 64-byte line per row.
+  // otherwise cost a 128-byte line per row.
   uint8_t* tile_seen = nullptr;
   bool fmask_on = false, fmask_valid = false;
   int fmask_mode = 0;  // DM_FMASK=auto|on|off (read at dm_create; tests / A/B): 0 auto, 1 on, 2 off
