@@ -9,17 +9,19 @@ the global map, rows_r a multiple of 64 except for the last band.
   cell writes are disjoint and the union of the bands equals a 1-GPU map
   bit for bit (tests/test_sharded.py).
 * Frontier extraction has the only real exchange steps.  On GPUs they are
-  device-resident (one host synchronisation per call, as on one GPU): edge
-  rows are gathered with RCCL straight into the neighbours' halos, every band
+  device-resident (one host synchronisation per call, as on one GPU): each
+  band's first / last rows go to its two neighbours only, received straight
+  into their halos (one batched RCCL send / receive; 2 W bytes each way,
+  exchange_neighbour_rows), every band
   writes an export record (include/dm.h: its edge components as indices into
   its sorted cluster list, and the clusters), the records are all-gathered
   with RCCL and every rank merges them with libdm's merge kernels
   (dm_merge_bands, csrc/dm_merge.hip).  The host path below is the
   restatement the CPU tests run (and the fallback when a band's record
   overflows its capacity):
-  1. halo rows: each band's first/last state rows are all-gathered (W bytes
-     per edge) and installed as the neighbours' halos, so the 8-neighbour
-     frontier test sees across band edges;
+  1. halo rows: each band's first/last state rows are sent to the
+     neighbouring bands (W bytes per edge) and installed as their halos, so
+     the 8-neighbour frontier test sees across band edges;
   2. label merge: each band's first/last-row labels (band-local min-index
      labels, int64) are all-gathered; every rank forms the cross-edge
      equivalence pairs (8-connectivity: x-1, x, x+1) and resolves them with
@@ -67,6 +69,23 @@ def group_ranks(dist, group=None) -> list[int]:
     if group is None or group is dist.group.WORLD:
         return list(range(dist.get_world_size()))
     return [int(r) for r in dist.get_process_group_ranks(group)]
+
+
+def exchange_neighbour_rows(dist, group, peers, rank: int, world_size: int, first, last, before, after):
+    """Post the band-edge exchange with the two neighbour bands only (SURVEY.md
+    §8(e)): `first` (this band's first row) goes to rank - 1 and `last` to
+    rank + 1; `before` receives rank - 1's last row and `after` rank + 1's
+    first row (None at the map's top / bottom band).  `peers`: the group's
+    global ranks.  Returns the works to wait for (one batched RCCL launch, or
+    gloo's per-op requests)."""
+    ops = []
+    if rank > 0:
+        ops.append(dist.P2POp(dist.isend, first, peers[rank - 1], group))
+        ops.append(dist.P2POp(dist.irecv, before, peers[rank - 1], group))
+    if rank + 1 < world_size:
+        ops.append(dist.P2POp(dist.isend, last, peers[rank + 1], group))
+        ops.append(dist.P2POp(dist.irecv, after, peers[rank + 1], group))
+    return dist.batch_isend_irecv(ops) if ops else []
 
 
 def band_params(params: DmParams, world_size: int, rank: int) -> DmParams:
@@ -171,7 +190,7 @@ class ShardedMapper:
         """`timeout`: seconds any collective (or the device work queued behind
         one) may take before this rank gives up with DM_ERR_COLLECTIVE.
         `force_exchange`: with world_size 1, run the multi-rank exchange
-        anyway (halo gather, export record, records gather, device merge)
+        anyway (halo exchange, export record, records gather, device merge)
         over `group` (a 1-rank process group): the RCCL path on one GPU."""
         self.params = DmParams.from_buffer_copy(params)
         self.rank, self.world_size, self.group = rank, world_size, group
@@ -198,6 +217,7 @@ class ShardedMapper:
 
             self._dist = dist
             self._nccl = dist.get_backend(group) == "nccl"
+            self._group_ranks = group_ranks(dist, group)
             if self._nccl:
                 import torch
 
@@ -210,7 +230,7 @@ class ShardedMapper:
                 self._torch = torch
                 self._tdev = torch.device("cuda", device)
                 # the band's map stream: its map kernels and the halo-row
-                # all-gather between them (RCCL orders itself against it)
+                # exchange between them (RCCL orders itself against it)
                 # (high priority, as libdm's own map stream: the front-end
                 # stream fills what the map chain leaves idle)
                 self.stream = torch.cuda.Stream(device=self._tdev, priority=-1)
@@ -218,13 +238,13 @@ class ShardedMapper:
                 # the export records are all-gathered on the band's exchange
                 # stream (its pass stream with overlap on), over a second
                 # communicator: a records gather that waits for a pass's
-                # labelling then never holds up the next pass's halo gather
+                # labelling then never holds up the next pass's halo exchange
                 # on the map stream (one communicator runs its collectives
                 # in issue order).  Built over the mapper's own group's
                 # ranks (a subgroup's ranks are not 0..P-1 globally);
                 # new_group is collective over the default group, so every
                 # process of it constructs its mappers in the same order.
-                self.rec_group = dist.new_group(group_ranks(dist, group))
+                self.rec_group = dist.new_group(self._group_ranks)
                 self._xstreams = {}
                 # records per band export: sized for the band up front (a
                 # cluster per tile: C5's 4096-beam fans reach 0.81), then to
@@ -333,11 +353,22 @@ class ShardedMapper:
         return out.cpu().numpy().reshape((self.world_size,) + arr.shape)
 
     def exchange_halos(self):
-        first, last = self.band.edge_rows()
-        rows = self._allgather(np.stack([first, last]))
-        before = rows[self.rank - 1, 1] if self.rank > 0 else None
-        after = rows[self.rank + 1, 0] if self.rank + 1 < self.world_size else None
-        self.band.set_halo(before, after)
+        """Host path: the halo rows from the two neighbour bands
+        (exchange_neighbour_rows), set on the band."""
+        import torch
+
+        first, last = (torch.from_numpy(np.ascontiguousarray(a, np.int8)) for a in self.band.edge_rows())
+        dev = self._device if self._nccl else None
+        if dev is not None:
+            first, last = first.to(dev), last.to(dev)
+        W, r, P = first.numel(), self.rank, self.world_size
+        before = torch.empty(W, dtype=torch.int8, device=dev) if r > 0 else None
+        after = torch.empty(W, dtype=torch.int8, device=dev) if r + 1 < P else None
+        self._exchange_rows(first, last, before, after)
+        if dev is not None:
+            self._drain("halo exchange", torch.cuda.current_stream(dev))
+        self.band.set_halo(None if before is None else before.cpu().numpy(),
+                           None if after is None else after.cpu().numpy())
 
     # -- device-resident exchange (RCCL + dm_merge_bands) -------------------
     def _buf(self, name, n, dtype):
@@ -361,6 +392,40 @@ class ShardedMapper:
             self._all_gather(o, t.cpu(), "all-gather", group)
             out.copy_(o)
 
+    def _halo_dev(self, rows):
+        """The band's halo rows from its two neighbours only, ordered on the
+        current stream (exchange_neighbour_rows: 2 W bytes each way instead of
+        an all-gather of every band's 2 W).  Returns the (before, after)
+        device rows, None at the map's top / bottom band."""
+        torch = self._torch
+        W, P, r = self.W, self.world_size, self.rank
+        before = self._buf("halo_before", W, torch.int8) if r > 0 else None
+        after = self._buf("halo_after", W, torch.int8) if r + 1 < P else None
+        if before is None and after is None:
+            return None, None
+        first, last = rows[:W], rows[W:]
+        if self._nccl:
+            dst = (before, after)
+        else:  # gloo (the on-GPU rehearsal) exchanges host copies
+            first, last = first.cpu(), last.cpu()
+            dst = tuple(None if b is None else torch.empty(W, dtype=torch.int8) for b in (before, after))
+        self._exchange_rows(first, last, *dst)
+        if not self._nccl:
+            for b, h in zip((before, after), dst):
+                if b is not None:
+                    b.copy_(h)
+        return before, after
+
+    def _exchange_rows(self, first, last, before, after):
+        self._check()
+        try:
+            works = exchange_neighbour_rows(self._dist, self.group, self._group_ranks, self.rank,
+                                            self.world_size, first, last, before, after)
+        except Exception as e:
+            self._fail(f"halo exchange failed: {e}")
+        for w in works:
+            self._wait(w, "halo exchange")
+
     def _xstream(self):
         """The band's exchange stream (dm_exchange_stream) as a torch stream."""
         ptr = self.band.exchange_stream()
@@ -373,19 +438,17 @@ class ShardedMapper:
         return xs
 
     def _device_enqueue(self):
-        """Halo all-gather (map stream), band frontiers + export record, and
+        """Neighbour halo exchange (map stream), band frontiers + export record, and
         the records' all-gather on the band's exchange stream (no host wait).
         Returns the gathered buffer and the exchange stream the merge runs on."""
         torch = self._torch
         W, P, r = self.W, self.world_size, self.rank
         with torch.cuda.stream(self.stream):
             rows = self._buf("rows", 2 * W, torch.int8)
-            grows = self._buf("grows", P * 2 * W, torch.int8)
             self.band.edge_rows_device(rows.data_ptr(), rows.data_ptr() + W)
-            self._gather_dev(rows, grows)
-            g0 = grows.data_ptr()
-            self.band.set_halo_device(g0 + (r - 1) * 2 * W + W if r > 0 else None,
-                                      g0 + (r + 1) * 2 * W if r + 1 < P else None)
+            before, after = self._halo_dev(rows)
+            self.band.set_halo_device(before.data_ptr() if before is not None else None,
+                                      after.data_ptr() if after is not None else None)
             nb = self.band.export_bytes(self.rec_cap)
             exp = self._buf("exp", nb, torch.uint8)
             gexp = self._buf("gexp", P * nb, torch.uint8)
@@ -517,5 +580,5 @@ class ShardedMapper:
         self.band.close()
 
 
-__all__ = ["ShardedMapper", "band_rows", "band_params", "merge_clusters", "relabel",
+__all__ = ["ShardedMapper", "band_rows", "band_params", "exchange_neighbour_rows", "merge_clusters", "relabel",
            "resolve_labels"]

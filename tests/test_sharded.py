@@ -225,3 +225,46 @@ def test_band_partition_matches_libdm():
             for r in range(P):
                 assert lib.dm_sharded_band_rows(H, P, r, ctypes.byref(r0), ctypes.byref(n)) == 0
                 assert (r0.value, n.value) == band_rows(H, P, r)
+
+
+def _halo_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "distributed-autonomous-exploration-and-mapping_amd"))
+    import torch
+    import torch.distributed as dist
+
+    from dm.sharded import exchange_neighbour_rows
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    W = 37
+    first = torch.full((W,), 10 * rank, dtype=torch.int8)
+    last = torch.full((W,), 10 * rank + 1, dtype=torch.int8)
+    before = torch.full((W,), -7, dtype=torch.int8) if rank > 0 else None
+    after = torch.full((W,), -7, dtype=torch.int8) if rank + 1 < world else None
+    for w in exchange_neighbour_rows(dist, dist.group.WORLD, list(range(world)), rank, world, first, last,
+                                     before, after):
+        w.wait()
+    out[rank] = (None if before is None else before.tolist(), None if after is None else after.tolist())
+    dist.destroy_process_group()
+
+
+def test_neighbour_halo_exchange():
+    """each band gets only its neighbours' facing rows — the
+    row before it is band r-1's last row, the row after it band r+1's first
+    row; the top and bottom bands have one neighbour (4 gloo ranks)."""
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    port = _free_port()
+    world = 4
+    procs = [ctx.Process(target=_halo_worker, args=(r, world, port, out)) for r in range(world)]
+    for q in procs:
+        q.start()
+    for q in procs:
+        q.join(120)
+        assert q.exitcode == 0
+    for r in range(world):
+        before, after = out[r]
+        assert before == (None if r == 0 else [10 * (r - 1) + 1] * 37)
+        assert after == (None if r == world - 1 else [10 * (r + 1)] * 37)
