@@ -15,8 +15,8 @@ frontier pass.  --no-overlap runs the steps back to back.
 N GPUs (weak scaling): rank r owns a 16384-row band of a 16384 x 16384*N map
 with its own 64 robots anywhere in the band (plus the neighbours' scans that
 reach across the band edge); frontiers are merged across bands on the device
-(RCCL all-gather of halo rows and export records, dm_merge_bands;
-dm/sharded.py).
+(halo rows sent to the two neighbour bands, RCCL all-gather of export
+records, dm_merge_bands; dm/sharded.py).
 
 Prints ONE JSON line on rank 0.  See DESIGN.md §5 for every field.
 """
