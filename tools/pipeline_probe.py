@@ -1,7 +1,7 @@
 """Host-side timing of the pipelined bench loop (C3, one GPU): per step, the
 wall time spent in the integrate call, in frontiers_end (waiting for the
 previous pass + copying its clusters) and in frontiers_begin (enqueueing the
-pass).  Diagnostic only."""
+pass).  Diagnostic only.  usage: python tools/pipeline_probe.py [c5 N]"""
 import os
 import sys
 import time
@@ -18,6 +18,8 @@ from dm import synth  # noqa: E402
 
 def main():
     G, res, S, N = 16384, 0.05, 64, 4096
+    if len(sys.argv) > 1 and sys.argv[1] == "c5":  # "c5 N": 65536^2 @ 1 cm, 64 robots x N beams
+        G, res, N = 65536, 0.01, int(sys.argv[2]) if len(sys.argv) > 2 else 48
     half = G * res / 2
     world = synth.make_world(0, -half, -half, half, half)
     st = synth.ScanStream(world, S, N, 500, region=(-half + 1, -half + 1, half - 1, half - 1))
