@@ -585,6 +585,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
 #ifndef DM_PRIO_PASS
 #define DM_PRIO_PASS 1
 #endif
+
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   e = hipStreamCreateWithPriority(&g->stream, hipStreamNonBlocking, DM_PRIO_GRID ? prio_hi : prio_lo);
@@ -613,6 +614,7 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
     e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
   }
+
   if ((rc = dm_reset(g))) return fail(rc);
   *out = g;
   return DM_OK;
@@ -705,7 +707,8 @@ namespace {
 
 // Host inputs -> device: poses to (x, y, cos yaw, sin yaw) with the C
 // library (as the oracle) into the next pinned staging buffer of the ring,
-// then both H2D copies on the front-end stream, then the integrate launch.
+// then the ranges H2D copy on the front-end stream (k_beam_prep reads the
+// poses from the mapped staging buffer), then the integrate launch.
 // Nothing here waits for the device except a staging buffer whose copy (two
 // calls ago) has not finished yet.
 int enqueue_host_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N, const float* ranges,
@@ -716,10 +719,12 @@ int enqueue_host_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N
   if ((rc = ensure_trig(g, N, angle_min, angle_increment))) return rc;
   const int64_t nb = (int64_t)S * N;
   hipStream_t fs = g->overlap ? g->fe_stream : g->stream;
-  // the copies go to the device buffers of the workspace set this call will
-  // use (dm_launch_integrate alternates them); with overlap the front-end
+  // the ranges copy goes to the device buffer of the workspace set this call
+  // will use (dm_launch_integrate alternates them); with overlap the front-end
   // stream first waits until that set is free (its last accumulation, which
-  // may read its inputs, is done)
+  // may read its inputs, is done).  The copy stays at the head of this call's
+  // front-end: on a stream of its own (waiting for the set, the front-end
+  // waiting for it) host-input steps took 1.6x as long.
   dm_grid::IntWs& w = g->iw[(g->iw_cur + 1) % dm_grid::kIntSets];
   if (g->overlap) {
     DM_HIP(dm_mark_ws_free(g));
@@ -743,14 +748,16 @@ int enqueue_host_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N
       g->h_pose4[i] = nullptr;
     }
     g->h_pose_cap = 0;
-    for (int i = 0; i < dm_grid::kPoseRing; ++i)
+    for (int i = 0; i < dm_grid::kPoseRing; ++i) {
       DM_HIP(hipHostMalloc((void**)&g->h_pose4[i], sizeof(double) * 4 * (size_t)std::max(S, 1),
-                           hipHostMallocDefault));
+                           hipHostMallocMapped));
+      DM_HIP(hipHostGetDevicePointer((void**)&g->h_pose4_dev[i], g->h_pose4[i], 0));
+    }
     g->h_pose_cap = (int64_t)std::max(S, 1) * 4;
   }
   const int slot = g->pose_head;
   g->pose_head = (g->pose_head + 1) % dm_grid::kPoseRing;
-  DM_HIP(hipEventSynchronize(g->ev_pose[slot]));  // its copy (two calls ago) is done
+  DM_HIP(hipEventSynchronize(g->ev_pose[slot]));  // its last reader (two calls ago) is done
   double* hp = g->h_pose4[slot];
   for (int32_t s = 0; s < S; ++s) {
     const double x = poses[3 * s], y = poses[3 * s + 1], yaw = poses[3 * s + 2];
@@ -760,15 +767,23 @@ int enqueue_host_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N
     hp[4 * s + 3] = sin(yaw);
   }
   // into the set's buffers: their last readers (the front-end of the set's
-  // previous call, on fs) are done (above)
-  if (S > 0)
+  // previous call, on fs) are done (above: that front-end precedes the set's
+  // last accumulation).  DM_HOST_POSE: no pose copy, k_beam_prep reads the
+  // mapped staging buffer (a 2 KB copy is a blit kernel, which waits for the
+  // accumulation's CUs and adds a compute -> copy-engine hand-off)
+  const double* d_pose = w.pose4;
+  if (DM_HOST_POSE) {
+    d_pose = g->h_pose4_dev[slot];
+  } else if (S > 0) {
     DM_HIP(hipMemcpyAsync(w.pose4, hp, sizeof(double) * 4 * (size_t)S, hipMemcpyHostToDevice, fs));
+  }
   if (nb > 0)
     DM_HIP(hipMemcpyAsync(w.ranges, ranges, sizeof(float) * (size_t)nb, hipMemcpyHostToDevice, fs));
-  // after BOTH copies: two calls later this event proves the caller's ranges
+  if ((rc = dm_launch_integrate(g, S, d_pose, N, w.ranges, g->trig))) return rc;
+  // after the front-end (which read the staging buffer) and so after the
+  // ranges copy: two calls later this event proves the caller's ranges
   // buffer has been read too (dm.h: reusable after the second call that follows)
   DM_HIP(hipEventRecord(g->ev_pose[slot], fs));
-  if ((rc = dm_launch_integrate(g, S, w.pose4, N, w.ranges, g->trig))) return rc;
   g->last_S = S;
   g->last_N = N;
   g->frontier_valid = false;

@@ -288,12 +288,17 @@ struct dm_grid {
   int iw_cur = 0;                // set of the last integrate call
   double* trig = nullptr; int32_t trig_n = -1; float trig_amin = 0, trig_inc = 0;
   int64_t trig_cap = 0;
-  // pinned (x, y, cos, sin) staging of host poses: a ring of two, each
-  // reusable once the H2D copy that read it is done (ev_pose), so a host-input
-  // call never waits for the previous call (dm_integrate_async)
+  // pinned, mapped (x, y, cos, sin) staging of host poses: a ring of two, each
+  // reusable once the front-end that read it (k_beam_prep, through the device
+  // address) is done (ev_pose), so a host-input call never waits for the
+  // previous call (dm_integrate_async)
   static constexpr int kPoseRing = 2;
   double* h_pose4[kPoseRing] = {nullptr, nullptr};
   hipEvent_t ev_pose[kPoseRing] = {nullptr, nullptr};
+  double* h_pose4_dev[kPoseRing] = {nullptr, nullptr};  // their device addresses (mapped)
+#ifndef DM_HOST_POSE
+#define DM_HOST_POSE 1  // 0: poses copied to the device like the ranges (A/B builds)
+#endif
   int64_t h_pose_cap = 0;
   int pose_head = 0;
   int32_t last_S = 0, last_N = 0;
