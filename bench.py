@@ -385,8 +385,8 @@ def main():
                                     t_fr)
 
     # PCIe-inclusive rate: the same pipelined steps fed from pinned host
-    # buffers through dm_integrate_async (H2D of ranges + poses on the
-    # library's front-end stream, overlapped with the previous frontier pass)
+    # buffers through dm_integrate_async (H2D of the ranges on the library's
+    # front-end stream, poses read from its mapped staging ring)
     host_inputs = None
     if not args.no_host_inputs:
         pinned = [torch.from_numpy(np.ascontiguousarray(r, np.float32)).pin_memory() for _, r in pool]
