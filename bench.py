@@ -15,8 +15,9 @@ frontier pass.  --no-overlap runs the steps back to back.
 N GPUs (weak scaling): rank r owns a 16384-row band of a 16384 x 16384*N map
 with its own 64 robots anywhere in the band (plus the neighbours' scans that
 reach across the band edge); frontiers are merged across bands on the device
-(halo rows sent to the two neighbour bands, RCCL all-gather of export
-records, dm_merge_bands; dm/sharded.py).
+(halo rows sent to the two neighbour bands with one batched RCCL send /
+receive, RCCL all-gather of the export records over the same communicator,
+dm_merge_bands; dm/sharded.py).
 
 Prints ONE JSON line on rank 0.  See DESIGN.md §5 for every field.
 """
@@ -60,6 +61,9 @@ def parse():
                     help="run the steps back to back without overlapping step k+1's integrate "
                          "front-end with step k's frontier pass")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1")
+    ap.add_argument("--records-comm", default="shared", choices=["shared", "separate"],
+                    help="N>1: all-gather the export records over the halo exchange's communicator "
+                         "(shared, default) or over a second one (separate; dm/sharded.py)")
     ap.add_argument("--collective-timeout", type=float, default=300.0,
                     help="N>1: seconds a collective may take before the job fails (DM_ERR_COLLECTIVE)")
     ap.add_argument("--device-override", type=int, default=None,
@@ -216,7 +220,7 @@ def main():
     params.origin_y = oy_global
     mapper = ShardedMapper(params, rank=rank, world_size=world_size, device=local_rank,
                            group=dist.group.WORLD if world_size > 1 else None,
-                           timeout=args.collective_timeout)
+                           timeout=args.collective_timeout, records_comm=args.records_comm)
     band = mapper.band
     S, N = args.robots, args.beams
 
@@ -364,11 +368,38 @@ def main():
     # live per-kernel timing with HIP events on the library's stream
     band.profile(True)
     band.profile_reset()
+    if world_size > 1:
+        mapper.set_timing(True)
     for k in range(args.profile_steps):
         step(k)
     kstats = band.profile_read()
     band.profile(False)
     avg = {name: tot / max(1, n) for name, (n, tot) in kstats.items()}
+    if world_size > 1:
+        # every rank's exchange phases per pass (ms, HIP events): halo
+        # send / receive with the two neighbour bands, the band's export, the
+        # records all-gather, the merge of all P records
+        xt = mapper.exchange_times()
+        mapper.set_timing(False)
+        ph = [xt["halo_ms"], avg.get("export"), xt["records_gather_ms"], avg.get("merge")]
+        t = torch.zeros((world_size, 4), dtype=torch.float64, device=cdev)
+        t[rank] = torch.tensor([float("nan") if v is None else float(v) for v in ph], dtype=torch.float64)
+        dist.all_reduce(t)
+        per = t.cpu().numpy()
+        nb = band.export_bytes(mapper.rec_cap)
+        ranks_info["exchange_ms_per_pass"] = {
+            "halo": [float(x) for x in per[:, 0]], "export": [float(x) for x in per[:, 1]],
+            "records_gather": [float(x) for x in per[:, 2]], "merge": [float(x) for x in per[:, 3]],
+            "passes_timed": int(xt["passes"]),
+            "how": "HIP events: halo = map stream reaching the neighbour send / receive to its "
+                   "completion; records_gather = this band's export record written to the all-gather's "
+                   "completion; export / merge = libdm's kernel timers (dm_profile)"}
+        ranks_info["exchange_bytes_per_pass"] = {
+            "halo_row_bytes": G, "halo_sent_per_interior_rank": 2 * G,
+            "records_gathered_per_rank": world_size * nb, "record_bytes": nb, "rec_cap": mapper.rec_cap,
+            "model": "halo: W B to each neighbour band; records: P x (64 + 8 W + 32 rec_cap) B "
+                     "(include/dm.h export record)"}
+        ranks_info["records_comm"] = mapper.records_comm
     dominant = max(kstats, key=lambda n: kstats[n][1]) if kstats else None
     # roofline of the dominant integrate kernel, k_tile_accum: it performs
     # every update (8 B each) and applies every touched cell (25 B each),
@@ -505,8 +536,10 @@ def main():
             "frontier_explored": explored,
             "stage_stats": {k: float(np.mean([st[k] for st in stats])) for k in stats[0]},
             "scans_per_rank_batch": float(np.mean([p.shape[0] for p, _ in pool])),
-            "exchange": ("device: RCCL all-gather of halo rows + export records, dm_merge_bands"
-                         if world_size > 1 else None),
+            "exchange": (f"device: halo rows sent to / received from the two neighbour bands (batched "
+                         f"{'RCCL' if args.backend == 'nccl' else args.backend} send / receive), export "
+                         f"records all-gathered ({args.records_comm} communicator), dm_merge_bands on "
+                         f"every rank" if world_size > 1 else None),
             "exchange_fallbacks": (sum(ranks_info["exchange_fallbacks"]) if ranks_info
                                    else getattr(mapper, "fallbacks", 0)),
             # N > 1: the world size the process group reports, the launcher,

@@ -749,8 +749,13 @@ int enqueue_host_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N
     }
     g->h_pose_cap = 0;
     for (int i = 0; i < dm_grid::kPoseRing; ++i) {
+      // Coherent: k_beam_prep reads the slot through its device address and
+      // the slot is rewritten every kPoseRing calls at the same address, so
+      // the GPU must not keep it in L2 (non-coherent host memory may be
+      // cached there; the other mapped buffers the device reads are
+      // Mapped | Coherent too)
       DM_HIP(hipHostMalloc((void**)&g->h_pose4[i], sizeof(double) * 4 * (size_t)std::max(S, 1),
-                           hipHostMallocMapped));
+                           hipHostMallocMapped | hipHostMallocCoherent));
       DM_HIP(hipHostGetDevicePointer((void**)&g->h_pose4_dev[i], g->h_pose4[i], 0));
     }
     g->h_pose_cap = (int64_t)std::max(S, 1) * 4;

@@ -698,7 +698,9 @@ __global__ __launch_bounds__(kFW * 64) void k_frontier_bits(
     uint64_t U, Fr, Ue;
     uint32_t uL, uR, eL, eR;
     if (!use_fmask || (ty == 0 && g.has_before) || (ty == g.TY - 1 && g.has_after)) {
-      // neighbour tiles of this band that are still all unknown (uniform loads)
+      // neighbour tiles of this band that are still all unknown (uniform loads);
+      // relies on the tile_seen invariant of dm_internal.h (every state writer
+      // sets the flag or is followed by k_recount)
       uint32_t unseen = 0u;
       if (DM_SEEN_HALO) {
         const bool l = tx > 0, r = tx + 1 < g.TX, u = ty > 0, d = ty + 1 < g.TY;

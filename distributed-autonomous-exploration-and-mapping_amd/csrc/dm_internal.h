@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <chrono>
 #include <string>
 #include <vector>
@@ -238,6 +239,13 @@ struct dm_grid {
   // take an unseen neighbour's facing cells as unknown without reading them:
   // the explored region's borders face unseen tiles, whose halo column would
   // otherwise cost a 128-byte line per row.
+  // INVARIANT (the frontier pass is wrong without it): every kernel that
+  // writes `state` either sets tile_seen[tile] = 1 for the tiles it wrote
+  // (k_tile_accum: light / medium items, the heavy finisher, sparse items)
+  // or is followed by k_recount over the map (dm_launch_recount: dm_reset,
+  // dm_set_state, dm_set_logodds, dm_load).  A new state writer must do one
+  // of the two; tests/test_gpu_tile_seen.py fails against a library whose
+  // bit rows trust a stale flag (mutation-checked in round 5).
   uint8_t* tile_seen = nullptr;
   bool fmask_on = false, fmask_valid = false;
   int fmask_mode = 0;  // DM_FMASK=auto|on|off (read at dm_create; tests / A/B): 0 auto, 1 on, 2 off
@@ -509,9 +517,22 @@ inline void dm_select_fw(dm_grid* g, int s) {
 // hipEventSynchronize, which after a short active wait sleeps on an
 // interrupt and wakes up tens of microseconds late (the bench's step
 // cadence showed +20-80 us spikes on ~10 % of the steps).  After kSpinNs of
-// polling it blocks as before.
+// polling it blocks as before: 2 ms, like ShardedMapper._poll's window (a
+// pipelined C3 pass ends ~70 us after the host starts waiting; longer waits
+// should not keep a host core busy, which several ranks' threads would
+// compete for).
+inline void dm_cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#elif defined(__aarch64__)
+  asm volatile("yield" ::: "memory");
+#else
+  std::atomic_signal_fence(std::memory_order_seq_cst);
+#endif
+}
+
 inline hipError_t dm_event_wait(hipEvent_t ev) {
-  constexpr long long kSpinNs = 20000000;  // 20 ms
+  constexpr long long kSpinNs = 2000000;  // 2 ms
   const auto t0 = std::chrono::steady_clock::now();
   for (unsigned it = 0;; ++it) {
     const hipError_t e = hipEventQuery(ev);
@@ -519,7 +540,7 @@ inline hipError_t dm_event_wait(hipEvent_t ev) {
     if ((it & 63u) == 63u &&
         std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() > kSpinNs)
       return hipEventSynchronize(ev);
-    __builtin_ia32_pause();
+    dm_cpu_relax();
   }
 }
 

@@ -186,12 +186,21 @@ class ShardedMapper:
     rank `rank`'s part.  With world_size == 1 it is a plain OccupancyMapper."""
 
     def __init__(self, params: DmParams, rank: int = 0, world_size: int = 1, device: int = 0,
-                 group=None, band=None, timeout: float = 300.0, force_exchange: bool = False):
+                 group=None, band=None, timeout: float = 300.0, force_exchange: bool = False,
+                 records_comm: str = "shared"):
         """`timeout`: seconds any collective (or the device work queued behind
         one) may take before this rank gives up with DM_ERR_COLLECTIVE.
         `force_exchange`: with world_size 1, run the multi-rank exchange
         anyway (halo exchange, export record, records gather, device merge)
-        over `group` (a 1-rank process group): the RCCL path on one GPU."""
+        over `group` (a 1-rank process group): the RCCL path on one GPU.
+        `records_comm`: "shared" (default) all-gathers the export records over
+        `group`, the halo exchange's own communicator, so every collective of
+        the mapper runs in one issue order on one communicator; "separate"
+        builds a second communicator for them (dist.new_group over the same
+        ranks), so a records gather waiting for a pass's labelling does not
+        hold up the next pass's halo exchange.  Two communicators driven from
+        two streams at once have run on one GPU only (tests/test_gpu_nccl.py),
+        never across devices, hence the default."""
         self.params = DmParams.from_buffer_copy(params)
         self.rank, self.world_size, self.group = rank, world_size, group
         self._exchange = world_size > 1 or bool(force_exchange)
@@ -207,6 +216,11 @@ class ShardedMapper:
         self.W = int(params.width)
         self._device = None
         self._dev_path = False
+        if records_comm not in ("shared", "separate"):
+            raise ValueError(f"records_comm must be 'shared' or 'separate', not {records_comm!r}")
+        self.records_comm = records_comm
+        self.timing = False  # set_timing(): HIP-event times of the exchange phases
+        self._tev = collections.deque()  # (halo start, halo end, gather start, gather end) per pass
         self._pending = collections.deque()  # frontiers_begin() passes in flight, oldest first
         try:
             self.max_in_flight = int(load_library().dm_max_passes_in_flight())
@@ -236,15 +250,18 @@ class ShardedMapper:
                 self.stream = torch.cuda.Stream(device=self._tdev, priority=-1)
                 self.band.set_stream(self.stream.cuda_stream)
                 # the export records are all-gathered on the band's exchange
-                # stream (its pass stream with overlap on), over a second
-                # communicator: a records gather that waits for a pass's
-                # labelling then never holds up the next pass's halo exchange
-                # on the map stream (one communicator runs its collectives
-                # in issue order).  Built over the mapper's own group's
-                # ranks (a subgroup's ranks are not 0..P-1 globally);
-                # new_group is collective over the default group, so every
-                # process of it constructs its mappers in the same order.
-                self.rec_group = dist.new_group(self._group_ranks)
+                # stream (its pass stream with overlap on).  "shared": over
+                # the mapper's group, the halo's communicator (one issue
+                # order for every collective; a gather waiting for pass k's
+                # labelling delays pass k+1's halo exchange behind it).
+                # "separate": over a second communicator, so that gather
+                # never holds up the next halo exchange on the map stream.
+                # Built over the mapper's own group's ranks (a subgroup's
+                # ranks are not 0..P-1 globally); new_group is collective
+                # over the default group, so every process of it constructs
+                # its mappers in the same order.
+                self.rec_group = (dist.new_group(self._group_ranks) if records_comm == "separate"
+                                  else group)
                 self._xstreams = {}
                 # records per band export: sized for the band up front (a
                 # cluster per tile: C5's 4096-beam fans reach 0.81), then to
@@ -443,10 +460,15 @@ class ShardedMapper:
         Returns the gathered buffer and the exchange stream the merge runs on."""
         torch = self._torch
         W, P, r = self.W, self.world_size, self.rank
+        tev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if self.timing else None
         with torch.cuda.stream(self.stream):
             rows = self._buf("rows", 2 * W, torch.int8)
             self.band.edge_rows_device(rows.data_ptr(), rows.data_ptr() + W)
+            if tev:
+                tev[0].record(self.stream)
             before, after = self._halo_dev(rows)
+            if tev:  # the map stream waits for the exchange's completion here
+                tev[1].record(self.stream)
             self.band.set_halo_device(before.data_ptr() if before is not None else None,
                                       after.data_ptr() if after is not None else None)
             nb = self.band.export_bytes(self.rec_cap)
@@ -455,8 +477,36 @@ class ShardedMapper:
             self.band.frontiers_export_device(exp.data_ptr(), self.rec_cap)
         xs = self._xstream()
         with torch.cuda.stream(xs):
+            if tev:  # reached once this band's export record is written
+                tev[2].record(xs)
             self._gather_dev(exp, gexp, self.rec_group)
+            if tev:
+                tev[3].record(xs)
+        if tev:
+            self._tev.append(tev)
         return gexp, xs
+
+    # -- exchange timing (bench.py's N > 1 line) ------------------------------
+    def set_timing(self, on: bool = True):
+        """Record HIP events around this rank's halo exchange (map stream) and
+        records all-gather (exchange stream) of every following pass; the
+        export and merge kernels are timed by libdm's own profile."""
+        self.timing = bool(on) and self._dev_path
+        self._tev.clear()
+
+    def exchange_times(self) -> dict:
+        """Mean ms per pass since set_timing(True): `halo_ms` from the map
+        stream reaching the halo exchange to its completion (the peers' rows
+        included: a late neighbour shows here), `records_gather_ms` from this
+        band's export record being written to the all-gather's completion
+        (waits for the slowest rank's record), and the passes counted."""
+        if not self._tev:
+            return {"passes": 0, "halo_ms": None, "records_gather_ms": None}
+        self._torch.cuda.synchronize(self._tdev)
+        halo = [t[0].elapsed_time(t[1]) for t in self._tev]
+        gath = [t[2].elapsed_time(t[3]) for t in self._tev]
+        return {"passes": len(self._tev), "halo_ms": float(np.mean(halo)),
+                "records_gather_ms": float(np.mean(gath))}
 
     def _device_finish(self, result) -> Frontiers | None:
         """Frontiers from a device merge result, or None when a band's export

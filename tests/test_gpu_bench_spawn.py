@@ -41,6 +41,15 @@ def test_bench_self_spawns_two_ranks():
     assert abs(d["value"] - sum(r["updates"]) / (d["ms_per_step"] * 1e-3 * d["steps"])) < 1e-6 * d["value"]
     assert d["exchange_fallbacks"] == sum(r["exchange_fallbacks"])
     assert d["config"]["grid"] == [4096, 8192] and d["config"]["parallelism"] == "row-bands x2"
+    # per-rank exchange phases (HIP events / libdm timers) and the bytes model
+    x = r["exchange_ms_per_pass"]
+    for k in ("halo", "export", "records_gather", "merge"):
+        assert len(x[k]) == 2 and all(v == v and v >= 0 for v in x[k]), (k, x)
+    assert x["passes_timed"] >= 2
+    b = r["exchange_bytes_per_pass"]
+    assert b["halo_row_bytes"] == 4096 and b["records_gathered_per_rank"] == 2 * b["record_bytes"]
+    assert b["record_bytes"] == 64 + 8 * 4096 + 32 * b["rec_cap"]
+    assert r["records_comm"] == "shared" and "neighbour bands" in d["exchange"]
 
 
 def test_bench_one_gpu_runs_in_process():

@@ -242,6 +242,36 @@ def test_async_host_inputs_reused_without_sync(oracle_lib, overlap):
         assert_map_equal(m, om)
 
 
+@pytest.mark.parametrize("overlap", [True, False])
+def test_host_pose_ring_matches_device_inputs(overlap):
+    """k_beam_prep reads the poses of a host-input call straight
+    from the mapped staging ring (kPoseRing slots, rewritten at the same
+    address every other call).  Ten host-input calls with a different pose
+    set each (both slots reused four times, no synchronising call in between)
+    must give exactly the map, U and T of the same batches fed as device
+    inputs: a stale pose read from a cached slot would move a scan's rays."""
+    import torch
+
+    p, batches, amin, inc = cases.world_case(57, 1500, 1300, 0.05, 6, 1024, 10, region_frac=0.7)
+    S, N = batches[0][1].shape
+    dev = _device_batches(batches)
+    pinned = [torch.empty((S, N), dtype=torch.float32).pin_memory() for _ in range(3)]
+    with dm.OccupancyMapper(p) as a, dm.OccupancyMapper(p) as b:
+        a.set_overlap(overlap)
+        b.set_overlap(overlap)
+        for k, (poses, ranges) in enumerate(batches):
+            buf = pinned[k % 3]  # free again: call k-3 was two calls ago
+            buf.numpy()[...] = ranges
+            a.integrate_async(poses, buf.data_ptr(), S, N, amin, inc)
+            pz, rz = dev[k]
+            b.integrate_device(pz.data_ptr(), S, rz.data_ptr(), N, amin, inc)
+        a.synchronize()
+        b.synchronize()
+        assert a.last_counts() == b.last_counts()
+        np.testing.assert_array_equal(a.logodds().view(np.uint32), b.logodds().view(np.uint32))
+        np.testing.assert_array_equal(a.state(), b.state())
+
+
 def test_front_end_gate_timeout_is_a_sticky_error(oracle_lib, monkeypatch):
     """A timed-out front-end hand-off (fault injection: DM_FAULT_GATE=1 makes
     the gate wait for a sequence number that never comes, ~10 us) must not

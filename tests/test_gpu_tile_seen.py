@@ -72,3 +72,44 @@ def test_reset_clears_seen_tiles(oracle_lib):
             fr = m.frontiers(want_mask=True, want_labels=True)
             assert_frontiers_equal(fr, *om.frontiers())
         assert_map_equal(m, om)
+
+
+def _band_edge_state(H, W, edge):
+    """Free regions that end exactly at a band edge (row `edge`, a multiple of
+    64), on either side of it, next to tiles of the other band that were never
+    written (their facing cells are halo rows there, not tile_seen skips)."""
+    st = np.full((H, W), -1, np.int8)
+    st[edge - 64:edge, 0:64] = 0          # band 0's last tile row, below it unseen band-1 tiles
+    st[edge:edge + 64, 128:192] = 0       # band 1's first tile row, above it unseen band-0 tiles
+    st[edge - 1:edge + 1, 256:300] = 0    # a strip across the edge
+    st[edge - 1, 320:384] = 0             # one free row on band 0's side only
+    st[edge, 400:W] = 0                   # one free row on band 1's side, to the ragged map edge
+    st[edge - 30:edge + 30, 200:202] = 100
+    return st
+
+
+@pytest.mark.parametrize("fmask", ["off", "on"])
+def test_band_edge_tiles_with_and_without_fmask(oracle_lib, monkeypatch, fmask):
+    """tile_seen next to band halos, with the bit rows read from
+    the state bytes (DM_FMASK=off) and from fmask (on): a sharded handle's
+    bands (ty == 0 / ty == TY-1 tiles read the halo rows), bulk-written and
+    then grown by rays, against the oracle."""
+    monkeypatch.setenv("DM_FMASK", fmask)
+    W, H, edge = 470, 512, 256
+    p = cases.make_params(W, H)
+    st = _band_edge_state(H, W, edge)
+    L0 = np.where(st == 100, np.float32(p.l_occ), np.where(st == 0, np.float32(p.l_free), np.float32(0)))
+    om = oracle_lib.OracleMap(p)
+    om.L[...] = L0
+    om.state[...] = st
+    with dm.OccupancyMapper(p, devices=[0, 0]) as sh:
+        sh.set_logodds(L0)
+        np.testing.assert_array_equal(sh.state(), st)
+        assert_frontiers_equal(sh.frontiers(want_mask=True, want_labels=True), *om.frontiers())
+        for k in range(3):
+            poses, ranges, amin, inc = cases.random_scans(950 + k, p, 3, 360, spread=0.5)
+            sh.integrate(poses, ranges, amin, inc)
+            om.integrate(poses, ranges, amin, inc)
+            fr = sh.frontiers(want_mask=True, want_labels=True)
+            assert_frontiers_equal(fr, *om.frontiers())
+        assert_map_equal(sh, om)
