@@ -527,6 +527,8 @@ def main():
                 "avg_launch_ms": t_accum_ms,
                 "algorithmic_bytes_per_launch": bytes_accum,
                 "bytes_model": "8*U + 25*T per call (SURVEY.md §8(d) per-unit figures)",
+                **hbm_model({k: float(np.mean([st[k] for st in stats])) for k in ("active_tiles", "pieces")},
+                            t_accum_ms, T_mean),
                 "atomics": atom,
                 "frontier": fr_roof,
             },
@@ -780,7 +782,31 @@ def _cadence(marks):
             "max": float(d.max()), "n": int(d.size)}
 
 
-def _profiled_roofline(band, run, U_mean, T_mean):
+HBM_MODEL_NOTE = ("bytes k_tile_accum moves from HBM by the design: 10 B per cell of every active 64x64 "
+                  "tile (L and state read and written, whole tiles at line granularity) + 16 B per packed "
+                  "piece read. The hit / miss counts (the 8*U of `frac`) stay in LDS and are not in it, so "
+                  "frac (the SURVEY.md §8(d) model) reads ~2x (C3) to ~3x+ (C5-4096) above it. Sparse items "
+                  "(<= 15 pieces: C5's sparse scans) load only their touched 4-cell groups, so there the "
+                  "whole-tile model over-counts and frac_hbm_touched (10 B per touched cell + pieces, a "
+                  "lower bound) is the closer figure")
+
+
+def hbm_model(stats_mean, t_ms, T_mean=None):
+    """frac_hbm_model: the design's own HBM bytes per
+    k_tile_accum launch (HBM_MODEL_NOTE) over its launch time, beside `frac`
+    (SURVEY.md §8(d)'s 8 U + 25 T, which counts LDS-resident counter bytes)."""
+    act, pieces = stats_mean.get("active_tiles"), stats_mean.get("pieces")
+    if not act or not t_ms or t_ms <= 0:
+        return {"frac_hbm_model": None, "hbm_model_bytes_per_launch": None, "frac_hbm_touched": None,
+                "hbm_model": HBM_MODEL_NOTE}
+    b = 10.0 * 4096.0 * act + 16.0 * pieces
+    bt = 10.0 * T_mean + 16.0 * pieces if T_mean else None
+    rate = lambda x: x / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS  # noqa: E731
+    return {"frac_hbm_model": rate(b), "hbm_model_bytes_per_launch": b,
+            "frac_hbm_touched": rate(bt) if bt else None, "hbm_model": HBM_MODEL_NOTE}
+
+
+def _profiled_roofline(band, run, U_mean, T_mean, stats_mean=None):
     """Per-kernel average launch time (HIP events on the library's stream)
     over `run()`, and the k_tile_accum roofline (SURVEY.md §8(d) bytes)."""
     band.profile(True)
@@ -797,6 +823,7 @@ def _profiled_roofline(band, run, U_mean, T_mean):
         "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
         "traffic": None, "avg_launch_ms": t_ms, "algorithmic_bytes_per_launch": bytes_accum,
         "bytes_model": "8*U + 25*T per call (SURVEY.md §8(d) per-unit figures)",
+        **hbm_model(stats_mean or {}, t_ms, T_mean),
     }
 
 
@@ -1004,7 +1031,8 @@ def _run_c5(args, np, torch, synth, m, params, amin, dev, world):
         fst = m.last_stats()  # the last pass's listed tiles, tile-local components, clusters
         mean = lambda key: float(np.mean([st[key] for st in stats]))  # noqa: E731
         avg, roof = _profiled_roofline(m, lambda: [(integrate(k), m.frontiers()) for k in range(5)],
-                                       mean("updates"), mean("touched"))
+                                       mean("updates"), mean("touched"),
+                                       {k: mean(k) for k in ("active_tiles", "pieces")})
         # PMC traffic of this sweep point (tools/pmc_passes.sh over
         # `bench.py --config C5 --sweep N`, workload "C5-N"), when measured
         # on these sources

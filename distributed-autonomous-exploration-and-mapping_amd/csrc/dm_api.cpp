@@ -21,7 +21,7 @@
 
 // Wait for all three streams; nothing of this handle is in flight afterwards.
 hipError_t dm_sync_all(dm_grid* g) {
-  for (hipStream_t s : {g->stream, g->fe_stream, g->pass_stream, g->big_stream}) {
+  for (hipStream_t s : {g->stream, g->fe_streams[0], g->fe_streams[1], g->pass_stream, g->big_stream}) {
     if (!s) continue;
     const hipError_t e = hipStreamSynchronize(s);
     if (e != hipSuccess) return e;
@@ -113,9 +113,12 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   if (nb > g->beams_cap || blocks > g->blk_cap) {
     const int64_t nbc = std::max<int64_t>(nb, g->beams_cap);
     const int64_t bc = std::max<int64_t>(blocks, g->blk_cap);
-    int rc = dev_alloc(&g->beams, nbc, "beams");
-    if (!rc) rc = dev_alloc(&g->blk_hist, bc * 1024, "per-block tile histograms");
-    if (!rc) rc = dev_alloc(&g->blk_n, bc, "per-block histogram sizes");
+    int rc = 0;
+    for (auto& w : g->iw) {
+      if (!rc) rc = dev_alloc(&w.beams, nbc, "beams");
+      if (!rc) rc = dev_alloc(&w.blk_hist, bc * 1024, "per-block tile histograms");
+      if (!rc) rc = dev_alloc(&w.blk_n, bc, "per-block histogram sizes");
+    }
     if (rc) { g->beams_cap = g->blk_cap = 0; return rc; }
     g->beams_cap = nbc;
     g->blk_cap = bc;
@@ -132,9 +135,11 @@ int grow_integrate(dm_grid* g, int32_t S, int32_t N) {
   int64_t act = std::min<int64_t>(g->NT, std::min<int64_t>(segs, (int64_t)S * side * side));
   if (act < 1) act = 1;
   if (act > g->act_cap) {
-    int rc = dev_alloc(&g->act_raw, act * kShards, "first-touch lists");
-    for (auto& w : g->iw)
+    int rc = 0;
+    for (auto& w : g->iw) {
+      if (!rc) rc = dev_alloc(&w.act_raw, act * kShards, "first-touch lists");
       if (!rc) rc = dev_alloc(&w.litems, act, "light work items");
+    }
     if (rc) { g->act_cap = 0; return rc; }
     g->act_cap = act;
   }
@@ -538,11 +543,13 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   DM_HIP(hipMemset(g->fl_n, 0, sizeof(unsigned long long) * 48));
   if ((rc = dev_alloc(&g->bits_flag, 16, "bit-row hand-off word"))) return fail(rc);
   DM_HIP(hipMemset(g->bits_flag, 0, sizeof(unsigned long long) * 16));
-  if ((rc = dev_alloc(&g->fe_flag, 16, "front-end completion word"))) return fail(rc);
-  DM_HIP(hipMemset(g->fe_flag, 0, sizeof(unsigned long long) * 16));
+  if ((rc = dev_alloc(&g->fe_flag, 32, "front-end completion words"))) return fail(rc);
+  DM_HIP(hipMemset(g->fe_flag, 0, sizeof(unsigned long long) * 32));
   if ((rc = dev_alloc(&g->border, g->NT * 256, "frontier borders"))) return fail(rc);
-  if ((rc = dev_alloc(&g->rel, 4 * g->NT, "tile-edge hand-off words"))) return fail(rc);
-  DM_HIP(hipMemset(g->rel, 0, sizeof(unsigned long long) * 4 * (size_t)g->NT));
+  // [0, 4 NT): the dense passes' pair hand-off words; [4 NT, 8 NT): the
+  // sparse passes' per-edge stamps (dm_frontier.hip, EDGE tile kernels)
+  if ((rc = dev_alloc(&g->rel, 8 * g->NT, "tile-edge hand-off words"))) return fail(rc);
+  DM_HIP(hipMemset(g->rel, 0, sizeof(unsigned long long) * 8 * (size_t)g->NT));
   if ((rc = dev_alloc(&g->edge_label, 2 * g->W, "edge labels"))) return fail(rc);
   if ((rc = dev_alloc(&g->halo, 2 * g->W, "halo rows"))) return fail(rc);
   // slot arrays sized for the map up front (a pass that overflows them has
@@ -591,8 +598,10 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   e = hipStreamCreateWithPriority(&g->stream, hipStreamNonBlocking, DM_PRIO_GRID ? prio_hi : prio_lo);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate"));
   g->own_stream = true;
-  e = hipStreamCreateWithPriority(&g->fe_stream, hipStreamNonBlocking, DM_PRIO_FE ? prio_hi : prio_lo);
-  if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(front-end)"));
+  for (int i = 0; i < dm_grid::kFeStreams; ++i) {
+    e = hipStreamCreateWithPriority(&g->fe_streams[i], hipStreamNonBlocking, DM_PRIO_FE ? prio_hi : prio_lo);
+    if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(front-end)"));
+  }
   e = hipStreamCreateWithPriority(&g->pass_stream, hipStreamNonBlocking, DM_PRIO_PASS ? prio_hi : prio_lo);
   if (e != hipSuccess) return fail(dm_hip_check(e, "hipStreamCreate(pass)"));
   e = hipStreamCreateWithPriority(&g->big_stream, hipStreamNonBlocking, DM_PRIO_PASS ? prio_hi : prio_lo);
@@ -602,7 +611,8 @@ int dm_create(dm_grid** out, const dm_params* p, int device) {
   // waits on a readback slot's event and then reads mapped host memory:
   // default fences.
   for (hipEvent_t* ev : {&g->ev_fe, &g->ev_bits[0], &g->ev_bits[1], &g->iw[0].ev_free, &g->iw[1].ev_free,
-                         &g->ev_bigfork, &g->ev_big, &g->flist_ev[0], &g->flist_ev[1]}) {
+                         &g->ev_bigfork, &g->ev_big, &g->flist_ev[0], &g->flist_ev[1], &g->ev_fe_end[0],
+                         &g->ev_fe_end[1]}) {
     e = hipEventCreateWithFlags(ev, hipEventDisableTiming | hipEventDisableSystemFence);
     if (e != hipSuccess) return fail(dm_hip_check(e, "hipEventCreate"));
   }
@@ -627,7 +637,8 @@ int dm_destroy(dm_grid* g) {
   (void)dm_sync_all(g);
   for (auto& t : g->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
   for (hipEvent_t ev : {g->ev_fe, g->ev_bits[0], g->ev_bits[1], g->iw[0].ev_free, g->iw[1].ev_free,
-                        g->ev_bigfork, g->ev_big, g->flist_ev[0], g->flist_ev[1]})
+                        g->ev_bigfork, g->ev_big, g->flist_ev[0], g->flist_ev[1], g->ev_fe_end[0],
+                        g->ev_fe_end[1]})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& r : g->rb) {
     if (r.ev) (void)hipEventDestroy(r.ev);
@@ -635,7 +646,8 @@ int dm_destroy(dm_grid* g) {
     if (r.h_out) (void)hipHostFree(r.h_out - kRbHostRecords);
     dev_free(r.m_out);
   }
-  if (g->fe_stream) (void)hipStreamDestroy(g->fe_stream);
+  for (hipStream_t& fs : g->fe_streams)
+    if (fs) (void)hipStreamDestroy(fs);
   if (g->pass_stream) (void)hipStreamDestroy(g->pass_stream);
   if (g->big_stream) (void)hipStreamDestroy(g->big_stream);
   for (auto& f : g->fw) {
@@ -651,16 +663,17 @@ int dm_destroy(dm_grid* g) {
     dev_free(w.pieces); dev_free(w.hitems); dev_free(w.litems); dev_free(w.heavy_list); dev_free(w.slabs);
     dev_free(w.heavy_done); dev_free(w.tile_count); dev_free(w.tile_cur); dev_free(w.cnt); dev_free(w.sh);
     dev_free(w.pose4); dev_free(w.ranges);
+    dev_free(w.beams); dev_free(w.blk_hist); dev_free(w.blk_n); dev_free(w.act_raw);
   }
   dev_free(g->L); dev_free(g->state); dev_free(g->fmask); dev_free(g->fedge); dev_free(g->tile_seen);
-  dev_free(g->tile_free); dev_free(g->beams); dev_free(g->blk_hist); dev_free(g->blk_n);
+  dev_free(g->tile_free);
   dev_free(g->trig);
   dev_free(g->bs_key); dev_free(g->bs_key2); dev_free(g->bs_idx); dev_free(g->bs_idx2);
   dev_free(g->rs_cnt); dev_free(g->rs_off); dev_free(g->rs_status);
   dev_free(g->border); dev_free(g->rel); dev_free(g->slot_label); dev_free(g->slot_root);
   dev_free(g->slot_own); dev_free(g->slot_acc); dev_free(g->clusters); dev_free(g->cell_slot);
   dev_free(g->edge_label); dev_free(g->mask); dev_free(g->labels);
-  dev_free(g->halo); dev_free(g->fe_flag); dev_free(g->act_raw);
+  dev_free(g->halo); dev_free(g->fe_flag);
   dev_free(g->slot_k); dev_free(g->rank_of); dev_free(g->m_parent); dev_free(g->m_label);
   dev_free(g->m_acc); dev_free(g->m_clu); dev_free(g->m_cnt);
   if (g->h_mcnt) (void)hipHostFree(g->h_mcnt);
@@ -718,14 +731,14 @@ int enqueue_host_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N
   if ((rc = grow_integrate(g, S, N))) return rc;
   if ((rc = ensure_trig(g, N, angle_min, angle_increment))) return rc;
   const int64_t nb = (int64_t)S * N;
-  hipStream_t fs = g->overlap ? g->fe_stream : g->stream;
+  hipStream_t fs = g->overlap ? dm_fe_stream_of(g, dm_next_set(g)) : g->stream;
   // the ranges copy goes to the device buffer of the workspace set this call
   // will use (dm_launch_integrate alternates them); with overlap the front-end
   // stream first waits until that set is free (its last accumulation, which
   // may read its inputs, is done).  The copy stays at the head of this call's
   // front-end: on a stream of its own (waiting for the set, the front-end
   // waiting for it) host-input steps took 1.6x as long.
-  dm_grid::IntWs& w = g->iw[(g->iw_cur + 1) % dm_grid::kIntSets];
+  dm_grid::IntWs& w = g->iw[dm_next_set(g)];
   if (g->overlap) {
     DM_HIP(dm_mark_ws_free(g));
     DM_HIP(hipStreamWaitEvent(fs, w.free_wait ? w.free_wait : w.ev_free, 0));

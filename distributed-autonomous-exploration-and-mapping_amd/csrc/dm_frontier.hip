@@ -38,6 +38,28 @@ DM_PH_DECL(ftile)
 namespace {
 
 constexpr int kFT = 256;              // threads per frontier workgroup
+// Tile-edge unions, two ways (template parameter EDGE of the tile kernels):
+//  * EDGE = false (dense passes, C3's ray fans): in-kernel, through the
+//    stamped hand-off words rel[0, 4 NT) (the tile that arrives second at a
+//    pair unites it; rounds 2-5);
+//  * EDGE = true (sparse passes: the wave kernel + run-rich tiles beside it,
+//    C5): the tile kernels only publish their edges' slot ids and a per-edge
+//    stamp (rel[4 NT + 4 tile + side] = pass stamp, a region of its own so
+//    the two encodings never meet); k_frontier_edges, launched after them,
+//    unites every tile pair across its edges and corners.
+// DM_EDGE_KERNEL (A/B builds): 1 the split above, 0 every pass in-kernel,
+// 2 every pass with the edge kernel.
+#ifndef DM_EDGE_KERNEL
+#define DM_EDGE_KERNEL 1
+#endif
+#ifndef DM_EDGE_HALVE
+#define DM_EDGE_HALVE 0
+#endif
+#if DM_EDGE_HALVE
+#define EDGE_UNITE dm_uf_unite_idx_halve
+#else
+#define EDGE_UNITE dm_uf_unite_idx2
+#endif
 // waves per SIMD for k_frontier_tile: 7 workgroups per CU (LDS 22.6 KB each,
 // <= 72 VGPRs), so a C3 pass's ~3.3k listed tiles run in two rounds of the
 // chip's 1792 slots instead of three of 1280
@@ -133,6 +155,7 @@ __device__ inline int root_rank(const uint64_t* s_root, const int32_t* pre, int 
 // or only the positions bflag marks (k_frontier_bits: too run-rich for the
 // wave kernel); a workgroup then gathers the flags of its next 64 positions
 // in one load round and works through the marked ones.
+template <bool EDGE>
 __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
     FGeom g, const uint64_t* __restrict__ fbits, const int32_t* __restrict__ bflag,
     const int32_t* __restrict__ ftiles, const unsigned long long* __restrict__ list_n,
@@ -339,6 +362,14 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
         sl = v < g.slot_per ? (int32_t)(sh0 + v) : -1;
       }
       const uint64_t fb = __ballot(sl >= 0);
+      if constexpr (EDGE) {
+      // publish only: the edge's slot ids and its stamp (k_frontier_edges
+      // reads both after this kernel; the kernel boundary orders them)
+      if (fb) {
+        border[j * 256 + tid] = sl;
+        if (lane == 0) rel[4 * g.NT + 4 * j + side] = stamp;
+      }
+      } else {
       if (fb) {
         __hip_atomic_store(&border[j * 256 + tid], sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -410,6 +441,7 @@ __global__ __launch_bounds__(kFT, DM_FT_OCC) void k_frontier_tile_big(
             if (me >= 0 && b >= 0) dm_uf_unite_idx(slot_parent, me, b, &cnt[CNT_OVERFLOW], kOvUnionFind);
           }
         }
+      }
       }
     }
     // band edge rows (cross-band merging) and optional dense outputs
@@ -599,7 +631,7 @@ __device__ inline void tile_rows(const FGeom& g, const int8_t* __restrict__ stat
 // facing edge (published slot ids, sc1 loads): lane = position along the
 // edge, cell pos against the neighbour's cells pos-1, pos, pos+1.  A lane
 // skips the pairs the previous lane (previous edge cell) issues.
-__device__ inline void edge_unions(int32_t sl, const int32_t* border, int32_t nb, int opp, int lane,
+[[maybe_unused]] __device__ inline void edge_unions(int32_t sl, const int32_t* border, int32_t nb, int opp, int lane,
                                    int32_t* slot_parent, unsigned long long* flag) {
   const int32_t v = __hip_atomic_load(&border[(int64_t)nb * 256 + opp * 64 + lane], __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT);
@@ -759,6 +791,7 @@ __global__ __launch_bounds__(kFW * 64) void k_frontier_bits(
   }
 }
 
+template <bool EDGE>
 __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
     FGeom g, const uint64_t* __restrict__ fbits,
     const int32_t* __restrict__ ftiles, const unsigned long long* __restrict__ list_n,
@@ -955,6 +988,16 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
     uint64_t fb[4];
 #pragma unroll
     for (int sd = 0; sd < 4; ++sd) fb[sd] = __ballot(sl[sd] >= 0);
+    if constexpr (EDGE) {
+    // publish only (k_frontier_edges unites the pairs after this kernel)
+#pragma unroll
+    for (int sd = 0; sd < 4; ++sd)
+      if (fb[sd]) {
+        border[(int64_t)tile * 256 + sd * 64 + lane] = sl[sd];
+        if (lane == 0) rel[4 * g.NT + 4 * (int64_t)tile + sd] = stamp;
+      }
+    DM_PH(dm_phase_acc_ftile, 6);
+    } else {
 #pragma unroll
     for (int sd = 0; sd < 4; ++sd)
       if (fb[sd]) __hip_atomic_store(&border[(int64_t)tile * 256 + sd * 64 + lane], sl[sd], __ATOMIC_RELAXED,
@@ -1003,6 +1046,7 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
       }
       DM_PH(dm_phase_acc_ftile, 8);
     }
+    }
     // ---- 9. band edge rows (cross-band merging) and optional dense outputs ---
     const int32_t gy = ty0 + lane;
     if (gy < g.R && (dense || gy == 0 || gy == g.R - 1)) {
@@ -1022,6 +1066,113 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
     DM_PH(dm_phase_acc_ftile, 10);
   }
   DM_PHW_FLUSH(dm_phase_acc_ftile);
+}
+
+// Unions across tile edges, after the tile kernels of a pass (DM_EDGE_KERNEL).
+// One wave per listed tile, which owns the relations to its right, lower,
+// lower-left and lower-right neighbours (every adjacent tile pair has exactly
+// one owner).  A relation is united only where both tiles published the
+// facing edge in THIS pass (rel[4 * tile + side] == stamp: the tile has
+// frontier cells on that edge; a stale record of an earlier pass is never
+// read).  The right and lower edges: lane = position along the edge, its
+// cell against the neighbour's cells pos-1, pos, pos+1 (edge_unions); the
+// corners: one lane each.  Unions are keyed by slot index, as in the tile
+// kernels (dm_uf_unite_idx); k_frontier_resolve folds the min labels.  In
+// the tile kernels the same unions waited behind the border stores' drain,
+// a returning hand-off atomic and the neighbour's border loads (C3: 35 % of
+// k_frontier_tile_big's workgroup time, profiles/r06_phase_c3.log); here
+// they are thousands of short independent waves.
+__global__ __launch_bounds__(kFW * 64) void k_frontier_edges(FGeom g, const int32_t* __restrict__ ftiles,
+                                                             const unsigned long long* __restrict__ list_n,
+                                                             const int32_t* __restrict__ border,
+                                                             const unsigned long long* __restrict__ rel,
+                                                             int32_t* slot_parent, unsigned long long* cnt) {
+  const unsigned long long stamp = cnt[CNT_STAMP];
+  const int w = threadIdx.x >> 6, lane = __lane_id();
+  const int64_t nft = (int64_t)*list_n;
+  unsigned long long* uflag = &cnt[CNT_OVERFLOW];
+  __shared__ int2 s_pairs[kFW][4 * 64];  // a wave's pairs (<= 3 per lane + a corner)
+  // two waves per listed tile: wave 2j + 0 its right edge (and both lower
+  // corners, on lanes 0 / 63), wave 2j + 1 its lower edge
+  for (int64_t v = (int64_t)blockIdx.x * kFW + w; v < 2 * nft; v += (int64_t)gridDim.x * kFW) {
+    const int64_t tile = __builtin_amdgcn_readfirstlane(ftiles[v >> 1]);
+    const int rel_kind = (int)(v & 1);  // 0 right edge + corners, 1 lower edge
+    const int32_t tx = (int32_t)(tile % g.TX), ty = (int32_t)(tile / g.TX);
+    const bool right = tx + 1 < g.TX, down = ty + 1 < g.TY, left = tx > 0;
+    // everything in ONE round of loads after the tile id: the stamps that
+    // say which records are this pass's, and the records themselves
+    // (speculative: a record of an earlier pass is read but not used)
+    const int64_t nb = rel_kind == 0 ? (right ? tile + 1 : tile) : (down ? tile + g.TX : tile);
+    const int my_side = rel_kind == 0 ? 3 : 1, nb_side = rel_kind == 0 ? 2 : 0;
+    const unsigned long long* est = rel + 4 * g.NT;  // the per-edge stamps (EDGE tile kernels)
+    const unsigned long long m_me = est[4 * tile + my_side];
+    const unsigned long long m_nb = est[4 * nb + nb_side];
+    const int32_t sl = border[tile * 256 + my_side * 64 + lane];
+    const int32_t v_nb = border[nb * 256 + nb_side * 64 + lane];
+    // corners (rel_kind 0, lanes 0 / 63): this tile's (63, 0) / (63, 63)
+    // against the lower-left tile's (0, 63) / the lower-right tile's (0, 0)
+    const bool corner_lane = rel_kind == 0 && down && ((lane == 0 && left) || (lane == 63 && right));
+    const int64_t dn = lane == 0 ? tile + g.TX - 1 : tile + g.TX + 1;
+    unsigned long long m_row = 0ull, m_dn = 0ull;
+    int32_t c_me = -1, c_dn = -1;
+    if (corner_lane) {
+      m_row = est[4 * tile + 1];
+      m_dn = est[4 * dn + 0];
+      c_me = border[tile * 256 + 64 + lane];
+      c_dn = border[dn * 256 + (lane == 0 ? 63 : 0)];
+    }
+    const bool has_nb = rel_kind == 0 ? right : down;
+    // this lane's distinct pairs (cell pos against the neighbour's pos-1,
+    // pos, pos+1, minus those the previous lane issues), compacted into the
+    // wave's list so each lane then runs ONE union instead of up to three in
+    // turn
+    int32_t sb[3] = {-1, -1, -1};
+    bool keep[4] = {false, false, false, false};
+    if (has_nb && m_me == stamp && m_nb == stamp) {  // uniform
+      sb[0] = __shfl_up(v_nb, 1);
+      sb[1] = v_nb;
+      sb[2] = __shfl_down(v_nb, 1);
+      if (lane == 0) sb[0] = -1;
+      if (lane == 63) sb[2] = -1;
+      const int32_t psl = __shfl_up(sl, 1);
+      int32_t psb[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) psb[q] = __shfl_up(sb[q], 1);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int32_t b = sb[q];
+        bool dup = sl < 0 || b < 0;
+#pragma unroll
+        for (int r = 0; r < q; ++r) dup |= sb[r] == b;
+        if (lane > 0 && psl == sl) dup |= (psb[0] == b) | (psb[1] == b) | (psb[2] == b);
+        keep[q] = !dup;
+      }
+    }
+    keep[3] = corner_lane && m_row == stamp && m_dn == stamp && c_me >= 0 && c_dn >= 0;
+    const int np = (int)keep[0] + (int)keep[1] + (int)keep[2] + (int)keep[3];
+    int incl = np;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int t = __shfl_up(incl, d);
+      if (lane >= d) incl += t;
+    }
+    const int total = __shfl(incl, 63);
+    if (total == 0) continue;
+    int2* lst = s_pairs[w];
+    {
+      int at = incl - np;
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if (keep[q]) lst[at++] = make_int2(sl, sb[q]);
+      if (keep[3]) lst[at] = make_int2(c_me, c_dn);
+    }
+    wave_lds_sync();
+    for (int i = lane; i < total; i += 64) {
+      const int2 q = lst[i];
+      EDGE_UNITE(slot_parent, q.x, q.y, uflag, kOvUnionFind);
+    }
+    wave_lds_sync();
+  }
 }
 
 // Slot s is in use iff its offset inside its shard region is below that
@@ -1713,6 +1864,18 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   const bool dense = g->frontier_kernel == 2 ||
                      (g->frontier_kernel == 0 && g->ftf_hint > 0 && g->runs_hint > kDenseRuns * g->ftf_hint &&
                       g->ftf_hint <= kDenseMaxTiles);
+  // Tile-edge unions in the tile kernels or in k_frontier_edges after them
+  // (DESIGN.md §3.2): the edge kernel for sparse passes with fewer clusters
+  // than listed tiles (C5 12-768 beams: passes 3-10 % shorter, steps up to
+  // 11 %), in-kernel for dense passes (C3: the extra launch costs more than
+  // the tiles save, 3-4 % per step) and for sparse passes with more
+  // clusters than tiles (C5-4096's 4.6 per tile: many distinct pairs per
+  // edge, step 2-15 % slower with the edge kernel);
+  // profiles/r06_edge_kernel_ab.log.  Both are exact for any map.
+  const bool edge = DM_EDGE_KERNEL == 2 ||
+                    (DM_EDGE_KERNEL == 1 && !dense && g->sort_hint <= std::max<int64_t>(g->ftile_hint, 1));
+  auto* const big_kernel = edge ? k_frontier_tile_big<true> : k_frontier_tile_big<false>;
+  auto* const wave_kernel = edge ? k_frontier_tile<true> : k_frontier_tile<false>;
   dm_timer_begin(g, "frontier_bits", &t);
   DM_LAUNCH(k_frontier_bits, dim3(bits_grid), dim3(kFW * 64), 0, g->stream, fg, g->state, g->halo, g->fmask,
             g->fedge, g->tile_seen, g->ftiles, g->ftiles_n, list_n, g->fbits, g->cnt, g->fmask_on ? 1 : 0,
@@ -1746,14 +1909,15 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
     DM_HIP(hipEventRecord(g->ev_bigfork, ps));
     DM_HIP(hipStreamWaitEvent(g->big_stream, g->ev_bigfork, 0));
     dm_timer_begin(g, "frontier_big", &t, g->big_stream);
-    DM_LAUNCH(k_frontier_tile_big, dim3(big_grid), dim3(kFT), 0, g->big_stream, fg, g->fbits, g->big_tiles,
+    DM_LAUNCH(big_kernel, dim3(big_grid), dim3(kFT), 0, g->big_stream, fg, g->fbits,
+              g->big_tiles,
               g->ftiles, list_n, g->border, g->rel, g->slot_label, g->slot_parent, g->slot_own,
               g->slot_acc, g->mask, g->cell_slot, g->edge_slot, g->cnt, g->fsh, 0);
     dm_timer_end(g, &t);
     DM_HIP(hipGetLastError());
     DM_HIP(hipEventRecord(g->ev_big, g->big_stream));
     dm_timer_begin(g, "frontier_tile", &t, ps);
-    DM_LAUNCH(k_frontier_tile, dim3(wave_grid), dim3(kFW * 64), 0, ps, fg, g->fbits,
+    DM_LAUNCH(wave_kernel, dim3(wave_grid), dim3(kFW * 64), 0, ps, fg, g->fbits,
                        g->ftiles, list_n, g->border, g->rel,
                        g->slot_label, g->slot_parent, g->slot_own, g->slot_acc, g->mask, g->cell_slot,
                        g->edge_slot, g->cnt, g->fsh, g->big_tiles);
@@ -1768,9 +1932,19 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
     // (caps of 256-1024 workgroups, to leave the map update more slots,
     // measured slower: DESIGN.md §3.3.2)
     const int dense_grid = grid_for(std::min<int64_t>(g->NT, g->ftile_hint > 0 ? want_waves : g->NT), 1, 8192);
-    DM_LAUNCH(k_frontier_tile_big, dim3(dense_grid), dim3(kFT), 0, ps, fg, g->fbits, nullptr, g->ftiles, list_n,
+    DM_LAUNCH(big_kernel, dim3(dense_grid), dim3(kFT), 0, ps, fg, g->fbits, nullptr,
+              g->ftiles, list_n,
               g->border, g->rel, g->slot_label, g->slot_parent, g->slot_own, g->slot_acc, g->mask,
               g->cell_slot, g->edge_slot, g->cnt, g->fsh, 1);
+    dm_timer_end(g, &t);
+    DM_HIP(hipGetLastError());
+  }
+  if (edge) {
+    dm_timer_begin(g, "frontier_edges", &t, ps);
+    // two waves per listed tile (the kernel grid-strides)
+    DM_LAUNCH(k_frontier_edges, dim3(grid_for(2 * std::min<int64_t>(want_waves, g->NT), kFW, 16384)),
+              dim3(kFW * 64), 0, ps, fg, g->ftiles, list_n, g->border, g->rel,
+              g->slot_parent, g->cnt);
     dm_timer_end(g, &t);
     DM_HIP(hipGetLastError());
   }

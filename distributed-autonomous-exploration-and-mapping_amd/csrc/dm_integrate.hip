@@ -1575,7 +1575,7 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   // accumulation and a frontier pass still in flight on g->stream
   hipStream_t fs = g->stream;
   if (g->overlap) {
-    fs = g->fe_stream;
+    fs = dm_fe_stream_of(g, g->iw_cur);
     DM_HIP(dm_mark_ws_free(g));  // still owed when no frontier pass came in between
     DM_HIP(hipStreamWaitEvent(fs, w.free_wait ? w.free_wait : w.ev_free, 0));
   }
@@ -1605,30 +1605,66 @@ int dm_launch_integrate(dm_grid* g, int32_t S, const double* d_pose4, int32_t N,
   KernelTimer t;
   dm_timer_begin(g, "beam_prep", &t, fs);
   DM_LAUNCH(k_beam_prep, dim3(nblk), dim3(256), 0, fs, a, ge, d_pose4, d_ranges,
-            d_trig, g->beams, w.tile_count, g->act_raw, w.sh, g->blk_hist, g->blk_n, w.cnt);
+            d_trig, w.beams, w.tile_count, w.act_raw, w.sh, w.blk_hist, w.blk_n, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "plan", &t, fs);
   DM_LAUNCH(k_plan, dim3(grid_for(g->act_cap, kPlanThreads, 256)), dim3(kPlanThreads), 0, fs,
-                     ge, g->act_raw, w.sh, w.tile_cur, w.tile_count, w.hitems, w.litems,
+                     ge, w.act_raw, w.sh, w.tile_cur, w.tile_count, w.hitems, w.litems,
                      w.heavy_list, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   dm_timer_begin(g, "scatter", &t, fs);
-  DM_LAUNCH(k_scatter, dim3(nblk), dim3(256), 0, fs, a, ge, g->beams,
-            w.tile_cur, g->blk_hist, g->blk_n, w.pieces, w.cnt);
+  DM_LAUNCH(k_scatter, dim3(nblk), dim3(256), 0, fs, a, ge, w.beams,
+            w.tile_cur, w.blk_hist, w.blk_n, w.pieces, w.cnt);
   dm_timer_end(g, &t);
   DM_HIP(hipGetLastError());
   if (g->overlap) {
     // front-end -> map update by a device-side seq gate (an event wait
     // measured 211-213 vs 215-218 x 10^9 updates/s, profiles/r02_fe_gate_ab.log)
-    if (int rc = dm_launch_signal(fs, g->fe_flag)) return rc;
+    DM_HIP(hipEventRecord(g->ev_fe_end[g->iw_cur % 2], fs));
+    unsigned long long* flag = dm_fe_flag_of(g, g->iw_cur);
+    if (int rc = dm_launch_signal(fs, flag)) return rc;
     // a timeout sets the sticky halt word (not this call's counters: the
     // front-end's own reset, still queued, would clear them)
-    if (int rc = dm_launch_gate(g->stream, g->fe_flag, g->fe_flag + kHaltWord, 1ull, g->fault_gate ? 1000ull : 0ull,
+    if (int rc = dm_launch_gate(g->stream, flag, g->fe_flag + kHaltWord, 1ull, g->fault_gate ? 1000ull : 0ull,
                                 g->fault_gate ? (1ull << 40) : 0ull))
       return rc;
   }
+#ifdef DM_FE_DUMMY
+  // Diagnostic build only (never the product): one more k_beam_prep of this
+  // batch into scratch buffers on the front-end stream AFTER the front-end's
+  // hand-off signal (so it delays no accumulation), i.e. extra work beside
+  // the map chain; how much the pipelined step grows tells whether the step
+  // is bound by the chip's occupancy (workgroup-us) or by latency chains.
+  if (g->overlap) {
+    struct Dummy {
+      Beam* beams = nullptr; int32_t* tc = nullptr; int32_t* act = nullptr; int2* hist = nullptr;
+      int32_t* hn = nullptr; unsigned long long* sh = nullptr; unsigned long long* cnt = nullptr;
+      int64_t nb = 0, nt = 0, blocks = 0, act_cap = 0;
+    };
+    static Dummy d;
+    if (d.nb < nb || d.nt < g->NT || d.blocks < nblk || d.act_cap < g->act_cap) {
+      (void)hipDeviceSynchronize();
+      for (void* q : {(void*)d.beams, (void*)d.tc, (void*)d.act, (void*)d.hist, (void*)d.hn, (void*)d.sh,
+                      (void*)d.cnt})
+        if (q) (void)hipFree(q);
+      d.nb = nb; d.nt = g->NT; d.blocks = nblk; d.act_cap = g->act_cap;
+      DM_HIP(hipMalloc((void**)&d.beams, sizeof(Beam) * nb));
+      DM_HIP(hipMalloc((void**)&d.tc, sizeof(int32_t) * g->NT));
+      DM_HIP(hipMalloc((void**)&d.act, sizeof(int32_t) * g->act_cap * kShards));
+      DM_HIP(hipMalloc((void**)&d.hist, sizeof(int2) * 1024 * nblk));
+      DM_HIP(hipMalloc((void**)&d.hn, sizeof(int32_t) * nblk));
+      DM_HIP(hipMalloc((void**)&d.sh, sizeof(unsigned long long) * kShards * kShardWords));
+      DM_HIP(hipMalloc((void**)&d.cnt, sizeof(unsigned long long) * CNT_N));
+    }
+    DM_HIP(hipMemsetAsync(d.tc, 0, sizeof(int32_t) * g->NT, fs));
+    DM_LAUNCH(k_integrate_reset, dim3(2), dim3(256), 0, fs, d.cnt, d.sh);
+    DM_LAUNCH(k_beam_prep, dim3(nblk), dim3(256), 0, fs, a, ge, d_pose4, d_ranges, d_trig, d.beams, d.tc,
+              d.act, d.sh, d.hist, d.hn, d.cnt);
+    DM_HIP(hipGetLastError());
+  }
+#endif
   const int vec_ok = (g->W % 4 == 0) ? 1 : 0;
   // heavy chunks and medium tiles first (the long items), then the light
   // tiles; the last item of each heavy tile applies its merged slab

@@ -160,8 +160,22 @@ struct dm_grid {
   // (iw[p].ev_free), which is long done when the steps are pipelined, so no
   // marker sits behind the accumulation of call k.
   bool overlap = false;
-  hipStream_t fe_stream = nullptr;
+  // DM_FE_STREAMS = 2: consecutive calls' front-ends alternate between two
+  // streams (call k on fe_streams[set % 2], the set being its workspace
+  // set), so call k+1's front-end may start before call k's has finished
+  // instead of queueing behind it; each stream has its own hand-off words
+  // (dm_fe_flag_of).  1: one front-end stream (fe_streams[0]).
+#ifndef DM_FE_STREAMS
+#define DM_FE_STREAMS 1
+#endif
+  static constexpr int kFeStreams = DM_FE_STREAMS;
+  static_assert(kFeStreams == 1 || kFeStreams == 2, "one or two front-end streams");
+  hipStream_t fe_streams[2] = {nullptr, nullptr};
   hipEvent_t ev_fe = nullptr;
+  // the end of the last front-end of each set parity (before its signal):
+  // a caller that refills a buffer every front-end reads (the sharded
+  // handle's peer copies of the inputs) orders itself after it
+  hipEvent_t ev_fe_end[2] = {nullptr, nullptr};
   // front-end completion word (k_fe_signal / k_fe_gate, dm_integrate.hip):
   // the sequence number of the last call whose front-end finished
   unsigned long long* fe_flag = nullptr;  // [kSigWord] / [kGateWord] hand-off counts, [kHaltWord] sticky error
@@ -254,18 +268,21 @@ struct dm_grid {
   unsigned long long* fsh = nullptr;    // [kShards][kShardWords] frontier shards
   unsigned long long* h_sh = nullptr;   // pinned mirror of the last call's integrate shards, then fsh
 
-  // integrate workspace
-  Beam* beams = nullptr; int64_t beams_cap = 0;
+  // integrate workspace capacities (the arrays are per set, IntWs)
+  int64_t beams_cap = 0;
   int64_t blk_cap = 0;            // workgroups blk_hist / blk_n hold
-  int2* blk_hist = nullptr;       // [beam blocks][1024] k_beam_prep's (tile, pieces | hash slot << 16) histogram
-  int32_t* blk_n = nullptr;       // [beam blocks] its entries
   int64_t segs_cap = 0;           // pieces per workspace
-  int32_t* act_raw = nullptr;    // [kShards][act_cap] first-touch lists per shard
   int64_t act_cap = 0;
   int64_t hitem_cap = 0;
   int64_t heavy_cap = 0;
   // what the front-end hands to the accumulation, one set per call parity
   struct IntWs {
+    // the front-end's own scratch (k_beam_prep -> k_plan / k_scatter): per
+    // set, so two calls' front-ends may run at once (DM_FE_STREAMS)
+    Beam* beams = nullptr;          // [beams_cap]
+    int2* blk_hist = nullptr;       // [beam blocks][1024] k_beam_prep's (tile, pieces | hash slot << 16) histogram
+    int32_t* blk_n = nullptr;       // [beam blocks] its entries
+    int32_t* act_raw = nullptr;     // [kShards][act_cap] first-touch lists per shard
     PackedPiece* pieces = nullptr;    // [segs_cap] ray pieces binned by tile
     int4* hitems = nullptr;           // heavy work items {tile, first piece, pieces, heavy ordinal}
     int4* litems = nullptr;           // light work items {tile, first piece, pieces, -1} [act_cap]
@@ -483,6 +500,18 @@ inline void dm_select_slot(dm_grid* g, int slot) {
   g->h_out_cap = r.h_out_cap;
   g->m_out = r.m_out;
 }
+
+// The front-end stream of workspace set `set` and its hand-off words
+// (k_seq_signal / k_seq_gate: [kSigWord], [kGateWord] of 16 words per
+// stream; the sticky halt word fe_flag[kHaltWord] is shared).
+inline hipStream_t dm_fe_stream_of(const dm_grid* g, int set) {
+  return g->fe_streams[set % dm_grid::kFeStreams];
+}
+inline unsigned long long* dm_fe_flag_of(const dm_grid* g, int set) {
+  return g->fe_flag + 16 * (set % dm_grid::kFeStreams);
+}
+// the set (and stream) the next integrate call will use
+inline int dm_next_set(const dm_grid* g) { return (g->iw_cur + 1) % dm_grid::kIntSets; }
 
 // Settle the free events owed by the integrate workspaces (their last
 // accumulation is enqueued on g->stream before this point): `recorded`, an

@@ -496,7 +496,7 @@ int dm_sh_integrate_device(dm_grid* g, int32_t S, const double* d_pose4, int32_t
     const double* pp = d_pose4;
     const float* rp = d_ranges;
     // the stream the band's front-end (the only reader of the inputs) runs on
-    hipStream_t fs = b->overlap ? b->fe_stream : b->stream;
+    hipStream_t fs = b->overlap ? dm_fe_stream_of(b, dm_next_set(b)) : b->stream;
     DM_HIP(hipSetDevice(d));
     if (wait_in) DM_HIP(hipStreamWaitEvent(fs, s->ev_in, 0));
     if (nb > 0 && d != src) {  // inputs on another device: a copy the band owns
@@ -513,7 +513,9 @@ int dm_sh_integrate_device(dm_grid* g, int32_t S, const double* d_pose4, int32_t
         s->d_ranges_cap[(size_t)r] = nb;
       }
       // on the front-end's stream: after the previous call's front-end read
-      // the last copy, before this call's reads it
+      // the last copy (on another stream when front-ends alternate between
+      // two: ev_fe_end), before this call's reads it
+      if (dm_grid::kFeStreams > 1 && b->overlap) DM_HIP(hipStreamWaitEvent(fs, b->ev_fe_end[b->iw_cur % 2], 0));
       DM_HIP(hipMemcpyPeerAsync(s->d_pose[(size_t)r], d, d_pose4, src, sizeof(double) * 4 * (size_t)S, fs));
       DM_HIP(hipMemcpyPeerAsync(s->d_ranges[(size_t)r], d, d_ranges, src, sizeof(float) * (size_t)nb, fs));
       pp = s->d_pose[(size_t)r];

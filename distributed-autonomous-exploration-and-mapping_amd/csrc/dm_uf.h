@@ -79,6 +79,66 @@ __device__ inline int32_t dm_uf_root(const int32_t* par, int32_t x, unsigned lon
   return x;
 }
 
+// Find with path halving: every other node on the way is re-pointed to its
+// grandparent (a relaxed agent-scope store).  Only a non-root is ever
+// re-pointed, and only to an ancestor, so a CAS hooking a root is never
+// undone and the forest stays acyclic (parents only point to smaller
+// indices); a racing halving store just writes another ancestor.
+__device__ inline int32_t dm_uf_find_halve(int32_t* par, int32_t x, unsigned long long* flag,
+                                           unsigned long long bit) {
+  for (int it = 0; it < kUfFindBound; ++it) {
+    const int32_t p = dm_uf_load(par + x);
+    if (p == x) return x;
+    const int32_t gp = dm_uf_load(par + p);
+    if (gp == p) return p;
+    __hip_atomic_store(par + x, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    x = gp;
+  }
+  dm_uf_flag(flag, bit);
+  return x;
+}
+
+// dm_uf_unite_idx with halving finds (many concurrent unions over one
+// forest: k_frontier_edges)
+__device__ inline void dm_uf_unite_idx_halve(int32_t* par, int32_t a, int32_t b, unsigned long long* flag,
+                                             unsigned long long bit) {
+  for (int it = 0; it < kUfUniteBound; ++it) {
+    a = dm_uf_find_halve(par, a, flag, bit);
+    b = dm_uf_find_halve(par, b, flag, bit);
+    if (a == b) return;
+    if (a < b) { const int32_t t = a; a = b; b = t; }
+    const int32_t old = atomicCAS(&par[a], a, b);
+    if (old == a) return;
+    a = old;
+  }
+  dm_uf_flag(flag, bit);
+}
+
+// dm_uf_unite_idx with both finds walked in step (their loads issued
+// together: one round trip per level of the deeper chain instead of one per
+// level of each).
+__device__ inline void dm_uf_unite_idx2(int32_t* par, int32_t a, int32_t b, unsigned long long* flag,
+                                        unsigned long long bit) {
+  for (int it = 0; it < kUfUniteBound; ++it) {
+    for (int f = 0;; ++f) {
+      if (f == kUfFindBound) {
+        dm_uf_flag(flag, bit);
+        return;
+      }
+      const int32_t pa = dm_uf_load(par + a), pb = dm_uf_load(par + b);
+      if (pa == a && pb == b) break;
+      a = pa;
+      b = pb;
+    }
+    if (a == b) return;
+    if (a < b) { const int32_t t = a; a = b; b = t; }
+    const int32_t old = atomicCAS(&par[a], a, b);
+    if (old == a) return;
+    a = old;  // hooked meanwhile: climb from its real parent
+  }
+  dm_uf_flag(flag, bit);
+}
+
 // Union keyed by node index instead of label: hook the root with the larger
 // index under the other.  Used where the labels are not known yet when the
 // unions run (the in-kernel tile-edge unions of k_frontier_tile: a

@@ -268,3 +268,21 @@ def test_neighbour_halo_exchange():
         before, after = out[r]
         assert before == (None if r == 0 else [10 * (r - 1) + 1] * 37)
         assert after == (None if r == world - 1 else [10 * (r + 1)] * 37)
+
+
+def test_records_comm_choice_is_validated():
+    """records_comm picks the communicator of the export-record all-gather
+    (DESIGN.md §4): "shared" (the default, the halo's own group) or
+    "separate"; anything else is refused before any collective is set up."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "distributed-autonomous-exploration-and-mapping_amd"))
+    from dm.sharded import ShardedMapper
+    from oracle_band import OracleBand
+
+    p = cases.make_params(128, 128)
+    with pytest.raises(ValueError):
+        ShardedMapper(p, band=OracleBand(p), records_comm="ring")
+    sm = ShardedMapper(p, band=OracleBand(p))
+    assert sm.records_comm == "shared" and not sm.timing
+    sm.set_timing(True)  # no device path: timing stays off, nothing to report
+    assert not sm.timing and sm.exchange_times()["passes"] == 0

@@ -31,6 +31,13 @@ for s in "$@"; do
     bench)
       timeout -k 10 400 python -u bench.py > $OUT/bench.log 2>&1
       rc=$?; echo "bench rc=$rc"; tail -1 $OUT/bench.log | cut -c1-600; ok $rc || exit $rc ;;
+    rehearse:*)
+      # N ranks of the multi-GPU bench on this one GPU (gloo, host-staged
+      # exchange): the N > 1 line's fields, not xGMI timings
+      n=${s#rehearse:}
+      timeout -k 10 500 python -u bench.py --gpus $n --backend gloo --device-override 0 --steps 20 --warmup 5 \
+        --cpu-seconds 0 --pool 3 --no-host-inputs > $OUT/rehearse_$n.log 2>&1
+      rc=$?; echo "rehearse $n rc=$rc"; tail -1 $OUT/rehearse_$n.log | cut -c1-300; ok $rc || exit $rc ;;
     shard)
       timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --backend gloo --device-override 0 \
