@@ -767,8 +767,11 @@ int enqueue_host_integrate(dm_grid* g, int32_t S, const double* poses, int32_t N
       // the GPU must not keep it in L2 (non-coherent host memory may be
       // cached there; the other mapped buffers the device reads are
       // Mapped | Coherent too)
+#ifndef DM_POSE_COHERENT
+#define DM_POSE_COHERENT 1  // 0: Mapped only (the round-5 allocation; A/B builds)
+#endif
       DM_HIP(hipHostMalloc((void**)&g->h_pose4[i], sizeof(double) * 4 * (size_t)std::max(S, 1),
-                           hipHostMallocMapped | hipHostMallocCoherent));
+                           hipHostMallocMapped | (DM_POSE_COHERENT ? hipHostMallocCoherent : 0u)));
       DM_HIP(hipHostGetDevicePointer((void**)&g->h_pose4_dev[i], g->h_pose4[i], 0));
     }
     g->h_pose_cap = (int64_t)std::max(S, 1) * 4;
