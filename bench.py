@@ -393,7 +393,9 @@ def main():
             "passes_timed": int(xt["passes"]),
             "how": "HIP events: halo = map stream reaching the neighbour send / receive to its "
                    "completion; records_gather = this band's export record written to the all-gather's "
-                   "completion; export / merge = libdm's kernel timers (dm_profile)"}
+                   "completion; export / merge = libdm's kernel timers (dm_profile) of the record kernel "
+                   "(k_export; the band's frontier pipeline before it is timed under its own kernels in "
+                   "kernel_avg_ms) and of the merge"}
         ranks_info["exchange_bytes_per_pass"] = {
             "halo_row_bytes": G, "halo_sent_per_interior_rank": 2 * G,
             "records_gathered_per_rank": world_size * nb, "record_bytes": nb, "rec_cap": mapper.rec_cap,
