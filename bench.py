@@ -529,7 +529,8 @@ def main():
                 "avg_launch_ms": t_accum_ms,
                 "algorithmic_bytes_per_launch": bytes_accum,
                 "bytes_model": "8*U + 25*T per call (SURVEY.md §8(d) per-unit figures)",
-                **hbm_model({k: float(np.mean([st[k] for st in stats])) for k in ("active_tiles", "pieces")},
+                **hbm_model({k: float(np.mean([st[k] for st in stats]))
+                             for k in ("active_tiles", "pieces", "sparse_items")},
                             t_accum_ms, T_mean),
                 "atomics": atom,
                 "frontier": fr_roof,
@@ -784,13 +785,13 @@ def _cadence(marks):
             "max": float(d.max()), "n": int(d.size)}
 
 
-HBM_MODEL_NOTE = ("bytes k_tile_accum moves from HBM by the design: 10 B per cell of every active 64x64 "
-                  "tile (L and state read and written, whole tiles at line granularity) + 16 B per packed "
-                  "piece read. The hit / miss counts (the 8*U of `frac`) stay in LDS and are not in it, so "
-                  "frac (the SURVEY.md §8(d) model) reads ~2x (C3) to ~3x+ (C5-4096) above it. Sparse items "
-                  "(<= 15 pieces: C5's sparse scans) load only their touched 4-cell groups, so there the "
-                  "whole-tile model over-counts and frac_hbm_touched (10 B per touched cell + pieces, a "
-                  "lower bound) is the closer figure")
+HBM_MODEL_NOTE = ("bytes k_tile_accum moves from HBM by the design: 10 B per cell of every dense item's "
+                  "64x64 tile (L and state read and written, whole tiles at line granularity) + 16 B per "
+                  "packed piece read; sparse items (<= 15 pieces, C5's sparse scans) load and store only "
+                  "their touched 4-cell groups, at most 40 B per touched cell, which frac_hbm_touched "
+                  "(10 B per touched cell + pieces) bounds from below. The hit / miss counts (the 8*U of "
+                  "`frac`) stay in LDS and are in neither, so frac (the SURVEY.md §8(d) model) reads ~2x "
+                  "(C3) to ~3x+ (C5-4096) above the bytes moved; frac_traffic (PMC) is the measured figure")
 
 
 def hbm_model(stats_mean, t_ms, T_mean=None):
@@ -801,7 +802,8 @@ def hbm_model(stats_mean, t_ms, T_mean=None):
     if not act or not t_ms or t_ms <= 0:
         return {"frac_hbm_model": None, "hbm_model_bytes_per_launch": None, "frac_hbm_touched": None,
                 "hbm_model": HBM_MODEL_NOTE}
-    b = 10.0 * 4096.0 * act + 16.0 * pieces
+    dense = act - (stats_mean.get("sparse_items") or 0.0)  # a tile is one dense or one sparse item
+    b = 10.0 * 4096.0 * dense + 16.0 * pieces
     bt = 10.0 * T_mean + 16.0 * pieces if T_mean else None
     rate = lambda x: x / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS  # noqa: E731
     return {"frac_hbm_model": rate(b), "hbm_model_bytes_per_launch": b,
@@ -1034,7 +1036,7 @@ def _run_c5(args, np, torch, synth, m, params, amin, dev, world):
         mean = lambda key: float(np.mean([st[key] for st in stats]))  # noqa: E731
         avg, roof = _profiled_roofline(m, lambda: [(integrate(k), m.frontiers()) for k in range(5)],
                                        mean("updates"), mean("touched"),
-                                       {k: mean(k) for k in ("active_tiles", "pieces")})
+                                       {k: mean(k) for k in ("active_tiles", "pieces", "sparse_items")})
         # PMC traffic of this sweep point (tools/pmc_passes.sh over
         # `bench.py --config C5 --sweep N`, workload "C5-N"), when measured
         # on these sources
@@ -1053,7 +1055,8 @@ def _run_c5(args, np, torch, synth, m, params, amin, dev, world):
                      "integrate_updates_per_s": mean("updates") / float(np.median(ti)),
                      "updates_per_batch": mean("updates"), "touched_cells_per_batch": mean("touched"),
                      "clusters": len(fr) if fr is not None else None,
-                     "stage_stats": {k: mean(k) for k in ("pieces", "active_tiles", "work_items", "heavy_tiles")},
+                     "stage_stats": {k: mean(k) for k in ("pieces", "active_tiles", "work_items", "heavy_tiles",
+                                                          "sparse_items")},
                      "frontier_tiles": fst["frontier_tiles"], "frontier_slots": fst["frontier_slots"],
                      "kernel_avg_ms": avg, "roofline": roof})
         if N == sweep[-1] and args.cpu_seconds > 0:

@@ -871,7 +871,8 @@ int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out) {
                                dm_shard_sum(g->h_sh, SH_TH), pieces,
                                ic[CNT_ACTIVE],               items,
                                ic[CNT_HEAVY],                g->h_cnt[CNT_FL0],
-                               dm_shard_sum(fs, SH_SLOT),    g->h_cnt[CNT_CLUSTERS]};
+                               dm_shard_sum(fs, SH_SLOT),    g->h_cnt[CNT_CLUSTERS],
+                               ic[CNT_SITEMS]};
   for (int32_t i = 0; i < cap && i < kNStats; ++i) out[i] = v[i];
   if (n_out) *n_out = kNStats;
   return DM_OK;

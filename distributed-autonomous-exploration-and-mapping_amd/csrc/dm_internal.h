@@ -92,7 +92,8 @@ enum { SH_U = 0, SH_T = 1, SH_TH = 2, SH_ACT = 3 };
 enum { SH_SLOT = 0, SH_RUNS = 1, SH_FTF = 2, SH_BIG = 3 };
 
 // dm_last_stats entries (include/dm.h)
-constexpr int kNStats = 10;
+constexpr int kNStats = 11;
+constexpr bool dm_stat_is_frontier(int i) { return i >= 7 && i <= 9; }  // the others: integrate
 
 // Readback header in front of the sorted cluster records (device out_clu and
 // pinned h_out both point kRbRecords records into their allocation): the

@@ -593,7 +593,9 @@ int dm_sh_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out) {
     uint64_t v[kNStats] = {0};
     int32_t n = 0;
     if (int rc = dm_last_stats(s->band[(size_t)r], v, kNStats, &n)) return rc;
-    for (int i = s->active[(size_t)r] ? 0 : 7; i < kNStats; ++i) sum[i] += v[i];
+    // a band without scans in the last call contributes its frontier stats only
+    for (int i = 0; i < kNStats; ++i)
+      if (s->active[(size_t)r] || dm_stat_is_frontier(i)) sum[i] += v[i];
   }
   for (int32_t i = 0; i < cap && i < kNStats; ++i) out[i] = sum[i];
   if (n_out) *n_out = kNStats;

@@ -180,7 +180,7 @@ class OccupancyMapper:
         return int(U.value), int(T.value)
 
     STAT_NAMES = ("updates", "touched", "touched_heavy", "pieces", "active_tiles", "work_items",
-                  "heavy_tiles", "frontier_tiles", "frontier_slots", "frontier_clusters")
+                  "heavy_tiles", "frontier_tiles", "frontier_slots", "frontier_clusters", "sparse_items")
 
     def last_stats(self) -> dict:
         """Diagnostics of the most recent integrate call (dm_last_stats)."""

@@ -152,7 +152,11 @@ int dm_last_counts(dm_grid* g, uint64_t* updates, uint64_t* touched);
 /* Diagnostics of the most recent calls (synchronises the stream):
  * out[0..6] = integrate: U, T, T applied by the heavy-tile pass, pieces (ray
  * pieces binned by tile), active tiles, apply work items, heavy tiles;
- * out[7..9] = frontiers: tiles visited, tile-local components, clusters. */
+ * out[7..9] = frontiers: tiles visited, tile-local components, clusters;
+ * out[10] = integrate: sparse work items (light tiles with at most 15
+ * pieces, which load only the cells they touch; counted in out[5] too).
+ * *n_out = the number of entries the library has (11); a caller's smaller
+ * cap gets the first cap of them. */
 int dm_last_stats(dm_grid* g, uint64_t* out, int32_t cap, int32_t* n_out);
 
 /* OccupancyGrid.data for the band: int8[band_rows*width] (-1 / 0 / 100). */

@@ -64,3 +64,25 @@ def test_edge_modes_on_band_handles(oracle_lib, monkeypatch, kernel):
         for poses, ranges in batches:
             assert sh.integrate(poses, ranges, amin, inc) == om.integrate(poses, ranges, amin, inc)
         assert_frontiers_equal(sh.frontiers(want_mask=True, want_labels=True), *om.frontiers())
+
+
+def test_sparse_item_stat(oracle_lib):
+    """dm_last_stats out[10]: the call's sparse work items (light tiles with at
+    most 15 pieces) -- a 12-beam scan set on a 1 cm map is almost all sparse
+    tiles, a dense fan has few; never more than the active tiles (a tile is
+    one item of one kind) and counted in the work items too.  The map itself
+    stays bit-exact."""
+    p, batches, amin, inc = cases.world_case(75, 1200, 1000, 0.01, 8, 12, 2, region_frac=0.8)
+    om = oracle_lib.OracleMap(p)
+    with dm.OccupancyMapper(p) as m:
+        for poses, ranges in batches:
+            assert m.integrate(poses, ranges, amin, inc) == om.integrate(poses, ranges, amin, inc)
+        st = m.last_stats()
+        assert 0 < st["sparse_items"] <= st["active_tiles"] <= st["work_items"]
+        assert st["sparse_items"] >= st["active_tiles"] // 2
+        assert_map_equal(m, om)
+    p, batches, amin, inc = cases.world_case(76, 800, 800, 0.05, 4, 4096, 1, region_frac=0.5)
+    with dm.OccupancyMapper(p) as m:
+        m.integrate(*batches[0], amin, inc)
+        st = m.last_stats()
+        assert st["sparse_items"] < st["active_tiles"] <= st["work_items"]
