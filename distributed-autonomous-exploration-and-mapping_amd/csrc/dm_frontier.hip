@@ -1082,36 +1082,50 @@ __global__ __launch_bounds__(kFW * 64, DM_FL_OCC) void k_frontier_tile(
 // a returning hand-off atomic and the neighbour's border loads (C3: 35 % of
 // k_frontier_tile_big's workgroup time, profiles/r06_phase_c3.log); here
 // they are thousands of short independent waves.
+#ifndef DM_EDGE_WAVES
+#define DM_EDGE_WAVES 1  // waves per listed tile in k_frontier_edges (2: one per relation, A/B)
+#endif
 __global__ __launch_bounds__(kFW * 64) void k_frontier_edges(FGeom g, const int32_t* __restrict__ ftiles,
                                                              const unsigned long long* __restrict__ list_n,
                                                              const int32_t* __restrict__ border,
                                                              const unsigned long long* __restrict__ rel,
                                                              int32_t* slot_parent, unsigned long long* cnt) {
+  constexpr int kRel = DM_EDGE_WAVES == 2 ? 1 : 2;  // relations per wave
   const unsigned long long stamp = cnt[CNT_STAMP];
   const int w = threadIdx.x >> 6, lane = __lane_id();
   const int64_t nft = (int64_t)*list_n;
   unsigned long long* uflag = &cnt[CNT_OVERFLOW];
-  __shared__ int2 s_pairs[kFW][4 * 64];  // a wave's pairs (<= 3 per lane + a corner)
-  // two waves per listed tile: wave 2j + 0 its right edge (and both lower
-  // corners, on lanes 0 / 63), wave 2j + 1 its lower edge
-  for (int64_t v = (int64_t)blockIdx.x * kFW + w; v < 2 * nft; v += (int64_t)gridDim.x * kFW) {
-    const int64_t tile = __builtin_amdgcn_readfirstlane(ftiles[v >> 1]);
-    const int rel_kind = (int)(v & 1);  // 0 right edge + corners, 1 lower edge
+  const unsigned long long* est = rel + 4 * g.NT;  // the per-edge stamps (EDGE tile kernels)
+  __shared__ int2 s_pairs[kFW][kRel * 4 * 64];  // a wave's pairs (<= 3 per lane + a corner, per relation)
+  // relation 0: the tile's right edge (and both lower corners, on lanes 0 /
+  // 63); relation 1: its lower edge.  One wave per listed tile takes both
+  // (DM_EDGE_WAVES 1), or wave 2j + r relation r of tile j (2)
+  const int64_t nv = DM_EDGE_WAVES == 2 ? 2 * nft : nft;
+  for (int64_t v = (int64_t)blockIdx.x * kFW + w; v < nv; v += (int64_t)gridDim.x * kFW) {
+    const int64_t tile = __builtin_amdgcn_readfirstlane(ftiles[DM_EDGE_WAVES == 2 ? v >> 1 : v]);
     const int32_t tx = (int32_t)(tile % g.TX), ty = (int32_t)(tile / g.TX);
     const bool right = tx + 1 < g.TX, down = ty + 1 < g.TY, left = tx > 0;
     // everything in ONE round of loads after the tile id: the stamps that
     // say which records are this pass's, and the records themselves
     // (speculative: a record of an earlier pass is read but not used)
-    const int64_t nb = rel_kind == 0 ? (right ? tile + 1 : tile) : (down ? tile + g.TX : tile);
-    const int my_side = rel_kind == 0 ? 3 : 1, nb_side = rel_kind == 0 ? 2 : 0;
-    const unsigned long long* est = rel + 4 * g.NT;  // the per-edge stamps (EDGE tile kernels)
-    const unsigned long long m_me = est[4 * tile + my_side];
-    const unsigned long long m_nb = est[4 * nb + nb_side];
-    const int32_t sl = border[tile * 256 + my_side * 64 + lane];
-    const int32_t v_nb = border[nb * 256 + nb_side * 64 + lane];
-    // corners (rel_kind 0, lanes 0 / 63): this tile's (63, 0) / (63, 63)
+    unsigned long long m_me[kRel], m_nb[kRel];
+    int32_t sl[kRel], v_nb[kRel];
+    bool has_nb[kRel];
+#pragma unroll
+    for (int q = 0; q < kRel; ++q) {
+      const int rk = DM_EDGE_WAVES == 2 ? (int)(v & 1) : q;
+      const int64_t nb = rk == 0 ? (right ? tile + 1 : tile) : (down ? tile + g.TX : tile);
+      const int my_side = rk == 0 ? 3 : 1, nb_side = rk == 0 ? 2 : 0;
+      has_nb[q] = rk == 0 ? right : down;
+      m_me[q] = est[4 * tile + my_side];
+      m_nb[q] = est[4 * nb + nb_side];
+      sl[q] = border[tile * 256 + my_side * 64 + lane];
+      v_nb[q] = border[nb * 256 + nb_side * 64 + lane];
+    }
+    // corners (with relation 0, lanes 0 / 63): this tile's (63, 0) / (63, 63)
     // against the lower-left tile's (0, 63) / the lower-right tile's (0, 0)
-    const bool corner_lane = rel_kind == 0 && down && ((lane == 0 && left) || (lane == 63 && right));
+    const bool rel0 = DM_EDGE_WAVES == 2 ? (v & 1) == 0 : true;
+    const bool corner_lane = rel0 && down && ((lane == 0 && left) || (lane == 63 && right));
     const int64_t dn = lane == 0 ? tile + g.TX - 1 : tile + g.TX + 1;
     unsigned long long m_row = 0ull, m_dn = 0ull;
     int32_t c_me = -1, c_dn = -1;
@@ -1121,55 +1135,56 @@ __global__ __launch_bounds__(kFW * 64) void k_frontier_edges(FGeom g, const int3
       c_me = border[tile * 256 + 64 + lane];
       c_dn = border[dn * 256 + (lane == 0 ? 63 : 0)];
     }
-    const bool has_nb = rel_kind == 0 ? right : down;
-    // this lane's distinct pairs (cell pos against the neighbour's pos-1,
+    // each lane's distinct pairs (cell pos against the neighbour's pos-1,
     // pos, pos+1, minus those the previous lane issues), compacted into the
-    // wave's list so each lane then runs ONE union instead of up to three in
-    // turn
-    int32_t sb[3] = {-1, -1, -1};
-    bool keep[4] = {false, false, false, false};
-    if (has_nb && m_me == stamp && m_nb == stamp) {  // uniform
-      sb[0] = __shfl_up(v_nb, 1);
-      sb[1] = v_nb;
-      sb[2] = __shfl_down(v_nb, 1);
-      if (lane == 0) sb[0] = -1;
-      if (lane == 63) sb[2] = -1;
-      const int32_t psl = __shfl_up(sl, 1);
-      int32_t psb[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) psb[q] = __shfl_up(sb[q], 1);
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int32_t b = sb[q];
-        bool dup = sl < 0 || b < 0;
-#pragma unroll
-        for (int r = 0; r < q; ++r) dup |= sb[r] == b;
-        if (lane > 0 && psl == sl) dup |= (psb[0] == b) | (psb[1] == b) | (psb[2] == b);
-        keep[q] = !dup;
-      }
-    }
-    keep[3] = corner_lane && m_row == stamp && m_dn == stamp && c_me >= 0 && c_dn >= 0;
-    const int np = (int)keep[0] + (int)keep[1] + (int)keep[2] + (int)keep[3];
-    int incl = np;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int t = __shfl_up(incl, d);
-      if (lane >= d) incl += t;
-    }
-    const int total = __shfl(incl, 63);
-    if (total == 0) continue;
+    // wave's list, so each lane then runs ONE union at a time instead of up
+    // to three (or six) in turn
     int2* lst = s_pairs[w];
-    {
-      int at = incl - np;
+    int total = 0;
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
-        if (keep[q]) lst[at++] = make_int2(sl, sb[q]);
-      if (keep[3]) lst[at] = make_int2(c_me, c_dn);
+    for (int q = 0; q < kRel; ++q) {
+      int32_t sb[3] = {-1, -1, -1};
+      bool keep[3] = {false, false, false};
+      if (has_nb[q] && m_me[q] == stamp && m_nb[q] == stamp) {  // uniform
+        sb[0] = __shfl_up(v_nb[q], 1);
+        sb[1] = v_nb[q];
+        sb[2] = __shfl_down(v_nb[q], 1);
+        if (lane == 0) sb[0] = -1;
+        if (lane == 63) sb[2] = -1;
+        const int32_t psl = __shfl_up(sl[q], 1);
+        int32_t psb[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) psb[k] = __shfl_up(sb[k], 1);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int32_t b = sb[k];
+          bool dup = sl[q] < 0 || b < 0;
+#pragma unroll
+          for (int r = 0; r < k; ++r) dup |= sb[r] == b;
+          if (lane > 0 && psl == sl[q]) dup |= (psb[0] == b) | (psb[1] == b) | (psb[2] == b);
+          keep[k] = !dup;
+        }
+      }
+      const bool kc = q == 0 && corner_lane && m_row == stamp && m_dn == stamp && c_me >= 0 && c_dn >= 0;
+      const int np = (int)keep[0] + (int)keep[1] + (int)keep[2] + (int)kc;
+      int incl = np;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
+      }
+      int at = total + incl - np;
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        if (keep[k]) lst[at++] = make_int2(sl[q], sb[k]);
+      if (kc) lst[at] = make_int2(c_me, c_dn);
+      total += __shfl(incl, 63);
     }
+    if (total == 0) continue;
     wave_lds_sync();
     for (int i = lane; i < total; i += 64) {
-      const int2 q = lst[i];
-      EDGE_UNITE(slot_parent, q.x, q.y, uflag, kOvUnionFind);
+      const int2 pr = lst[i];
+      EDGE_UNITE(slot_parent, pr.x, pr.y, uflag, kOvUnionFind);
     }
     wave_lds_sync();
   }
@@ -1941,8 +1956,8 @@ int dm_enqueue_frontiers(dm_grid* g, bool want_mask, bool want_labels, bool spli
   }
   if (edge) {
     dm_timer_begin(g, "frontier_edges", &t, ps);
-    // two waves per listed tile (the kernel grid-strides)
-    DM_LAUNCH(k_frontier_edges, dim3(grid_for(2 * std::min<int64_t>(want_waves, g->NT), kFW, 16384)),
+    // DM_EDGE_WAVES waves per listed tile (the kernel grid-strides)
+    DM_LAUNCH(k_frontier_edges, dim3(grid_for(DM_EDGE_WAVES * std::min<int64_t>(want_waves, g->NT), kFW, 16384)),
               dim3(kFW * 64), 0, ps, fg, g->ftiles, list_n, g->border, g->rel,
               g->slot_parent, g->cnt);
     dm_timer_end(g, &t);
