@@ -791,7 +791,9 @@ HBM_MODEL_NOTE = ("bytes k_tile_accum moves from HBM by the design: 10 B per cel
                   "their touched 4-cell groups, at most 40 B per touched cell, which frac_hbm_touched "
                   "(10 B per touched cell + pieces) bounds from below. The hit / miss counts (the 8*U of "
                   "`frac`) stay in LDS and are in neither, so frac (the SURVEY.md §8(d) model) reads ~2x "
-                  "(C3) to ~3x+ (C5-4096) above the bytes moved; frac_traffic (PMC) is the measured figure")
+                  "(C3) to ~3x+ (C5-4096) above the bytes moved; frac_traffic (PMC) is the measured figure. "
+                  "When more than half the active tiles are sparse items (C5 12-768 beams) their scattered "
+                  "4-cell groups move whole lines that neither model counts, and frac_hbm_model is null")
 
 
 def hbm_model(stats_mean, t_ms, T_mean=None):
@@ -802,12 +804,17 @@ def hbm_model(stats_mean, t_ms, T_mean=None):
     if not act or not t_ms or t_ms <= 0:
         return {"frac_hbm_model": None, "hbm_model_bytes_per_launch": None, "frac_hbm_touched": None,
                 "hbm_model": HBM_MODEL_NOTE}
-    dense = act - (stats_mean.get("sparse_items") or 0.0)  # a tile is one dense or one sparse item
+    sparse = stats_mean.get("sparse_items") or 0.0
+    dense = act - sparse  # a tile is one dense or one sparse item
     b = 10.0 * 4096.0 * dense + 16.0 * pieces
     bt = 10.0 * T_mean + 16.0 * pieces if T_mean else None
     rate = lambda x: x / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS  # noqa: E731
-    return {"frac_hbm_model": rate(b), "hbm_model_bytes_per_launch": b,
-            "frac_hbm_touched": rate(bt) if bt else None, "hbm_model": HBM_MODEL_NOTE}
+    # a call whose tiles are mostly sparse items moves line-granular bytes of
+    # scattered 4-cell groups that neither model counts: no model fraction
+    applies = sparse <= 0.5 * act
+    return {"frac_hbm_model": rate(b) if applies else None, "hbm_model_bytes_per_launch": b if applies else None,
+            "frac_hbm_touched": rate(bt) if bt else None, "hbm_model_applies": applies,
+            "hbm_model": HBM_MODEL_NOTE}
 
 
 def _profiled_roofline(band, run, U_mean, T_mean, stats_mean=None):

@@ -220,7 +220,9 @@ class ShardedMapper:
             raise ValueError(f"records_comm must be 'shared' or 'separate', not {records_comm!r}")
         self.records_comm = records_comm
         self.timing = False  # set_timing(): HIP-event times of the exchange phases
-        self._tev = collections.deque()  # (halo start, halo end, gather start, gather end) per pass
+        # (halo start, halo end, gather start, gather end) per timed pass; the
+        # most recent 4096 are kept (a mapper left timing does not grow)
+        self._tev = collections.deque(maxlen=4096)
         self._pending = collections.deque()  # frontiers_begin() passes in flight, oldest first
         try:
             self.max_in_flight = int(load_library().dm_max_passes_in_flight())
