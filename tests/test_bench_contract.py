@@ -96,3 +96,25 @@ def test_bench_parser_knows_every_config():
     assert out.returncode == 0, out.stderr
     for cfg in ("C1", "C2", "C3", "C4", "C5"):
         assert cfg in out.stdout
+
+
+def test_r06_headline_fields():
+    """Round 6's final C3 line: the measured traffic and the design's own byte
+    model beside the SURVEY model's `frac`, and the two agree."""
+    d = _load("r06_final_bench.json")
+    r = d["roofline"]
+    assert r["traffic"] and r["frac_traffic"] and r["frac_hbm_model"]
+    assert r["frac_hbm_model"] < r["frac"]  # the SURVEY model counts LDS-resident counter bytes
+    assert abs(r["frac_hbm_model"] - r["frac_traffic"]) < 0.1 * r["frac_traffic"]
+    assert d["value"] >= 1e10 and d["frontier_ms"] < 2.0 and d["value_host_inputs"] >= 1e10
+
+
+def test_hbm_model_applies_only_where_dense_items_dominate():
+    sys.path.insert(0, REPO)
+    import bench
+
+    dense = bench.hbm_model({"active_tiles": 3000.0, "pieces": 600000.0, "sparse_items": 10.0}, 0.048, 5e6)
+    assert dense["hbm_model_applies"] and 0 < dense["frac_hbm_model"] < 1
+    sparse = bench.hbm_model({"active_tiles": 20000.0, "pieces": 45000.0, "sparse_items": 19000.0}, 0.09, 1e6)
+    assert not sparse["hbm_model_applies"] and sparse["frac_hbm_model"] is None
+    assert sparse["frac_hbm_touched"] > 0
