@@ -17,10 +17,14 @@
 //                   kernel that reads the map), plus the pass's resets
 //   k_frontier_tile(_big)  per listed tile: runs, LDS union-find (atomicMin
 //                   hooking, root = min index), per-component sums, one slot
-//                   per tile-local component; then the unions across its
-//                   edges with the neighbour tiles that finished before it
-//                   (the later tile of each edge unites: a stamped hand-off
-//                   word per tile pair), lock-free CAS union-find keyed by slot
+//                   per tile-local component; then, in dense passes, the
+//                   unions across its edges with the neighbour tiles that
+//                   finished before it (the later tile of each edge unites: a
+//                   stamped hand-off word per tile pair), lock-free CAS
+//                   union-find keyed by slot; in sparse passes it only
+//                   publishes its edges
+//   k_frontier_edges (sparse passes) the unions across every tile edge and
+//                   corner, after the tile kernels
 //   k_frontier_resolve / k_frontier_compact  roots, int64 sums and the min
 //                   label of each merged set, cluster list
 //   k_rank_sort / row sort  records by label, centroids, readback
