@@ -83,3 +83,32 @@ def test_gpu_ld06_stream_into_map(oracle_lib):
         np.testing.assert_array_equal(np.isnan(r), np.isnan(er))
         assert m.integrate(poses, r, 0.0, inc) == om.integrate(poses, er, 0.0, inc)
         np.testing.assert_array_equal(m.state(), om.state)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("direction", [True, False])
+def test_gpu_ld06_edge_angles_and_sizes(oracle_lib, direction):
+    """Angles at and past the scan's ends (a hair below 0, 0, 359.999, 360,
+    past 360, +-1e30, +-inf, NaN: out-of-range ones are dropped, as the
+    driver's idx >= N / idx < 0 test does), the largest distance, zero
+    distance with and without intensity, empty first and last revolutions,
+    and the smallest and largest beam counts the boundary accepts."""
+    import dm
+
+    ang = np.float32([-0.001, 0.0, 0.0, 359.999, 360.0, 360.001, 1e30, -1e30, np.inf, -np.inf, np.nan, 180.0, 180.0])
+    pts = np.zeros(ang.size, dtype=np.dtype(LD06_POINT_DTYPE))
+    pts["angle_deg"] = ang
+    pts["distance_mm"] = [5, 65535, 0, 12000, 1, 7, 9, 9, 9, 9, 9, 0, 3]
+    pts["intensity"] = [1, 2, 0, 4, 5, 6, 7, 7, 7, 7, 7, 9, 0]
+    segs = [pts[:0], pts, random_points(20, 500, collide=True), pts[::-1].copy(), pts[:0]]
+    allp = np.concatenate(segs)
+    off = np.cumsum([0] + [len(s) for s in segs]).astype(np.int64)
+    with dm.OccupancyMapper(dm.default_params(64, 64)) as m:
+        for N in (2, 3, 360, 8192):
+            r, i = m.ld06_to_scans(allp, off, N, direction, want_intensities=True)
+            er, ei = oracle_lib.ld06_to_scans(allp, off, N, direction)
+            np.testing.assert_array_equal(np.isnan(r), np.isnan(er))
+            np.testing.assert_array_equal(np.nan_to_num(r).view(np.uint32), np.nan_to_num(er).view(np.uint32))
+            np.testing.assert_array_equal(np.isnan(i), np.isnan(ei))
+            np.testing.assert_array_equal(np.nan_to_num(i), np.nan_to_num(ei))
+            assert np.isnan(r[0]).all() and np.isnan(r[-1]).all()  # the empty revolutions
