@@ -433,3 +433,41 @@ def test_sparse_items_threshold(oracle_lib, monkeypatch, sparse):
             assert_map_equal(m, om)
             fr = m.frontiers(want_mask=True, want_labels=True)
             assert_frontiers_equal(fr, *om.frontiers())
+
+
+def test_geometry_edge_cases(oracle_lib):
+    """Ray geometry at its degenerate points, bit-exact against the oracle:
+    beams along the axes and the diagonals (yaw multiples of pi/4: Bresenham's
+    ties), sensors on cell corners with ranges that end exactly on cell
+    boundaries, negative / -inf / subnormal ranges (skipped as too short),
+    sensors far outside the map whose rays cross it or miss it, and sensors
+    on the map's last row / column."""
+    res = np.float32(0.05)
+    p = cases.make_params(160, 96, resolution=float(res), origin=(-4.0, -2.4))
+    om = oracle_lib.OracleMap(p)
+    with dm.OccupancyMapper(p) as m:
+        def both(poses, ranges, amin, inc):
+            poses = np.asarray(poses, np.float64)
+            ranges = np.asarray(ranges, np.float32)
+            assert m.integrate(poses, ranges, amin, inc) == om.integrate(poses, ranges, amin, inc)
+
+        # eight beams at yaw + k * pi/4 from cell corners, lengths on cell boundaries
+        corners = [[0.0, 0.0, 0.0], [0.05, -0.05, 0.0], [1.0, 1.0, np.pi / 2], [-2.0, 0.5, np.pi]]
+        lens = np.float32([0.05, 0.1, 0.25, 1.0, 1.5, 2.0, 0.5, 3.0])
+        both(corners, np.tile(lens, (4, 1)), 0.0, float(np.float32(np.pi / 4)))
+        # the same from cell centres, and just off the corners
+        both([[0.025, 0.025, 0.0], [1e-9, -1e-9, 0.0]], np.tile(lens, (2, 1)), 0.0, float(np.float32(np.pi / 4)))
+        # negative, -inf, subnormal and zero ranges among valid ones
+        bad = np.float32([-1.0, -np.inf, 1e-40, 0.0, 2.0, -0.0, 0.0199, 0.02])
+        both([[0.3, 0.2, 0.1]], bad[None, :], 0.0, 0.7)
+        # sensors far outside the map: rays crossing it, ending inside it, missing it
+        far = [[-9.0, 0.0, 0.0], [0.0, -7.5, np.pi / 2], [9.5, 3.0, np.pi], [-9.0, -9.0, np.pi / 4]]
+        rr = np.float32([[12.0, 6.0, 11.9, 3.0]] * 4)
+        both(far, rr, -0.05, 0.05)
+        # sensors on the last row / column and on the map's corner cells
+        W, H = 160 * res, 96 * res
+        edge = [[-4.0 + W - 0.01, 0.0, 0.3], [0.0, -2.4 + H - 0.01, -1.2], [-3.99, -2.39, 0.8],
+                [-4.0 + W - 0.01, -2.4 + H - 0.01, 3.5]]
+        both(edge, np.full((4, 90), 2.5, np.float32), -np.pi, float(np.float32(2 * np.pi / 90)))
+        assert_map_equal(m, om)
+        assert_frontiers_equal(m.frontiers(want_mask=True, want_labels=True), *om.frontiers())
