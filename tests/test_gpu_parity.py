@@ -471,3 +471,44 @@ def test_geometry_edge_cases(oracle_lib):
         both(edge, np.full((4, 90), 2.5, np.float32), -np.pi, float(np.float32(2 * np.pi / 90)))
         assert_map_equal(m, om)
         assert_frontiers_equal(m.frontiers(want_mask=True, want_labels=True), *om.frontiers())
+
+
+def spiral_state(n, gap=2):
+    """A one-cell-wide free spiral in unknown space, `gap` cells between its
+    turns: every free cell is a frontier cell and the whole spiral is ONE
+    8-connected component that winds through every tile many times, the
+    longest tile-to-tile union chains a map of this size can hold."""
+    st = np.full((n, n), -1, np.int8)
+    lo, hi = 0, n - 1
+    y = x = 0
+    while lo <= hi:
+        st[lo, lo:hi + 1] = 0                      # top row, left to right
+        st[lo:hi + 1, hi] = 0                      # right column, down
+        if hi - lo <= gap:
+            break
+        st[hi, lo + gap - 1:hi + 1] = 0            # bottom row, right to left
+        st[lo + gap:hi + 1, lo + gap - 1] = 0      # left column, up (stops short of the top row)
+        lo += gap
+        hi -= gap
+        st[lo, lo - 1:lo + 1] = 0                  # step into the next turn
+    return st
+
+
+@pytest.mark.parametrize("n", [300, 1536])
+def test_frontiers_on_spiral(oracle_lib, n):
+    import time
+
+    st = spiral_state(n)
+    p = cases.make_params(n, n)
+    om = oracle_lib.OracleMap(p)
+    om.state[...] = st
+    expect = om.frontiers()
+    with dm.OccupancyMapper(p) as m:
+        m.set_state(st)
+        m.frontiers()  # first pass: lists, grids, hints
+        t0 = time.perf_counter()
+        fr = m.frontiers(want_mask=True, want_labels=True)
+        dt = time.perf_counter() - t0
+        assert_frontiers_equal(fr, *expect)
+    assert len(expect[2]) >= 1
+    assert dt < 0.5, f"spiral frontier pass took {dt:.3f} s"
