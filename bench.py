@@ -51,8 +51,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="budget for the CPU-oracle baseline sample (0 disables)")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--depth", type=int, default=2,
-                    help="frontier passes in flight in the pipelined steps (1 or 2; libdm keeps 2 readback slots)")
+    ap.add_argument("--depth", type=int, default=None,
+                    help="frontier passes in flight in the pipelined steps (1 or 2; libdm keeps 2 readback "
+                         "slots); default 2, and 1 for the one-scan replays C1 / C2 (depth 2 measured no "
+                         "faster there and less steady: profiles/r06_depth_ab.log)")
     ap.add_argument("--order", default="eb", choices=["eb", "be"],
                     help="host order per pipelined step after integrate(k): 'eb' collects pass "
                          "k-depth then starts pass k; 'be' starts pass k then collects pass "
@@ -82,7 +84,10 @@ def parse():
                     help="skip the PCIe-inclusive measurement (value_host_inputs)")
     ap.add_argument("--step-trace", default=None,
                     help="C3 / C4: write every timed step's host start-to-start time (us) to this JSON file")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.depth is None:
+        args.depth = 1 if args.config in ("C1", "C2") else 2
+    return args
 
 
 def _free_port() -> int:
@@ -838,25 +843,25 @@ def _profiled_roofline(band, run, U_mean, T_mean, stats_mean=None):
     }
 
 
-def _pipelined(mapper, integrate, ks):
-    """integrate(k) + frontier pass per k, step k's pass collected after step
-    k+1's integrate was enqueued (as the C3 bench)."""
+def _pipelined(mapper, integrate, ks, depth=2):
+    """integrate(k) + frontier pass per k, as the C3 bench's run_steps: up to
+    `depth` passes in flight, pass k collected after batch k + depth was
+    enqueued (depth 1: after batch k + 1), then the passes still in flight.
+    Returns the last pass's frontiers."""
+    ks = list(ks)
+    if not ks:
+        return None
+    depth = max(1, min(depth, len(ks)))
     fr = None
-
-    def end():
-        r = mapper.frontiers_end()
-        return r if r is not None else mapper.frontiers()
-
-    first = True
-    for k in ks:
+    for i, k in enumerate(ks):
         integrate(k)
-        if not first:
-            fr = end()
+        if i >= depth:
+            mapper.frontiers_end()
         mapper.frontiers_begin()
-        first = False
-    if not first:
-        fr = end()
-    return fr
+    for _ in range(depth):
+        fr = mapper.frontiers_end()
+    # None: the pass overflowed a capacity (grown now); rerun on this map
+    return fr if fr is not None else mapper.frontiers()
 
 
 def run_config(args):
@@ -927,11 +932,11 @@ def _run_replay(args, np, torch, synth, m, params, amin, dev):
         U += st["updates"]
         T += st["touched"]
     m.reset()
-    _pipelined(m, integrate, range(min(args.warmup * 20, n)))
+    _pipelined(m, integrate, range(min(args.warmup * 20, n)), args.depth)
     m.reset()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    fr = _pipelined(m, integrate, range(n))
+    fr = _pipelined(m, integrate, range(n), args.depth)
     m.synchronize()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -993,7 +998,7 @@ def _run_replay(args, np, torch, synth, m, params, amin, dev):
         "updates_total": U, "touched_total": T,
         "integrate_ms": float(np.median(ti)) * 1e3, "frontier_ms": float(np.median(tf)) * 1e3,
         "clusters": len(fr) if fr is not None else None, "kernel_avg_ms": avg, "roofline": roof,
-        "pipelined": "scan k+1's integrate front-end overlaps scan k's frontier pass",
+        "pipelined": f"scan k+1's integrate front-end overlaps scan k's frontier pass, {args.depth} passes in flight",
         "cpu_baseline": cpu, "gen_seconds": t_gen,
     }
 
@@ -1022,10 +1027,10 @@ def _run_c5(args, np, torch, synth, m, params, amin, dev, world):
             integrate(k)
             stats.append(m.last_stats())
         m.reset()
-        _pipelined(m, integrate, range(args.warmup))
+        _pipelined(m, integrate, range(args.warmup), args.depth)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        fr = _pipelined(m, integrate, range(args.warmup, args.warmup + args.steps))
+        fr = _pipelined(m, integrate, range(args.warmup, args.warmup + args.steps), args.depth)
         m.synchronize()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
@@ -1098,7 +1103,7 @@ def _run_c5(args, np, torch, synth, m, params, amin, dev, world):
                    "grid": [65536, 65536], "resolution_m": 0.01, "scans_per_batch": S,
                    "beams_per_scan": sweep, "parallelism": "single GPU"},
         "frontier_ms": head["frontier_ms"], "roofline": head["roofline"], "sweep": rows,
-        "pipelined": "step k+1's integrate front-end overlaps step k's frontier pass",
+        "pipelined": f"step k+1's integrate front-end overlaps step k's frontier pass, {args.depth} passes in flight",
         "cpu_baseline": cpu,
     }
 

@@ -1,6 +1,7 @@
 #!/bin/bash
 # libdm variant A/B over the C5 beam-density sweep (GPU box, repo root):
-#   bash tools/c5_ab.sh ROUNDS SWEEP tag1 tag2 ...   ("base" = dm/libdm.so, else dm/libdm_<tag>.so)
+#   bash tools/c5_ab.sh ROUNDS SWEEP spec ...
+#   spec = tag[@--arg,value,...]  ("base" = dm/libdm.so, else dm/libdm_<tag>.so; args go to bench.py)
 # One `bench.py --config C5 --sweep SWEEP` per tag per round, alternating;
 # prints ms per step, frontier pass and kernel times per sweep point -> gpurun_out/c5_ab.log
 set -o pipefail
@@ -9,14 +10,15 @@ OUT=gpurun_out/c5_ab.log
 R=$1; SW=$2; shift 2
 D=distributed-autonomous-exploration-and-mapping_amd/dm
 for r in $(seq $R); do
-  for t in "$@"; do
+  for spec in "$@"; do
+    t=${spec%%@*}; args=""; [ "$t" != "$spec" ] && args=${spec#*@}
     lib=$D/libdm_$t.so; [ $t = base ] && lib=$D/libdm.so
-    DM_LIB=$PWD/$lib timeout -k 10 300 python -u bench.py --config C5 --sweep $SW --cpu-seconds 0 \
-      > gpurun_out/c5_ab_tmp.log 2>&1 || { echo "C5 $t failed"; tail -5 gpurun_out/c5_ab_tmp.log; exit 1; }
+    DM_LIB=$PWD/$lib timeout -k 10 300 python -u bench.py --config C5 --sweep $SW --cpu-seconds 0 ${args//,/ } \
+      > gpurun_out/c5_ab_tmp.log 2>&1 || { echo "C5 $spec failed"; tail -5 gpurun_out/c5_ab_tmp.log; exit 1; }
     python -c "
 import json; d=json.loads(open('gpurun_out/c5_ab_tmp.log').read().strip().splitlines()[-1])
 for s in d['sweep']:
-    print('$t', 'beams', s['beams_per_scan'], 'ms/step', round(s['ms_per_step'], 3), 'fr', round(s['frontier_ms'], 3),
+    print('$spec', 'beams', s['beams_per_scan'], 'ms/step', round(s['ms_per_step'], 3), 'fr', round(s['frontier_ms'], 3),
           {k: round(v * 1e3, 1) for k, v in s['kernel_avg_ms'].items()})
 " | tee -a $OUT
   done
