@@ -1,6 +1,6 @@
 #!/bin/bash
 # libdm variant A/B over the scan-replay / shared-map configs (GPU box, repo
-# root): bash tools/cfg_ab.sh "C1 C4" spec ...  (spec = tag[@--arg,value,...]; "base" =
+# root): bash tools/cfg_ab.sh "C1 C4" spec ...  (spec = tag[:VAR=V,...][@--arg,value,...]; "base" =
 # dm/libdm.so, else dm/libdm_<tag>.so; args go to bench.py); prints ms per step and kernel
 # times -> gpurun_out/cfg_ab.log
 set -o pipefail
@@ -10,9 +10,10 @@ CFGS=$1; shift
 D=distributed-autonomous-exploration-and-mapping_amd/dm
 for c in $CFGS; do
   for spec in "$@"; do
-    t=${spec%%@*}; args=""; [ "$t" != "$spec" ] && args=${spec#*@}
+    head=${spec%%@*}; args=""; [ "$head" != "$spec" ] && args=${spec#*@}
+    t=${head%%:*}; envs=""; [ "$t" != "$head" ] && envs=${head#*:}
     lib=$D/libdm_$t.so; [ $t = base ] && lib=$D/libdm.so
-    DM_LIB=$PWD/$lib timeout -k 10 300 python -u bench.py --config $c --cpu-seconds 0 ${args//,/ } \
+    env ${envs//,/ } DM_LIB=$PWD/$lib timeout -k 10 300 python -u bench.py --config $c --cpu-seconds 0 ${args//,/ } \
       > gpurun_out/cfg_ab_tmp.log 2>&1 || { echo "$c $spec failed"; tail -5 gpurun_out/cfg_ab_tmp.log; exit 1; }
     python -c "
 import json; d=json.loads(open('gpurun_out/cfg_ab_tmp.log').read().strip().splitlines()[-1])
