@@ -55,6 +55,8 @@ def parse():
                     help="frontier passes in flight in the pipelined steps (1 or 2; libdm keeps 2 readback "
                          "slots); default 2, and 1 for the one-scan replays C1 / C2 (depth 2 measured no "
                          "faster there and less steady: profiles/r06_depth_ab.log)")
+    ap.add_argument("--pin-host", default="off", choices=["auto", "off"],
+                    help="auto: the host thread on the CPUs of the GPU's NUMA node (pin_host_near_gpu)")
     ap.add_argument("--order", default="eb", choices=["eb", "be"],
                     help="host order per pipelined step after integrate(k): 'eb' collects pass "
                          "k-depth then starts pass k; 'be' starts pass k then collects pass "
@@ -155,6 +157,7 @@ def main():
     if args.device_override is not None:
         local_rank = args.device_override
     torch.cuda.set_device(local_rank)
+    host_cpus = pin_host_near_gpu(torch, local_rank, args.pin_host)
     if world_size > 1:
         import datetime
 
@@ -559,6 +562,7 @@ def main():
                           f"(dm_set_overlap + dm_frontiers_begin/_end), {args.depth} passes in flight")
             if pipelined else None,
             "cpu_baseline": cpu,
+            "host_cpus": host_cpus,
             "gen_seconds": t_gen,
             # host-side start-to-start time of each timed step (rank 0): a
             # host stall shows here as a long tail, kernel time in `roofline`
@@ -763,6 +767,36 @@ def cpu_baseline_strong(params, pool, amin, inc, budget_s):
             "frontier_ms": t_fr * 1e3}
 
 
+def pin_host_near_gpu(torch, dev_i, mode):
+    """--pin-host auto: run this process's host thread (the one that launches,
+    polls and reads back) on the CPUs of the GPU's own NUMA node, from the
+    GPU's PCI address in sysfs, intersected with the CPUs the process may use.
+    The library's pinned host buffers (pose ring, readback) are allocated
+    after this, so they land in that node's memory too.  Unpinned, a process
+    on a two-socket box runs where the scheduler puts it: the GPU then reads
+    the mapped buffers and the host polls across the socket link.  Returns
+    what was done (for the JSON line)."""
+    if mode == "off":
+        return {"pinned": False, "why": "--pin-host off"}
+    try:
+        p = torch.cuda.get_device_properties(dev_i)
+        addr = f"{getattr(p, 'pci_domain_id', 0):04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        base = f"/sys/bus/pci/devices/{addr}"
+        text = open(base + "/local_cpulist").read().strip()
+        node = open(base + "/numa_node").read().strip()
+        local = set()
+        for part in text.split(","):
+            lo, _, hi = part.partition("-")
+            local.update(range(int(lo), int(hi or lo) + 1))
+        cpus = local & os.sched_getaffinity(0)
+        if not cpus:
+            return {"pinned": False, "why": f"no allowed CPU on the GPU's node {node}"}
+        os.sched_setaffinity(0, cpus)
+        return {"pinned": True, "gpu_pci": addr, "numa_node": int(node), "cpus": len(cpus)}
+    except (OSError, ValueError, AttributeError) as e:
+        return {"pinned": False, "why": f"{type(e).__name__}: {e}"}
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -872,6 +906,7 @@ def run_config(args):
         raise SystemExit(f"--config {args.config} is a single-GPU measurement")
     dev_i = args.device_override or 0
     torch.cuda.set_device(dev_i)
+    host_cpus = pin_host_near_gpu(torch, dev_i, args.pin_host)
     dev = torch.device("cuda", dev_i)
     import dm
     from dm import synth
@@ -895,7 +930,7 @@ def run_config(args):
             out = _run_c5(args, np, torch, synth, mapper, params, amin, dev, world)
     finally:
         mapper.close()
-    out = {**base, **out}
+    out = {**base, **out, "host_cpus": host_cpus}
     print(json.dumps(out), flush=True)
     return out
 
