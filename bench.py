@@ -53,9 +53,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--depth", type=int, default=None,
                     help="frontier passes in flight in the pipelined steps (1 or 2; libdm keeps 2 readback "
-                         "slots); default 2, and 1 for the one-scan replays C1 / C2 (depth 2 measured no "
+                         "slots); default 2, and 1 for the 400² one-scan replay C1 (depth 2 measured no "
                          "faster there and less steady: profiles/r06_depth_ab.log)")
-    ap.add_argument("--pin-host", default="off", choices=["auto", "off"],
+    ap.add_argument("--pin-host", default="auto", choices=["auto", "off"],
                     help="auto: the host thread on the CPUs of the GPU's NUMA node (pin_host_near_gpu)")
     ap.add_argument("--order", default="eb", choices=["eb", "be"],
                     help="host order per pipelined step after integrate(k): 'eb' collects pass "
@@ -88,7 +88,7 @@ def parse():
                     help="C3 / C4: write every timed step's host start-to-start time (us) to this JSON file")
     args = ap.parse_args()
     if args.depth is None:
-        args.depth = 1 if args.config in ("C1", "C2") else 2
+        args.depth = 1 if args.config == "C1" else 2
     return args
 
 
